@@ -1,0 +1,212 @@
+/*
+ * mantis.h — C-ABI of the MI355X-native mantis3 hot path (libmantis_amd.so).
+ *
+ * Drop-in boundary for the reference's per-frame callback and service:
+ *   void quadDetection(const sensor_msgs::ImageConstPtr&,
+ *                      const sensor_msgs::CameraInfoConstPtr&)   src/mantis3.cpp:68-135
+ *   srv/mantisService.srv:1-13 (Image[] image, CameraInfo[] camera_info,
+ *        Vector3 delta_pos, Quaternion delta_quat -> Pose pose, float64 weight,
+ *        int32 num_particles)                                    (server: src/mantis_server.cpp:23-30)
+ * Plain C types only (no ROS/OpenCV/torch types). Every entry point returns a
+ * mantis_status; mantis_last_error() describes the last failure on a context.
+ * The library never calls exit()/abort() (the reference does: RPP.cpp:450-453).
+ *
+ * Ownership: input buffers are borrowed for the call only; host inputs are
+ * staged through pinned memory. The context owns all device memory and its
+ * HIP stream. Threading: one context per host thread; calls on one context are
+ * serialized (matching the reference's single ros::spin thread,
+ * src/mantis3.cpp:155). State carried across frames (the reference's globals
+ * `cv::RNG rng(1)` Mantis3Params.h:87 and the map) lives in the context.
+ */
+#ifndef MANTIS_H
+#define MANTIS_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MANTIS_ABI_VERSION 1
+
+typedef enum mantis_status {
+  MANTIS_OK = 0,
+  MANTIS_ERR_ARG = 1,       /* bad argument (null pointer, size, channel count) */
+  MANTIS_ERR_DEVICE = 2,    /* HIP runtime / kernel failure, or no GPU */
+  MANTIS_ERR_OOM = 3,       /* device or pinned allocation failed */
+  MANTIS_ERR_CAPACITY = 4,  /* a fixed-capacity workspace overflowed (see last_error) */
+  MANTIS_ERR_STATE = 5,     /* map not set, comm not initialised, ... */
+  MANTIS_ERR_COMM = 6       /* RCCL failure */
+} mantis_status;
+
+/* Per-frame outcome (reference early returns / gates, src/mantis3.cpp:82-132). */
+typedef enum mantis_reason {
+  MANTIS_PUBLISHED = 0,      /* yaw gap > MINIMUM_YAW_DIFFERENCE, pose published (PosePub.h:16) */
+  MANTIS_NO_QUADS = 1,       /* "no quadrilaterlals detected!" early return (mantis3.cpp:82-84) */
+  MANTIS_NO_HYPS = 2,        /* empty cluster (mantis3.cpp:94-97) */
+  MANTIS_YAW_AMBIGUOUS = 3,  /* pose computed but gate not met: not published */
+  MANTIS_NO_YAW = 4          /* every yaw set scored DBL_MAX (reference UB) */
+} mantis_reason;
+
+typedef struct mantis_config {
+  int32_t struct_size;          /* sizeof(mantis_config) */
+  int32_t device;               /* HIP device ordinal */
+  int32_t max_cams;             /* camera-frames per mantis_process_batch call */
+  int32_t max_width, max_height;
+  uint64_t rng_seed;            /* cv::RNG seed, 1 in the reference (Mantis3Params.h:87) */
+  int32_t canny_low;            /* ~canny_hysteresis, 50 (Mantis3Params.h:162); high = 3x */
+  int32_t polygon_epsilon;      /* ~polygon_epsilon, 10 (:164) */
+  double search_radius_multiplier; /* ~neighborhood_search_radius_multiplier, 0.1 (:166) */
+  double grid_spacing;          /* ~grid_spacing, 0.32 (:167) */
+  int32_t particles, iterations;/* 50, 10 (PoseAdjustment.h:29) */
+  int32_t gn_enable;            /* 0 = reference-parity mode (no GN refinement) */
+  int32_t gn_iterations;        /* rig GN iterations (<= 10) */
+  int32_t max_quads;            /* per-frame quad capacity (default 256) */
+  int32_t max_contour_points;   /* per-frame contour point pool (default 262144) */
+} mantis_config;
+
+typedef struct mantis_image {   /* sensor_msgs/Image (bgr8) + sensor_msgs/CameraInfo */
+  int32_t width, height;
+  int32_t step_bytes;           /* row stride, >= 3*width */
+  int32_t mem_kind;             /* 0 = host pointer, 1 = device pointer (already in HBM) */
+  const uint8_t* bgr;
+  double K[9];                  /* CameraInfo.K, row-major; rounded to float as get3x3FromVector does */
+  double D[4];                  /* fisheye k1..k4 (CameraInfo.D) */
+  double T_base_cam[16];        /* camera pose in the rig/base frame (row-major 4x4); identity for 1 cam */
+  int64_t stamp_ns;
+  const char* frame_id;
+} mantis_image;
+
+typedef struct mantis_motion {  /* mantisService delta_pos / delta_quat ("applied to each particle") */
+  double delta_pos[3];
+  double delta_quat_xyzw[4];
+} mantis_motion;
+
+typedef struct mantis_cam_result {
+  int32_t status;
+  int32_t reason;               /* mantis_reason */
+  int32_t publish;
+  int32_t n_quads;              /* after removeDuplicateQuads */
+  int32_t n_hyps;               /* after clustering (C) */
+  int32_t n_scored;             /* hypotheses scored (fast + slow) */
+  double position[3];           /* published camera position (w2c origin, PosePub.h:33-45) */
+  double orientation_xyzw[4];
+  double covariance[36];        /* diag(error / 600) (PosePub.h:47-56) */
+  double error;                 /* hyp.error of the published hypothesis (COLOR error) */
+  double min_yaw_diff;
+  double pf_error;              /* fast error of the particle-filter optimum */
+  double c2w[12];               /* published hypothesis, world->camera R (row-major) | t */
+} mantis_cam_result;
+
+typedef struct mantis_result {  /* one rig pose (mantisService response + diagnostics) */
+  int32_t status;
+  int32_t publish;
+  int32_t n_cams_published;
+  int32_t num_particles;        /* srv num_particles: hypotheses scored over the rig */
+  double position[3];           /* srv pose (base frame in world) */
+  double orientation_xyzw[4];
+  double covariance[36];
+  double weight;                /* srv weight: error of the chosen camera hypothesis */
+  double min_yaw_diff;
+  int32_t n_quads;
+  int32_t gn_iterations;
+  double gn_cost;               /* final GN cost (0 when GN disabled) */
+  uint64_t rng_state_after;
+} mantis_result;
+
+/* ---------------------------------------------------------------- context */
+void mantis_default_config(mantis_config* cfg);
+mantis_status mantis_create(const mantis_config* cfg, void** out_ctx);
+mantis_status mantis_destroy(void* ctx);
+const char* mantis_last_error(void* ctx);
+int32_t mantis_abi_version(void);
+
+/* whiteMap / redMap / greenMap (params/map.yaml, parsed as Mantis3Params.h:125-152) */
+mantis_status mantis_set_map(void* ctx, const double* white_xyz, int32_t nw, const double* red_xyz, int32_t nr,
+                             const double* green_xyz, int32_t ng);
+/* parseCoordinatesFromString (Mantis3Params.h:125-152); returns the row count, writes up to max_pts */
+int32_t mantis_parse_coordinates(const char* s, double* xyz, int32_t max_pts);
+
+/* cv::RNG state (checkpoint / resume of the cross-frame particle-filter stream) */
+mantis_status mantis_rng_get(void* ctx, uint64_t* state);
+mantis_status mantis_rng_set(void* ctx, uint64_t state);
+
+/* ------------------------------------------------------------ hot path */
+/* One rig pose from n_cams synchronized cameras (n_cams = 1 is exactly the
+ * reference callback quadDetection, src/mantis3.cpp:68-135). cam_out may be
+ * NULL; otherwise it receives n_cams per-camera results. */
+mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams, const mantis_motion* motion,
+                             mantis_result* out, mantis_cam_result* cam_out);
+/* n_rigs rigs of cams_per_rig cameras in one batched pass (throughput path):
+ * cams[r * cams_per_rig + c]; frames are processed (and draw RNG) in that order. */
+mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
+                                   mantis_result* out, mantis_cam_result* cam_out);
+
+/* ------------------------------------------- stage entry points (parity) */
+/* gray -> GaussianBlur 3x3 -> Canny(50,150) (QuadDetection.h:209-212); out W*H bytes 0/255 */
+mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out);
+/* detector binary (dilate x2, erode x1, QuadDetection.h:213-214) and the
+ * cleanImageByEdge mask (HypothesisEvaluation.h:319-386); either output may be NULL */
+mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out, uint8_t* mask_out);
+/* detectQuadrilaterals (QuadDetection.h:203-287): int corners x0,y0..x3,y3 per quad,
+ * after removeDuplicateQuads, in reference order */
+mantis_status mantis_detect_quads(void* ctx, const mantis_image* img, int32_t* corners, int32_t max_quads,
+                                  int32_t* n_quads);
+/* evaluateHypotheses (HypothesisEvaluation.h:31-41, 71-158) fast=1 (1 px, all landmarks vs WHITE)
+ * or evaluateHypothesisCOLOR (:89-105, 160-266) fast=0 (10x10 window, green vs GREEN).
+ * c2w: n x 12 doubles (world->camera R row-major | t). mask: W*H bytes (nonzero = keep) or NULL
+ * (score img as given). err: error per hypothesis (DBL_MAX if no projection), nproj: counts. */
+mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                      int32_t n, int32_t fast, double* err, int32_t* nproj);
+/* RPP::Rpp on n 4-point problems (RPP.cpp:13-64): img_pts n x 4 x 2 normalized, obj_pts n x 4 x 3.
+ * R n x 9, t n x 3, errs n x 2 (obj_err, img_err), rpp_status n (1 ok, 0 2nd-pose search failed,
+ * -1 rotation check failed = the reference's exit(1)). */
+mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
+                               double* t, double* errs, int32_t* rpp_status);
+
+/* ----------------------------------------- Gauss–Newton rig refinement (new) */
+/* One GN step over m camera observations: for camera c, corr_c normalized image points u (2)
+ * matched to world points X (3). Accumulates J^T J (21 upper-tri), J^T r (6), cost (1) into
+ * acc28 for the base pose T_w_b (4x4 row-major) with right-perturbation exp(delta).
+ * obs: rows of [cam_index, u_x, u_y, X, Y, Z]; T_base_cam: 16 doubles per camera. */
+mantis_status mantis_gn_accumulate(void* ctx, const double* T_w_b, const double* T_base_cam, int32_t n_cams,
+                                   const double* obs, int32_t n_obs, double* acc28);
+/* Solve (JtJ + lambda I) delta = -Jtr from acc28 and update T_w_b in place. */
+mantis_status mantis_gn_solve(const double* acc28, double lambda, double* T_w_b, double* delta6);
+
+/* ------------------------------------------------- multi-GPU (RCCL, xGMI) */
+/* 128-byte ncclUniqueId; rank 0 creates it, the caller broadcasts it. */
+mantis_status mantis_comm_unique_id(void* id128);
+mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int32_t rank);
+/* Camera-sharded rig: this rank contributes its cameras; the 28-double GN
+ * accumulators are summed with one ncclAllReduce per iteration. */
+mantis_status mantis_gn_allreduce(void* ctx, double* acc28);
+
+/* ------------------------------------------------------------- tools */
+/* Synthetic fisheye grid frames rendered in HBM (bench inputs). cams: n x mantis_synth_cam;
+ * out_dev: device buffer n x H x W x 3 (stride 3W). */
+typedef struct mantis_synth_cam {
+  double fx, fy, cx, cy;
+  double k[4];
+  double R_wc[9];
+  double pos[3];
+  int32_t w, h;
+  int32_t pad[2];
+} mantis_synth_cam;
+mantis_status mantis_synth_render(void* ctx, const mantis_synth_cam* cams, int32_t n, const uint64_t* seeds,
+                                  uint8_t* out_dev);
+/* Device buffers owned by the context (for device-resident benchmark inputs). */
+mantis_status mantis_device_alloc(void* ctx, size_t bytes, void** dev_ptr);
+mantis_status mantis_device_free(void* ctx, void* dev_ptr);
+mantis_status mantis_memcpy_h2d(void* ctx, void* dst_dev, const void* src_host, size_t bytes);
+mantis_status mantis_memcpy_d2h(void* ctx, void* dst_host, const void* src_dev, size_t bytes);
+mantis_status mantis_synchronize(void* ctx);
+/* Per-kernel timing of the last call (HIP events on the context stream), in ms. */
+int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t max);
+/* Enable stage timing events (1) or not (0). */
+mantis_status mantis_set_profiling(void* ctx, int32_t on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MANTIS_H */

@@ -1,0 +1,123 @@
+// Host build of the device-logic headers (mk_*.h) for CPU unit tests only:
+// lets tests/ check the per-work-item algorithms (RPP, Jenkins–Traub, the
+// libstdc++ sort port, border following + approxPolyDP, and the parallel
+// contour formulation) against the oracle without a GPU. The product path is
+// the HIP build in libmantis_amd.so; nothing here is loaded by it.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "mk_contour.h"
+#include "mk_math.h"
+#include "mk_rpp.h"
+#include "mk_sort.h"
+
+extern "C" {
+
+int hc_rpp(const double* model, const double* iprts, double* R, double* t, double* errs, int* err_code) {
+  mk::rpp::Result r = mk::rpp::solve(model, iprts);
+  std::memcpy(R, r.R, sizeof(r.R));
+  std::memcpy(t, r.t, sizeof(r.t));
+  errs[0] = r.obj_err;
+  errs[1] = r.img_err;
+  errs[2] = r.iterations;
+  *err_code = r.error;
+  return r.status;
+}
+
+int hc_rpoly(const double* op, int deg, double* zr, double* zi) { return mk::rpp::rpoly(op, deg, zr, zi); }
+
+void hc_sort_desc(const double* err, int n, int* perm) {
+  std::vector<mk::ErrIdx> v(n);
+  for (int i = 0; i < n; i++) v[i] = {err[i], i};
+  mk::std_sort_desc(v.data(), v.data() + n);
+  for (int i = 0; i < n; i++) perm[i] = v[i].i;
+}
+
+int hc_approx(const int32_t* pts, int n, double eps, int closed, int32_t* out) {
+  std::vector<int32_t> dst(2 * n + 2), stack(2 * n + 2);
+  int m = mk::approx_poly(pts, n, eps, closed != 0, dst.data(), stack.data());
+  std::memcpy(out, dst.data(), sizeof(int32_t) * 2 * m);
+  return m;
+}
+
+// Parallel contour formulation (what the GPU kernels compute), sequential here:
+// fg 8-connected / bg 4-connected labels with root = minimum padded index,
+// one border per fg component (outer, start = root) and per enclosed bg
+// component (hole, start = root - 1), CCOMP/LIST output order from the keys.
+int hc_find_contours(const uint8_t* bin, int w, int h, int mode, int32_t* pts, int max_pts, int32_t* meta,
+                     int max_c) {
+  const int Wp = w + 2, Hp = h + 2;
+  std::vector<uint8_t> img((size_t)Wp * Hp, 0);
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) img[(size_t)(y + 1) * Wp + x + 1] = bin[(size_t)y * w + x] ? 1 : 0;
+  std::vector<int> lab((size_t)Wp * Hp);
+  for (size_t i = 0; i < lab.size(); i++) lab[i] = (int)i;
+  auto find = [&](int x) {
+    while (lab[x] != x) x = lab[x] = lab[lab[x]];
+    return x;
+  };
+  auto unite = [&](int a, int b) {
+    a = find(a); b = find(b);
+    if (a == b) return;
+    if (a < b) lab[b] = a; else lab[a] = b;
+  };
+  for (int y = 0; y < Hp; y++)
+    for (int x = 0; x < Wp; x++) {
+      int p = y * Wp + x;
+      if (img[p]) {
+        const int dx[4] = {-1, -1, 0, 1}, dy[4] = {0, -1, -1, -1};
+        for (int k = 0; k < 4; k++) {
+          int xx = x + dx[k], yy = y + dy[k];
+          if (xx < 0 || yy < 0 || xx >= Wp) continue;
+          int q = yy * Wp + xx;
+          if (img[q]) unite(p, q);
+        }
+      } else {
+        if (x > 0 && !img[p - 1]) unite(p, p - 1);
+        if (y > 0 && !img[p - Wp]) unite(p, p - Wp);
+      }
+    }
+  for (size_t i = 0; i < lab.size(); i++) lab[i] = find((int)i);
+  struct B { long long key; int start; int hole; int parent; };
+  std::vector<B> bs;
+  for (int p = 0; p < Wp * Hp; p++) {
+    if (lab[p] != p) continue;
+    if (img[p]) bs.push_back({p, p, 0, p});
+    else if (p != 0) bs.push_back({p, p - 1, 1, lab[p - 1]});
+  }
+  // CCOMP: outers by key desc, each followed by its holes by key desc; LIST: all by key desc
+  std::sort(bs.begin(), bs.end(), [&](const B& a, const B& b) {
+    if (mode == 2) {
+      if (a.parent != b.parent) return a.parent > b.parent;
+      if (a.hole != b.hole) return a.hole < b.hole;
+    }
+    return a.key > b.key;
+  });
+  if ((int)bs.size() > max_c) return -1;
+  auto nz = [&](int idx) { return img[idx] != 0; };
+  int off = 0;
+  for (size_t i = 0; i < bs.size(); i++) {
+    int sx = bs[i].start % Wp, sy = bs[i].start / Wp;
+    int n = mk::trace_border(nz, Wp, sx, sy, bs[i].hole != 0, nullptr, 0);
+    if (off + n > max_pts) return -1;
+    mk::trace_border(nz, Wp, sx, sy, bs[i].hole != 0, pts + 2 * off, n);
+    meta[3 * i] = off;
+    meta[3 * i + 1] = n;
+    meta[3 * i + 2] = bs[i].hole;
+    off += n;
+  }
+  return (int)bs.size();
+}
+
+void hc_distort(const double* xyz, int n, const double* K, const double* D, double* px) {
+  mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
+  for (int i = 0; i < n; i++) mk::distort(cm, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], px + 2 * i, px + 2 * i + 1);
+}
+void hc_undistort(const double* px, int n, const double* K, const double* D, double* out) {
+  mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
+  for (int i = 0; i < n; i++) mk::undistort(cm, px[2 * i], px[2 * i + 1], out + 2 * i, out + 2 * i + 1);
+}
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+// Border following and polygon approximation for the quad detector
+// (detectQuadrilaterals, include/mantis3/QuadDetection.h:216-226), as
+// device/host code.
+//
+// The reference calls cv::findContours(RETR_CCOMP, CHAIN_APPROX_SIMPLE) and
+// cv::approxPolyDP(eps = POLYGON_EPSILON, closed) [3P, OpenCV >= 3.2]. The
+// sequential Suzuki–Abe raster scan is replaced by an equivalent parallel
+// formulation: every 8-connected foreground component
+// has one outer border starting at its raster-first pixel, every enclosed
+// 4-connected background component (hole) one hole border starting left of
+// its raster-first pixel; each border is then followed independently here.
+// The path depends only on the binary image (OpenCV's NBD marks never change
+// which pixels are nonzero), so one work-item per border reproduces
+// icvFetchContour's point sequence exactly.
+#pragma once
+#include <cstdint>
+
+#include "mk_math.h"
+
+namespace mk {
+
+// Direction codes 0..7: right, up-right, up, up-left, left, down-left, down, down-right.
+MK_HD int code_dx(int s) { return (s == 0 || s == 1 || s == 7) ? 1 : ((s >= 3 && s <= 5) ? -1 : 0); }
+MK_HD int code_dy(int s) { return (s >= 1 && s <= 3) ? -1 : ((s >= 5 && s <= 7) ? 1 : 0); }
+
+// Follow one border of the zero-padded binary image (Wp = W + 2 columns).
+// `nz(idx)` tests a padded pixel. Writes CHAIN_APPROX_SIMPLE points (image
+// coordinates = padded - 1) when out != nullptr (up to cap); returns the count.
+template <class NZ>
+MK_HD int trace_border(const NZ& nz, int Wp, int sx, int sy, bool hole, int32_t* out, int cap) {
+  int deltas[16];
+  for (int k = 0; k < 8; k++) deltas[k] = deltas[k + 8] = code_dy(k) * Wp + code_dx(k);
+  int i0 = sy * Wp + sx;
+  int s_end, s;
+  s_end = s = hole ? 0 : 4;
+  int i1;
+  do {
+    s = (s - 1) & 7;
+    i1 = i0 + deltas[s];
+  } while (!nz(i1) && s != s_end);
+  int px = sx - 1, py = sy - 1;
+  int n = 0;
+  if (s == s_end) {
+    if (out && n < cap) { out[0] = px; out[1] = py; }
+    return 1;
+  }
+  int i3 = i0, i4;
+  int prev_s = s ^ 4;
+  for (;;) {
+    s_end = s;
+    for (;;) {
+      i4 = i3 + deltas[++s];
+      if (nz(i4)) break;
+    }
+    s &= 7;
+    if (s != prev_s) {
+      if (out && n < cap) { out[2 * n] = px; out[2 * n + 1] = py; }
+      n++;
+      prev_s = s;
+    }
+    px += code_dx(s);
+    py += code_dy(s);
+    if (i4 == i0 && i3 == i1) break;
+    i3 = i4;
+    s = (s + 4) & 7;
+  }
+  return n;
+}
+
+// cv::approxPolyDP (approxPolyDP_<int>, closed or open) on n points `src`
+// (x,y int pairs). dst needs n pairs, stack n slices (2 ints each).
+// Returns the output count.
+MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack) {
+  int count = count0;
+  if (count == 0) return 0;
+  int top = 0;
+  int init_iters = 3;
+  int sl_s = 0, sl_e = 0, rs_s = 0, rs_e = 0;
+  int spx = -1000000, spy = -1000000, epx = 0, epy = 0, ptx = 0, pty = 0;
+  int i = 0, j, pos = 0, wpos, new_count = 0;
+  bool is_closed = closed0;
+  bool le_eps = false;
+#define MK_READ(X, Y, P)            \
+  do {                              \
+    X = src[2 * (P)];               \
+    Y = src[2 * (P) + 1];           \
+    if (++(P) >= count) (P) = 0;    \
+  } while (0)
+#define MK_PUSH(S, E) \
+  do {                \
+    stack[2 * top] = (S); stack[2 * top + 1] = (E); top++; \
+  } while (0)
+  eps *= eps;
+  if (!is_closed) {
+    rs_s = count;
+    epx = src[0]; epy = src[1];
+    spx = src[2 * (count - 1)]; spy = src[2 * (count - 1) + 1];
+    if (spx != epx || spy != epy) {
+      sl_s = 0;
+      sl_e = count - 1;
+      MK_PUSH(sl_s, sl_e);
+    } else {
+      is_closed = true;
+      init_iters = 1;
+    }
+  }
+  if (is_closed) {
+    rs_s = 0;
+    for (i = 0; i < init_iters; i++) {
+      double dist, max_dist = 0;
+      pos = (pos + rs_s) % count;
+      MK_READ(spx, spy, pos);
+      for (j = 1; j < count; j++) {
+        double dx, dy;
+        MK_READ(ptx, pty, pos);
+        dx = ptx - spx;
+        dy = pty - spy;
+        dist = dx * dx + dy * dy;
+        if (dist > max_dist) {
+          max_dist = dist;
+          rs_s = j;
+        }
+      }
+      le_eps = max_dist <= eps;
+    }
+    if (!le_eps) {
+      rs_e = sl_s = pos % count;
+      sl_e = rs_s = (rs_s + sl_s) % count;
+      MK_PUSH(rs_s, rs_e);
+      MK_PUSH(sl_s, sl_e);
+    } else {
+      dst[2 * new_count] = spx; dst[2 * new_count + 1] = spy; new_count++;
+    }
+  }
+  while (top > 0) {
+    top--;
+    sl_s = stack[2 * top];
+    sl_e = stack[2 * top + 1];
+    epx = src[2 * sl_e]; epy = src[2 * sl_e + 1];
+    pos = sl_s;
+    MK_READ(spx, spy, pos);
+    if (pos != sl_e) {
+      double dx, dy, dist, max_dist = 0;
+      dx = epx - spx;
+      dy = epy - spy;
+      while (pos != sl_e) {
+        MK_READ(ptx, pty, pos);
+        dist = fabs((pty - spy) * dx - (ptx - spx) * dy);
+        if (dist > max_dist) {
+          max_dist = dist;
+          rs_s = (pos + count - 1) % count;
+        }
+      }
+      le_eps = max_dist * max_dist <= eps * (dx * dx + dy * dy);
+    } else {
+      le_eps = true;
+      spx = src[2 * sl_s]; spy = src[2 * sl_s + 1];
+    }
+    if (le_eps) {
+      dst[2 * new_count] = spx; dst[2 * new_count + 1] = spy; new_count++;
+    } else {
+      rs_e = sl_e;
+      sl_e = rs_s;
+      MK_PUSH(rs_s, rs_e);
+      MK_PUSH(sl_s, sl_e);
+    }
+  }
+  if (!is_closed) { dst[2 * new_count] = src[2 * (count - 1)]; dst[2 * new_count + 1] = src[2 * (count - 1) + 1]; new_count++; }
+#undef MK_READ
+#undef MK_PUSH
+  // final clean-up of [almost] straight runs
+  is_closed = closed0;
+  count = new_count;
+#define MK_READD(X, Y, P)           \
+  do {                              \
+    X = dst[2 * (P)];               \
+    Y = dst[2 * (P) + 1];           \
+    if (++(P) >= count) (P) = 0;    \
+  } while (0)
+  pos = is_closed ? count - 1 : 0;
+  MK_READD(spx, spy, pos);
+  wpos = pos;
+  MK_READD(ptx, pty, pos);
+  for (i = !is_closed; i < count - !is_closed && new_count > 2; i++) {
+    double dx, dy, dist, succ;
+    MK_READD(epx, epy, pos);
+    dx = epx - spx;
+    dy = epy - spy;
+    dist = fabs((ptx - spx) * dy - (pty - spy) * dx);
+    succ = (ptx - spx) * (epx - ptx) + (pty - spy) * (epy - pty);
+    if (dist * dist <= 0.5 * eps * (dx * dx + dy * dy) && dx != 0 && dy != 0 && succ >= 0) {
+      new_count--;
+      dst[2 * wpos] = spx = epx;
+      dst[2 * wpos + 1] = spy = epy;
+      if (++wpos >= count) wpos = 0;
+      MK_READD(ptx, pty, pos);
+      i++;
+      continue;
+    }
+    dst[2 * wpos] = spx = ptx;
+    dst[2 * wpos + 1] = spy = pty;
+    if (++wpos >= count) wpos = 0;
+    ptx = epx;
+    pty = epy;
+  }
+  if (!is_closed) { dst[2 * wpos] = ptx; dst[2 * wpos + 1] = pty; }
+#undef MK_READD
+  return new_count;
+}
+
+}  // namespace mk
