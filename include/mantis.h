@@ -206,6 +206,12 @@ int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t ma
 /* Enable stage timing events (1) or not (0). */
 mantis_status mantis_set_profiling(void* ctx, int32_t on);
 
+/* ------------------------------------------------------- diagnostics */
+/* Stage-by-stage record of camera-frame `frame` of the last batch (quads,
+ * hypotheses, PF/shift/yaw errors); layout = oracle/oracle.h orc_frame_debug. */
+size_t mantis_frame_debug_size(void);
+mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,1 +1,311 @@
-"""mantis_amd — MI355X-native mantis3 hot path."""
+"""mantis_amd — MI355X-native mantis3 hot path.
+
+Python is only a thin ctypes view of the C-ABI in include/mantis.h, used by
+tests/, bench.py and __graft_entry__.py; the product is libmantis_amd.so
+(HIP kernels for gfx950 + C++ host orchestration). There is no CPU fallback:
+loading fails loudly when the library is missing, and mantis_create fails
+when no GPU is present.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmantis_amd.so")
+
+MANTIS_OK = 0
+REASONS = {0: "published", 1: "no_quads", 2: "no_hyps", 3: "yaw_ambiguous", 4: "no_yaw"}
+
+
+class MantisConfig(C.Structure):
+    _fields_ = [("struct_size", C.c_int32), ("device", C.c_int32), ("max_cams", C.c_int32),
+                ("max_width", C.c_int32), ("max_height", C.c_int32), ("rng_seed", C.c_uint64),
+                ("canny_low", C.c_int32), ("polygon_epsilon", C.c_int32),
+                ("search_radius_multiplier", C.c_double), ("grid_spacing", C.c_double),
+                ("particles", C.c_int32), ("iterations", C.c_int32), ("gn_enable", C.c_int32),
+                ("gn_iterations", C.c_int32), ("max_quads", C.c_int32), ("max_contour_points", C.c_int32)]
+
+
+class MantisImage(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("step_bytes", C.c_int32), ("mem_kind", C.c_int32),
+                ("bgr", C.c_void_p), ("K", C.c_double * 9), ("D", C.c_double * 4),
+                ("T_base_cam", C.c_double * 16), ("stamp_ns", C.c_int64), ("frame_id", C.c_char_p)]
+
+
+class MantisMotion(C.Structure):
+    _fields_ = [("delta_pos", C.c_double * 3), ("delta_quat_xyzw", C.c_double * 4)]
+
+
+class MantisCamResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("reason", C.c_int32), ("publish", C.c_int32), ("n_quads", C.c_int32),
+                ("n_hyps", C.c_int32), ("n_scored", C.c_int32), ("position", C.c_double * 3),
+                ("orientation_xyzw", C.c_double * 4), ("covariance", C.c_double * 36), ("error", C.c_double),
+                ("min_yaw_diff", C.c_double), ("pf_error", C.c_double), ("c2w", C.c_double * 12)]
+
+
+class MantisResult(C.Structure):
+    _fields_ = [("status", C.c_int32), ("publish", C.c_int32), ("n_cams_published", C.c_int32),
+                ("num_particles", C.c_int32), ("position", C.c_double * 3), ("orientation_xyzw", C.c_double * 4),
+                ("covariance", C.c_double * 36), ("weight", C.c_double), ("min_yaw_diff", C.c_double),
+                ("n_quads", C.c_int32), ("gn_iterations", C.c_int32), ("gn_cost", C.c_double),
+                ("rng_state_after", C.c_uint64)]
+
+
+class SynthCamC(C.Structure):
+    _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+                ("k", C.c_double * 4), ("R_wc", C.c_double * 9), ("pos", C.c_double * 3),
+                ("w", C.c_int32), ("h", C.c_int32), ("pad", C.c_int32 * 2)]
+
+
+class FrameDebug(C.Structure):
+    """Layout of mk::FrameDebug == oracle orc_frame_debug."""
+    _fields_ = [
+        ("reason", C.c_int32), ("publish", C.c_int32), ("n_raw_quads", C.c_int32), ("n_quads", C.c_int32),
+        ("quads", (C.c_int32 * 8) * 256), ("test_pts", (C.c_double * 8) * 256),
+        ("n_gen", C.c_int32), ("n_hyps", C.c_int32),
+        ("hyp_c2w", (C.c_double * 12) * 1024), ("hyp_err", C.c_double * 1024), ("hyp_n", C.c_int32 * 1024),
+        ("best1_c2w", C.c_double * 12), ("best1_err", C.c_double),
+        ("pf_c2w", C.c_double * 12), ("pf_err", C.c_double), ("pf_iter_err", C.c_double * 11),
+        ("shift_err", C.c_double * 81), ("top20_err", C.c_double * 20), ("yaw_err", C.c_double * 4),
+        ("yaw_best", C.c_int32), ("min_yaw_diff", C.c_double), ("pub_c2w", C.c_double * 12),
+        ("pub_error", C.c_double), ("position", C.c_double * 3), ("orientation_xyzw", C.c_double * 4),
+        ("covariance", C.c_double * 36), ("rng_state_after", C.c_uint64), ("n_scored", C.c_int32),
+    ]
+
+
+_lib = None
+
+_SIGS = {
+    "mantis_abi_version": (C.c_int32, []),
+    "mantis_default_config": (None, [C.POINTER(MantisConfig)]),
+    "mantis_create": (C.c_int, [C.POINTER(MantisConfig), C.POINTER(C.c_void_p)]),
+    "mantis_destroy": (C.c_int, [C.c_void_p]),
+    "mantis_last_error": (C.c_char_p, [C.c_void_p]),
+    "mantis_set_map": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
+    "mantis_parse_coordinates": (C.c_int32, [C.c_char_p, C.c_void_p, C.c_int32]),
+    "mantis_rng_get": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "mantis_rng_set": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "mantis_process": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_int32, C.POINTER(MantisMotion),
+                                 C.POINTER(MantisResult), C.POINTER(MantisCamResult)]),
+    "mantis_process_batch": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_int32, C.c_int32,
+                                       C.POINTER(MantisResult), C.POINTER(MantisCamResult)]),
+    "mantis_canny": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p]),
+    "mantis_masks": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p, C.c_void_p]),
+    "mantis_detect_quads": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p, C.c_int32,
+                                      C.POINTER(C.c_int32)]),
+    "mantis_score_hypotheses": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p, C.c_void_p, C.c_int32,
+                                          C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_rpp_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]),
+    "mantis_synth_render": (C.c_int, [C.c_void_p, C.POINTER(SynthCamC), C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "mantis_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mantis_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mantis_memcpy_d2h": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "mantis_synchronize": (C.c_int, [C.c_void_p]),
+    "mantis_kernel_times": (C.c_int32, [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int32]),
+    "mantis_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mantis_frame_debug_size": (C.c_size_t, []),
+    "mantis_get_frame_debug": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mantis_gn_accumulate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                       C.c_void_p]),
+    "mantis_gn_solve": (C.c_int, [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p]),
+    "mantis_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "mantis_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
+    "mantis_gn_allreduce": (C.c_int, [C.c_void_p, C.c_void_p]),
+}
+
+
+def lib():
+    """Load libmantis_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with __graft_entry__.build() (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class MantisError(RuntimeError):
+    pass
+
+
+def default_config(**kw):
+    cfg = MantisConfig()
+    lib().mantis_default_config(C.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def make_image(bgr, K, D, T_base_cam=None, device_ptr=None, width=None, height=None):
+    """mantis_image for a host numpy BGR8 array or a device pointer."""
+    im = MantisImage()
+    if device_ptr is not None:
+        im.width, im.height = width, height
+        im.step_bytes = 3 * width
+        im.mem_kind = 1
+        im.bgr = device_ptr
+    else:
+        assert bgr.dtype == np.uint8 and bgr.ndim == 3 and bgr.shape[2] == 3
+        bgr = np.ascontiguousarray(bgr)
+        im.height, im.width = bgr.shape[:2]
+        im.step_bytes = bgr.strides[0]
+        im.mem_kind = 0
+        im.bgr = bgr.ctypes.data
+        im._keep = bgr
+    Kf = np.asarray(K, np.float64).reshape(9)
+    for i in range(9):
+        im.K[i] = Kf[i]
+    Df = np.asarray(D, np.float64).reshape(4)
+    for i in range(4):
+        im.D[i] = Df[i]
+    T = np.eye(4) if T_base_cam is None else np.asarray(T_base_cam, np.float64)
+    for i in range(16):
+        im.T_base_cam[i] = T.reshape(16)[i]
+    return im
+
+
+class Mantis:
+    """One mantis_amd context (one GPU, one HIP stream, one cv::RNG stream)."""
+
+    def __init__(self, cfg=None, **kw):
+        L = lib()
+        self.cfg = cfg if cfg is not None else default_config(**kw)
+        h = C.c_void_p()
+        st = L.mantis_create(C.byref(self.cfg), C.byref(h))
+        if st != MANTIS_OK:
+            raise MantisError(f"mantis_create failed ({st}): {L.mantis_last_error(None).decode()}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mantis_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st, what):
+        if st != MANTIS_OK:
+            raise MantisError(f"{what} failed ({st}): {lib().mantis_last_error(self.h).decode()}")
+
+    def set_map(self, white, red, green):
+        self._map = [np.ascontiguousarray(a, np.float64) for a in (white, red, green)]
+        w, r, g = self._map
+        self._chk(lib().mantis_set_map(self.h, w.ctypes.data, len(w), r.ctypes.data, len(r), g.ctypes.data, len(g)),
+                  "set_map")
+
+    @property
+    def rng_state(self):
+        v = C.c_uint64()
+        self._chk(lib().mantis_rng_get(self.h, C.byref(v)), "rng_get")
+        return v.value
+
+    @rng_state.setter
+    def rng_state(self, s):
+        self._chk(lib().mantis_rng_set(self.h, C.c_uint64(s)), "rng_set")
+
+    def process(self, images, rigs=1):
+        n = len(images)
+        cams = (MantisImage * n)(*images)
+        out = (MantisResult * rigs)()
+        cam_out = (MantisCamResult * n)()
+        st = lib().mantis_process_batch(self.h, cams, rigs, n // rigs, out, cam_out)
+        self._chk(st, "process_batch")
+        return list(out), list(cam_out)
+
+    def frame_debug(self, i):
+        d = FrameDebug()
+        assert C.sizeof(d) == lib().mantis_frame_debug_size(), "FrameDebug layout mismatch"
+        self._chk(lib().mantis_get_frame_debug(self.h, i, C.byref(d), C.sizeof(d)), "get_frame_debug")
+        return d
+
+    def canny(self, img):
+        out = np.zeros((img.height, img.width), np.uint8)
+        self._chk(lib().mantis_canny(self.h, C.byref(img), out.ctypes.data), "canny")
+        return out
+
+    def masks(self, img):
+        det = np.zeros((img.height, img.width), np.uint8)
+        mask = np.zeros((img.height, img.width), np.uint8)
+        self._chk(lib().mantis_masks(self.h, C.byref(img), det.ctypes.data, mask.ctypes.data), "masks")
+        return det, mask
+
+    def detect_quads(self, img, max_quads=256):
+        corners = np.zeros((max_quads, 8), np.int32)
+        n = C.c_int32()
+        self._chk(lib().mantis_detect_quads(self.h, C.byref(img), corners.ctypes.data, max_quads, C.byref(n)),
+                  "detect_quads")
+        return corners[: n.value].copy()
+
+    def score(self, img, c2w, fast=True, mask=None):
+        c2w = np.ascontiguousarray(c2w, np.float64).reshape(-1, 12)
+        n = len(c2w)
+        err = np.zeros(n)
+        npj = np.zeros(n, np.int32)
+        mptr = None
+        if mask is not None:
+            mask = np.ascontiguousarray(mask, np.uint8)
+            mptr = mask.ctypes.data
+        self._chk(lib().mantis_score_hypotheses(self.h, C.byref(img), mptr, c2w.ctypes.data, n, int(fast),
+                                                err.ctypes.data, npj.ctypes.data), "score_hypotheses")
+        return err, npj
+
+    def rpp(self, img_pts, obj_pts):
+        img_pts = np.ascontiguousarray(img_pts, np.float64).reshape(-1, 4, 2)
+        obj_pts = np.ascontiguousarray(obj_pts, np.float64).reshape(-1, 4, 3)
+        n = len(img_pts)
+        R = np.zeros((n, 9))
+        t = np.zeros((n, 3))
+        e = np.zeros((n, 2))
+        s = np.zeros(n, np.int32)
+        self._chk(lib().mantis_rpp_batch(self.h, img_pts.ctypes.data, obj_pts.ctypes.data, n, R.ctypes.data,
+                                         t.ctypes.data, e.ctypes.data, s.ctypes.data), "rpp_batch")
+        return R.reshape(n, 3, 3), t, e, s
+
+    # device buffers -------------------------------------------------------
+    def device_alloc(self, nbytes):
+        p = C.c_void_p()
+        self._chk(lib().mantis_device_alloc(self.h, nbytes, C.byref(p)), "device_alloc")
+        return p.value
+
+    def device_free(self, p):
+        self._chk(lib().mantis_device_free(self.h, C.c_void_p(p)), "device_free")
+
+    def h2d(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        self._chk(lib().mantis_memcpy_h2d(self.h, C.c_void_p(dst), arr.ctypes.data, arr.nbytes), "h2d")
+
+    def d2h(self, arr, src):
+        self._chk(lib().mantis_memcpy_d2h(self.h, arr.ctypes.data, C.c_void_p(src), arr.nbytes), "d2h")
+        return arr
+
+    def synth_render(self, cams, seeds, out_dev):
+        n = len(cams)
+        arr = (SynthCamC * n)()
+        for i, c in enumerate(cams):
+            C.memmove(C.byref(arr[i]), C.byref(c), C.sizeof(SynthCamC))
+        s = np.ascontiguousarray(seeds, np.uint64)
+        self._chk(lib().mantis_synth_render(self.h, arr, n, s.ctypes.data, C.c_void_p(out_dev)), "synth_render")
+
+    def synchronize(self):
+        self._chk(lib().mantis_synchronize(self.h), "synchronize")
+
+    def set_profiling(self, on):
+        self._chk(lib().mantis_set_profiling(self.h, int(on)), "set_profiling")
+
+    def kernel_times(self):
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        n = lib().mantis_kernel_times(self.h, names, ms, 64)
+        return [(names[i].decode(), ms[i]) for i in range(n)]

@@ -1,0 +1,874 @@
+// libmantis_amd.so — C-ABI (include/mantis.h) and host orchestration of the
+// batched mantis3 hot path on one MI355X. One translation unit: the kernels
+// are included below so every launch sees its definition.
+//
+// Batch flow per mantis_process_batch call (one HIP stream, no host sync
+// until the results are copied back):
+//   H2D frames (pinned staging)      | host: gaussian stream for the batch
+//   image stages (all frames)        |   (cv::RNG, generated while the GPU
+//   contours -> quads -> RPP -> hyps |    runs the detector)
+//   offsets into the gaussian stream (frames that reach the PF, in order)
+//   H2D gaussians -> scoring/PF/shift/yaw -> D2H results
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "kernels.hip"
+
+using namespace mk;
+
+namespace {
+
+// ------------------------------------------------------------ cv::RNG (host)
+// The reference's global `cv::RNG rng(1)` (Mantis3Params.h:87): MWC step and
+// the float32 ziggurat of RNG::gaussian [OpenCV 3.x], generated on the host in
+// draw order and consumed on the device from a per-batch stream.
+struct ZigTables {
+  uint32_t kn[128];
+  float wn[128], fn[128];
+  ZigTables() {
+    const double m1 = 2147483648.0;
+    double dn = 3.442619855899, tn = dn, vn = 9.91256303526217e-3;
+    double q = vn / std::exp(-.5 * dn * dn);
+    kn[0] = (uint32_t)((dn / q) * m1);
+    kn[1] = 0;
+    wn[0] = (float)(q / m1);
+    wn[127] = (float)(dn / m1);
+    fn[0] = 1.f;
+    fn[127] = (float)std::exp(-.5 * dn * dn);
+    for (int i = 126; i >= 1; i--) {
+      dn = std::sqrt(-2. * std::log(vn / dn + std::exp(-.5 * dn * dn)));
+      kn[i + 1] = (uint32_t)((dn / tn) * m1);
+      tn = dn;
+      fn[i] = (float)std::exp(-.5 * dn * dn);
+      wn[i] = (float)(dn / m1);
+    }
+  }
+};
+const ZigTables& zig() {
+  static ZigTables t;
+  return t;
+}
+inline uint64_t rng_step(uint64_t x) { return (uint64_t)(uint32_t)x * 4164903690ULL + (x >> 32); }
+inline float rng_gauss(uint64_t& state) {
+  const ZigTables& T = zig();
+  const float r = 3.442620f;
+  const float rng_flt = 2.3283064365386962890625e-10f;
+  uint64_t temp = state;
+  float x, y;
+  for (;;) {
+    int hz = (int)(uint32_t)temp;
+    temp = rng_step(temp);
+    int iz = hz & 127;
+    x = hz * T.wn[iz];
+    if ((unsigned)std::abs(hz) < T.kn[iz]) break;
+    if (iz == 0) {
+      do {
+        x = (unsigned)temp * rng_flt;
+        temp = rng_step(temp);
+        y = (unsigned)temp * rng_flt;
+        temp = rng_step(temp);
+        x = (float)(-std::log(x + FLT_MIN) * 0.2904764);
+        y = (float)-std::log(y + FLT_MIN);
+      } while (y + y < x * x);
+      x = hz > 0 ? r + x : -r - x;
+      break;
+    }
+    y = (unsigned)temp * rng_flt;
+    temp = rng_step(temp);
+    if (T.fn[iz] + y * (T.fn[iz - 1] - T.fn[iz]) < std::exp(-.5 * x * x)) break;
+  }
+  state = temp;
+  return x;
+}
+
+#define HIP_OK(expr)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      c->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+      return MANTIS_ERR_DEVICE;                                                   \
+    }                                                                             \
+  } while (0)
+
+struct Ctx {
+  mantis_config cfg{};
+  hipStream_t s = nullptr;
+  std::string err;
+  uint64_t rng_state = 1;
+  // map
+  double* d_lm = nullptr;
+  int nw = 0, nr = 0, ng = 0;
+  // capacity
+  int F = 0, Wmax = 0, Hmax = 0;
+  size_t plane = 0;
+  int pool_cap = 0;
+  // device workspace
+  uint8_t *d_bgr = nullptr, *d_cls = nullptr, *d_strong = nullptr, *d_edge = nullptr, *d_t0 = nullptr,
+          *d_t1 = nullptr, *d_det = nullptr, *d_mask = nullptr;
+  int32_t* d_lab = nullptr;
+  FrameDesc* d_frames = nullptr;
+  Border* d_borders = nullptr;
+  int32_t *d_bcount = nullptr, *d_boff = nullptr, *d_pool = nullptr, *d_scratch = nullptr;
+  QuadRec* d_quads = nullptr;
+  RppOut* d_rpp = nullptr;
+  HypRec *d_gen = nullptr, *d_hyps = nullptr;
+  FrameState* d_st = nullptr;
+  FrameDebug* d_dbg = nullptr;
+  mantis_cam_result* d_res = nullptr;
+  float* d_gauss = nullptr;
+  int32_t* d_gtotal = nullptr;
+  // pinned host
+  float* h_gauss = nullptr;
+  uint64_t* h_states = nullptr;
+  mantis_cam_result* h_res = nullptr;
+  FrameState* h_st = nullptr;
+  int32_t* h_gtotal = nullptr;
+  FrameDesc* h_frames = nullptr;
+  // profiling
+  bool prof = false;
+  std::vector<std::string> ev_names;
+  std::vector<hipEvent_t> ev;
+  std::vector<float> last_ms;
+  std::vector<std::string> last_names;
+  std::vector<void*> user_allocs;
+  int lds_bytes = 0;
+  // multi-GPU
+  void* comm = nullptr;  // ncclComm_t
+  double* d_gn28 = nullptr;
+};
+
+void mark(Ctx* c, const char* name) {
+  if (!c->prof) return;
+  if (c->ev.size() <= c->ev_names.size()) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    c->ev.push_back(e);
+  }
+  (void)hipEventRecord(c->ev[c->ev_names.size()], c->s);
+  c->ev_names.push_back(name);
+}
+
+inline int blocks_for(size_t n, int per = 256, int cap = 4096) {
+  size_t b = (n + per - 1) / per;
+  return (int)std::min<size_t>(std::max<size_t>(b, 1), (size_t)cap);
+}
+
+Cam cam_from(const mantis_image& im) {
+  Cam m;
+  m.fx = (double)(float)im.K[0];
+  m.fy = (double)(float)im.K[4];
+  m.cx = (double)(float)im.K[2];
+  m.cy = (double)(float)im.K[5];
+  for (int k = 0; k < 4; k++) m.k[k] = im.D[k];
+  return m;
+}
+
+// Stage the frames into the batch: device-resident contiguous inputs are
+// used in place; everything else is copied (pitch-converted) into d_bgr.
+mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int& H) {
+  if (n <= 0 || n > c->F) { c->err = "frame count exceeds max_cams"; return MANTIS_ERR_ARG; }
+  W = cams[0].width;
+  H = cams[0].height;
+  if (W <= 2 || H <= 2 || W > c->Wmax || H > c->Hmax) { c->err = "image size outside [3, max]"; return MANTIS_ERR_ARG; }
+  const size_t fb = (size_t)W * H * 3;
+  for (int i = 0; i < n; i++) {
+    const mantis_image& im = cams[i];
+    if (im.width != W || im.height != H) { c->err = "all cameras of a batch must share one size"; return MANTIS_ERR_ARG; }
+    if (!im.bgr || im.step_bytes < 3 * W) { c->err = "bgr8 image with step >= 3*width required"; return MANTIS_ERR_ARG; }
+    FrameDesc& fd = c->h_frames[i];
+    fd.w = W;
+    fd.h = H;
+    fd.cam = cam_from(im);
+    if (im.mem_kind == 1 && im.step_bytes == 3 * W) {
+      fd.bgr = im.bgr;
+    } else {
+      uint8_t* dst = c->d_bgr + (size_t)i * fb;
+      HIP_OK(hipMemcpy2DAsync(dst, 3 * W, im.bgr, im.step_bytes, 3 * W, H,
+                              im.mem_kind == 1 ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->s));
+      fd.bgr = dst;
+    }
+  }
+  HIP_OK(hipMemcpyAsync(c->d_frames, c->h_frames, sizeof(FrameDesc) * n, hipMemcpyHostToDevice, c->s));
+  return MANTIS_OK;
+}
+
+// gray..Canny, hysteresis, detector binary (padded) and clean mask
+mantis_status run_image_stages(Ctx* c, int n, int W, int H) {
+  const size_t P = c->plane;
+  const size_t npx = (size_t)W * H;
+  const int Wp = W + 2, Hp = H + 2;
+  HIP_OK(hipMemsetAsync(c->d_strong, 0, P * n, c->s));
+  HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
+  mark(c, "start");
+  dim3 gt((W + TX - 1) / TX, (H + TY - 1) / TY, n);
+  k_canny_cls<<<gt, 256, 0, c->s>>>(c->d_frames, c->d_cls, c->d_lab, P, c->cfg.canny_low, 3 * c->cfg.canny_low);
+  mark(c, "canny_nms");
+  dim3 gp(blocks_for(npx), n);
+  k_uf_merge8<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, W, H, P);
+  k_hyst_flatten<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
+  k_hyst_edge<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, c->d_edge, W, H, P);
+  mark(c, "hysteresis");
+  // detector: dilate(iter 2) = 5x5 rect, erode(iter 1) = 3x3 rect
+  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_edge, c->d_t0, W, H, P, 2, 1);
+  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, 2, 1, 0);
+  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, 1, 0);
+  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_det, W, H, P, 1, 0, 1);
+  mark(c, "det_morph");
+  // cleanImageByEdge mask: M0 then 3 x {dilate, erode}(3+i) and erode(3)
+  k_grad_border<<<gp, 256, 0, c->s>>>(c->d_edge, c->d_t0, W, H, P);
+  for (int i = 0; i < 3; i++) {
+    int r = 3 + i;
+    k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, r, 1);
+    k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, r, 1, 0);
+    k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, r, 0);
+    k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, r, 0, 0);
+  }
+  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, 3, 0);
+  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_mask, W, H, P, 3, 0, 0);
+  mark(c, "mask_morph");
+  (void)Wp;
+  (void)Hp;
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+mantis_status run_contours(Ctx* c, int n, int W, int H) {
+  const size_t P = c->plane;
+  const int Wp = W + 2, Hp = H + 2;
+  const size_t np = (size_t)Wp * Hp;
+  HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
+  dim3 gp(blocks_for(np), n);
+  k_cc_init<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
+  k_cc_merge<<<gp, 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
+  k_cc_flatten<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
+  k_border_emit<<<gp, 256, 0, c->s>>>(c->d_det, c->d_lab, c->d_borders, c->d_st, Wp, Hp, P, kMaxBorders);
+  mark(c, "components");
+  const size_t bits_bytes = ((np + 31) / 32) * 4;
+  const int use_lds = bits_bytes <= (size_t)c->lds_bytes ? 1 : 0;
+  k_frame_contours<<<n, 1024, use_lds ? bits_bytes : 0, c->s>>>(
+      c->d_det, c->d_borders, c->d_st, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->pool_cap, c->d_quads,
+      c->d_dbg, c->d_frames, Wp, Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon, c->cfg.search_radius_multiplier,
+      use_lds);
+  mark(c, "contours_quads");
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+mantis_status run_pose(Ctx* c, int n) {
+  dim3 gr((kMaxQuads * 2 + 255) / 256, n);
+  k_rpp<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_rpp, c->cfg.grid_spacing / 2);
+  mark(c, "rpp");
+  k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
+  mark(c, "hyps_cluster");
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  k_gauss_offsets<<<1, 1, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+// Gaussian stream for up to n frames (frames that skip the PF draw nothing,
+// so the stream is contiguous and the device indexes it by prefix offsets).
+void gen_gauss(Ctx* c, int n) {
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  uint64_t s = c->rng_state;
+  c->h_states[0] = s;
+  for (int f = 0; f < n; f++) {
+    float* g = c->h_gauss + (size_t)f * per;
+    for (int k = 0; k < per; k++) g[k] = rng_gauss(s);
+    c->h_states[f + 1] = s;
+  }
+}
+
+mantis_status run_score(Ctx* c, int n) {
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n, hipMemcpyHostToDevice, c->s));
+  mark(c, "gauss_h2d");
+  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  k_frame_score<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mask, c->plane, L, c->d_st, c->d_hyps, c->d_gauss,
+                                               c->d_res, c->d_dbg, c->cfg.particles, c->cfg.iterations,
+                                               c->cfg.grid_spacing, 9);
+  mark(c, "score_pf_yaw");
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+void finish_profile(Ctx* c) {
+  if (!c->prof || c->ev_names.empty()) return;
+  (void)hipEventSynchronize(c->ev[c->ev_names.size() - 1]);
+  c->last_names.clear();
+  c->last_ms.clear();
+  for (size_t i = 1; i < c->ev_names.size(); i++) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev[i - 1], c->ev[i]);
+    c->last_names.push_back(c->ev_names[i]);
+    c->last_ms.push_back(ms);
+  }
+  c->ev_names.clear();
+}
+
+// 4x4 helpers for rig results (row-major)
+void mat4_mul(const double* a, const double* b, double* o) {
+  double r[16];
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      double s = 0;
+      for (int k = 0; k < 4; k++) s += a[i * 4 + k] * b[k * 4 + j];
+      r[i * 4 + j] = s;
+    }
+  std::memcpy(o, r, sizeof(r));
+}
+void mat4_inv_rigid(const double* a, double* o) {
+  double r[16] = {0};
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[i * 4 + j] = a[j * 4 + i];
+  for (int i = 0; i < 3; i++) r[i * 4 + 3] = -(r[i * 4 + 0] * a[3] + r[i * 4 + 1] * a[7] + r[i * 4 + 2] * a[11]);
+  r[15] = 1;
+  std::memcpy(o, r, sizeof(r));
+}
+void quat_to_mat4(const double* q, const double* p, double* T) {
+  mk::Quat qq{q[0], q[1], q[2], q[3]};
+  double R[9];
+  basis_from_quat(qq, R);
+  for (int i = 0; i < 16; i++) T[i] = 0;
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) T[i * 4 + j] = R[i * 3 + j];
+    T[i * 4 + 3] = p[i];
+  }
+  T[15] = 1;
+}
+
+// Rig pose from per-camera results (reference-parity mode: no GN): the
+// published camera with the lowest error, mapped through T_base_cam.
+void fuse_rig(const mantis_image* cams, const mantis_cam_result* cr, int nc, mantis_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  int best = -1;
+  int npub = 0, nscored = 0, nq = 0;
+  for (int i = 0; i < nc; i++) {
+    nscored += cr[i].n_scored;
+    nq += cr[i].n_quads;
+    if (cr[i].publish) {
+      npub++;
+      if (best < 0 || cr[i].error < cr[best].error) best = i;
+    }
+  }
+  out->num_particles = nscored;
+  out->n_quads = nq;
+  out->n_cams_published = npub;
+  out->status = MANTIS_OK;
+  if (best < 0) {
+    // nothing passes the yaw gate: report the first camera that produced a pose, unpublished
+    for (int i = 0; i < nc && best < 0; i++)
+      if (cr[i].reason == MANTIS_PUBLISHED || cr[i].reason == MANTIS_YAW_AMBIGUOUS) best = i;
+    out->publish = 0;
+    if (best < 0) return;
+  } else {
+    out->publish = 1;
+  }
+  double Twc[16], Tbc_inv[16], Twb[16];
+  quat_to_mat4(cr[best].orientation_xyzw, cr[best].position, Twc);
+  mat4_inv_rigid(cams[best].T_base_cam, Tbc_inv);
+  mat4_mul(Twc, Tbc_inv, Twb);
+  double R[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) R[i * 3 + j] = Twb[i * 4 + j];
+  mk::Quat q = basis_to_quat(R);
+  out->orientation_xyzw[0] = q.x; out->orientation_xyzw[1] = q.y;
+  out->orientation_xyzw[2] = q.z; out->orientation_xyzw[3] = q.w;
+  for (int i = 0; i < 3; i++) out->position[i] = Twb[i * 4 + 3];
+  for (int i = 0; i < 36; i++) out->covariance[i] = cr[best].covariance[i];
+  out->weight = cr[best].error;
+  out->min_yaw_diff = cr[best].min_yaw_diff;
+}
+
+mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
+  if (!c->d_lm) { c->err = "map not set (mantis_set_map)"; return MANTIS_ERR_STATE; }
+  int W, H;
+  mantis_status st = stage_frames(c, cams, n, W, H);
+  if (st != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, n, W, H)) != MANTIS_OK) return st;
+  if ((st = run_contours(c, n, W, H)) != MANTIS_OK) return st;
+  if ((st = run_pose(c, n)) != MANTIS_OK) return st;
+  gen_gauss(c, n);  // overlaps the device work queued above
+  if ((st = run_score(c, n)) != MANTIS_OK) return st;
+  HIP_OK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(mantis_cam_result) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(c->h_gtotal, c->d_gtotal, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  finish_profile(c);
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  int used = 0;
+  for (int f = 0; f < n; f++) {
+    if (c->h_st[f].reaches_pf) used++;
+    if (c->h_st[f].overflow) {
+      std::ostringstream os;
+      os << "frame " << f << ": workspace capacity exceeded (flags " << c->h_st[f].overflow << ", borders "
+         << c->h_st[f].n_borders << ", points " << c->h_st[f].n_points << ", raw quads " << c->h_st[f].n_raw_quads
+         << ")";
+      c->err = os.str();
+      c->h_res[f].status = MANTIS_ERR_CAPACITY;
+    }
+  }
+  if (used * per != *c->h_gtotal) { c->err = "internal: gaussian stream accounting mismatch"; return MANTIS_ERR_DEVICE; }
+  c->rng_state = c->h_states[used];
+  return MANTIS_OK;
+}
+
+template <class T>
+mantis_status dalloc(Ctx* c, T** p, size_t count) {
+  if (hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1)) != hipSuccess) {
+    c->err = "hipMalloc failed";
+    return MANTIS_ERR_OOM;
+  }
+  return MANTIS_OK;
+}
+template <class T>
+mantis_status halloc(Ctx* c, T** p, size_t count) {
+  if (hipHostMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1), hipHostMallocDefault) != hipSuccess) {
+    c->err = "hipHostMalloc failed";
+    return MANTIS_ERR_OOM;
+  }
+  return MANTIS_OK;
+}
+
+thread_local std::string g_create_err;
+
+}  // namespace
+
+extern "C" {
+
+int32_t mantis_abi_version(void) { return MANTIS_ABI_VERSION; }
+
+void mantis_default_config(mantis_config* cfg) {
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->struct_size = sizeof(mantis_config);
+  cfg->device = 0;
+  cfg->max_cams = 16;
+  cfg->max_width = 1280;
+  cfg->max_height = 720;
+  cfg->rng_seed = 1;
+  cfg->canny_low = 50;
+  cfg->polygon_epsilon = 10;
+  cfg->search_radius_multiplier = 0.1;
+  cfg->grid_spacing = 0.32;
+  cfg->particles = 50;
+  cfg->iterations = 10;
+  cfg->gn_enable = 0;
+  cfg->gn_iterations = 10;
+  cfg->max_quads = kMaxQuads;
+  cfg->max_contour_points = 262144;
+}
+
+mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
+  if (!out_ctx) return MANTIS_ERR_ARG;
+  *out_ctx = nullptr;
+  mantis_config cfg;
+  mantis_default_config(&cfg);
+  if (cfg_in) {
+    if (cfg_in->struct_size != (int32_t)sizeof(mantis_config)) {
+      g_create_err = "mantis_config.struct_size mismatch";
+      return MANTIS_ERR_ARG;
+    }
+    cfg = *cfg_in;
+  }
+  if (cfg.particles < 1 || cfg.particles > 96 || cfg.iterations < 0 || cfg.max_cams < 1 || cfg.max_width < 3 ||
+      cfg.max_height < 3) {
+    g_create_err = "invalid config";
+    return MANTIS_ERR_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg.device) {
+    g_create_err = "no HIP device available (libmantis_amd requires an MI355X / gfx950 GPU)";
+    return MANTIS_ERR_DEVICE;
+  }
+  Ctx* c = new Ctx();
+  c->cfg = cfg;
+  c->rng_state = cfg.rng_seed ? cfg.rng_seed : 0xffffffffULL;
+  if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+    g_create_err = "hipSetDevice/hipStreamCreate failed";
+    delete c;
+    return MANTIS_ERR_DEVICE;
+  }
+  c->F = cfg.max_cams;
+  c->Wmax = cfg.max_width;
+  c->Hmax = cfg.max_height;
+  c->plane = (size_t)(c->Wmax + 2) * (c->Hmax + 2);
+  c->pool_cap = cfg.max_contour_points;
+  const int F = c->F;
+  const int per = cfg.particles * cfg.iterations * 6;
+  mantis_status st = MANTIS_OK;
+  auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
+  chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
+  chk(dalloc(c, &c->d_cls, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_edge, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_t0, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_t1, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_det, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_frames, (size_t)F));
+  chk(dalloc(c, &c->d_borders, (size_t)F * kMaxBorders));
+  chk(dalloc(c, &c->d_bcount, (size_t)F * kMaxBorders));
+  chk(dalloc(c, &c->d_boff, (size_t)F * kMaxBorders));
+  chk(dalloc(c, &c->d_pool, (size_t)F * 2 * c->pool_cap));
+  chk(dalloc(c, &c->d_scratch, (size_t)F * 4 * c->pool_cap));
+  chk(dalloc(c, &c->d_quads, (size_t)F * kMaxQuads));
+  chk(dalloc(c, &c->d_rpp, (size_t)F * kMaxQuads * 2));
+  chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
+  chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
+  chk(dalloc(c, &c->d_st, (size_t)F));
+  chk(dalloc(c, &c->d_dbg, (size_t)F));
+  chk(dalloc(c, &c->d_res, (size_t)F));
+  chk(dalloc(c, &c->d_gauss, (size_t)F * per));
+  chk(dalloc(c, &c->d_gtotal, 1));
+  chk(halloc(c, &c->h_gauss, (size_t)F * per));
+  chk(halloc(c, &c->h_states, (size_t)F + 1));
+  chk(halloc(c, &c->h_res, (size_t)F));
+  chk(halloc(c, &c->h_st, (size_t)F));
+  chk(halloc(c, &c->h_gtotal, 1));
+  chk(halloc(c, &c->h_frames, (size_t)F));
+  if (st != MANTIS_OK) {
+    g_create_err = c->err;
+    mantis_destroy(c);
+    return st;
+  }
+  // the contour kernel keeps the padded frame as a bitmap in LDS when it fits
+  int max_lds = 0;
+  (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device);
+  const int static_lds = 28 * 1024;
+  c->lds_bytes = std::max(0, std::min(max_lds, 160 * 1024) - static_lds);
+  if (c->lds_bytes > 0)
+    (void)hipFuncSetAttribute((const void*)k_frame_contours, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes);
+  if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess) {
+    g_create_err = "hipMemset failed";
+    mantis_destroy(c);
+    return MANTIS_ERR_DEVICE;
+  }
+  *out_ctx = c;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_destroy(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  if (c->s) (void)hipStreamSynchronize(c->s);
+  if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_t0, c->d_t1, c->d_det, c->d_mask, c->d_lab,
+                   c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp,
+                   c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
+  for (void* p : dptrs)
+    if (p) (void)hipFree(p);
+  for (void* p : c->user_allocs) (void)hipFree(p);
+  void* hptrs[] = {c->h_gauss, c->h_states, c->h_res, c->h_st, c->h_gtotal, c->h_frames};
+  for (void* p : hptrs)
+    if (p) (void)hipHostFree(p);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->s) (void)hipStreamDestroy(c->s);
+  delete c;
+  return MANTIS_OK;
+}
+
+const char* mantis_last_error(void* ctx) {
+  if (!ctx) return g_create_err.c_str();
+  return ((Ctx*)ctx)->err.c_str();
+}
+
+mantis_status mantis_set_map(void* ctx, const double* white, int32_t nw, const double* red, int32_t nr,
+                             const double* green, int32_t ng) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || nw < 0 || nr < 0 || ng < 0 || nw + nr + ng > 768 || ng > 64 || (nw && !white) || (nr && !red) ||
+      (ng && !green)) {
+    if (c) c->err = "map: need nw+nr+ng <= 768 and ng <= 64";
+    return MANTIS_ERR_ARG;
+  }
+  std::vector<double> all;
+  all.insert(all.end(), white, white + 3 * nw);
+  all.insert(all.end(), red, red + 3 * nr);
+  all.insert(all.end(), green, green + 3 * ng);
+  if (c->d_lm) (void)hipFree(c->d_lm);
+  c->d_lm = nullptr;
+  if (dalloc(c, &c->d_lm, all.size()) != MANTIS_OK) return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpy(c->d_lm, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice));
+  c->nw = nw;
+  c->nr = nr;
+  c->ng = ng;
+  return MANTIS_OK;
+}
+
+int32_t mantis_parse_coordinates(const char* s, double* xyz, int32_t max_pts) {
+  if (!s) return 0;
+  std::vector<std::string> rows;
+  std::stringstream ts(s);
+  std::string tmp;
+  while (std::getline(ts, tmp, ';')) {
+    tmp.erase(std::remove(tmp.begin(), tmp.end(), '\n'), tmp.end());
+    tmp.erase(std::remove(tmp.begin(), tmp.end(), ' '), tmp.end());
+    rows.push_back(tmp);
+  }
+  int n = 0;
+  for (auto& e : rows) {
+    std::stringstream rs(e);
+    std::string rt;
+    double v[3] = {0, 0, 0};
+    for (int k = 0; k < 3; k++) {
+      std::getline(rs, rt, ',');
+      v[k] = std::atof(rt.data());
+    }
+    if (xyz && n < max_pts) { xyz[3 * n] = v[0]; xyz[3 * n + 1] = v[1]; xyz[3 * n + 2] = v[2]; }
+    n++;
+  }
+  return n;
+}
+
+mantis_status mantis_rng_get(void* ctx, uint64_t* state) {
+  if (!ctx || !state) return MANTIS_ERR_ARG;
+  *state = ((Ctx*)ctx)->rng_state;
+  return MANTIS_OK;
+}
+mantis_status mantis_rng_set(void* ctx, uint64_t state) {
+  if (!ctx) return MANTIS_ERR_ARG;
+  ((Ctx*)ctx)->rng_state = state ? state : 0xffffffffULL;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
+                                   mantis_result* out, mantis_cam_result* cam_out) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !cams || n_rigs <= 0 || cams_per_rig <= 0) return MANTIS_ERR_ARG;
+  const int n = n_rigs * cams_per_rig;
+  mantis_status st = process_frames(c, cams, n);
+  if (st != MANTIS_OK) return st;
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  (void)per;
+  int k = 0;
+  for (int r = 0; r < n_rigs; r++) {
+    const mantis_cam_result* cr = c->h_res + (size_t)r * cams_per_rig;
+    if (out) {
+      fuse_rig(cams + (size_t)r * cams_per_rig, cr, cams_per_rig, &out[r]);
+      for (int i = 0; i < cams_per_rig; i++) k += c->h_st[r * cams_per_rig + i].reaches_pf;
+      out[r].rng_state_after = c->h_states[k];
+    }
+  }
+  if (cam_out) std::memcpy(cam_out, c->h_res, sizeof(mantis_cam_result) * n);
+  for (int f = 0; f < n; f++)
+    if (c->h_res[f].status != 0) return MANTIS_ERR_CAPACITY;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams, const mantis_motion* motion,
+                             mantis_result* out, mantis_cam_result* cam_out) {
+  (void)motion;  // delta_pos/delta_quat: the mantis3 callback does not use them
+  return mantis_process_batch(ctx, cams, 1, n_cams, out, cam_out);
+}
+
+mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !out || frame < 0 || frame >= c->F || bytes != sizeof(FrameDebug)) {
+    if (c) c->err = "mantis_get_frame_debug: bad frame or size";
+    return MANTIS_ERR_ARG;
+  }
+  HIP_OK(hipMemcpy(out, c->d_dbg + frame, sizeof(FrameDebug), hipMemcpyDeviceToHost));
+  // the host-side RNG bookkeeping completes the record
+  return MANTIS_OK;
+}
+size_t mantis_frame_debug_size(void) { return sizeof(FrameDebug); }
+
+mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !img || !canny_out) return MANTIS_ERR_ARG;
+  int W, H;
+  mantis_status st = stage_frames(c, img, 1, W, H);
+  if (st != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, 1, W, H)) != MANTIS_OK) return st;
+  HIP_OK(hipMemcpyAsync(canny_out, c->d_edge, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (size_t i = 0; i < (size_t)W * H; i++) canny_out[i] = canny_out[i] ? 255 : 0;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out, uint8_t* mask_out) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !img) return MANTIS_ERR_ARG;
+  int W, H;
+  mantis_status st = stage_frames(c, img, 1, W, H);
+  if (st != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, 1, W, H)) != MANTIS_OK) return st;
+  if (det_out) {
+    HIP_OK(hipMemcpy2DAsync(det_out, W, c->d_det + (W + 2) + 1, W + 2, W, H, hipMemcpyDeviceToHost, c->s));
+  }
+  if (mask_out) HIP_OK(hipMemcpyAsync(mask_out, c->d_mask, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (size_t i = 0; det_out && i < (size_t)W * H; i++) det_out[i] = det_out[i] ? 255 : 0;
+  for (size_t i = 0; mask_out && i < (size_t)W * H; i++) mask_out[i] = mask_out[i] ? 255 : 0;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_detect_quads(void* ctx, const mantis_image* img, int32_t* corners, int32_t max_quads,
+                                  int32_t* n_quads) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !img || !n_quads) return MANTIS_ERR_ARG;
+  int W, H;
+  mantis_status st = stage_frames(c, img, 1, W, H);
+  if (st != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, 1, W, H)) != MANTIS_OK) return st;
+  if ((st = run_contours(c, 1, W, H)) != MANTIS_OK) return st;
+  HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState), hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  if (c->h_st[0].overflow) { c->err = "detect_quads: workspace capacity exceeded"; return MANTIS_ERR_CAPACITY; }
+  int nq = c->h_st[0].n_quads;
+  *n_quads = nq;
+  if (corners && max_quads > 0) {
+    std::vector<QuadRec> q(nq);
+    HIP_OK(hipMemcpy(q.data(), c->d_quads, sizeof(QuadRec) * nq, hipMemcpyDeviceToHost));
+    for (int i = 0; i < nq && i < max_quads; i++)
+      for (int k = 0; k < 8; k++) corners[8 * i + k] = q[i].c[k];
+  }
+  return MANTIS_OK;
+}
+
+mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                      int32_t n, int32_t fast, double* err, int32_t* nproj) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !img || !c2w || n <= 0 || !err || !nproj) return MANTIS_ERR_ARG;
+  if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
+  int W, H;
+  mantis_status st = stage_frames(c, img, 1, W, H);
+  if (st != MANTIS_OK) return st;
+  double* d_c2w = nullptr;
+  double* d_err = nullptr;
+  int32_t* d_np = nullptr;
+  if (dalloc(c, &d_c2w, (size_t)12 * n) != MANTIS_OK || dalloc(c, &d_err, (size_t)n) != MANTIS_OK ||
+      dalloc(c, &d_np, (size_t)n) != MANTIS_OK)
+    return MANTIS_ERR_OOM;
+  const uint8_t* d_mask = nullptr;
+  if (mask) {
+    HIP_OK(hipMemcpyAsync(c->d_mask, mask, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+    d_mask = c->d_mask;
+  }
+  HIP_OK(hipMemcpyAsync(d_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
+  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  mark(c, "start");
+  k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, fast, d_err, d_np);
+  mark(c, "score_api");
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(err, d_err, sizeof(double) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(nproj, d_np, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  finish_profile(c);
+  (void)hipFree(d_c2w);
+  (void)hipFree(d_err);
+  (void)hipFree(d_np);
+  return MANTIS_OK;
+}
+
+mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
+                               double* t, double* errs, int32_t* rpp_status) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !img_pts || !obj_pts || n <= 0 || !R || !t || !errs || !rpp_status) return MANTIS_ERR_ARG;
+  double *d_ip, *d_op, *d_R, *d_t, *d_e;
+  int32_t* d_s;
+  if (dalloc(c, &d_ip, (size_t)8 * n) || dalloc(c, &d_op, (size_t)12 * n) || dalloc(c, &d_R, (size_t)9 * n) ||
+      dalloc(c, &d_t, (size_t)3 * n) || dalloc(c, &d_e, (size_t)2 * n) || dalloc(c, &d_s, (size_t)n))
+    return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 8 * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
+  k_rpp_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_R, d_t, d_e, d_s);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(R, d_R, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(t, d_t, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(errs, d_e, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(rpp_status, d_s, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  void* ps[] = {d_ip, d_op, d_R, d_t, d_e, d_s};
+  for (void* p : ps) (void)hipFree(p);
+  return MANTIS_OK;
+}
+
+mantis_status mantis_synth_render(void* ctx, const mantis_synth_cam* cams, int32_t n, const uint64_t* seeds,
+                                  uint8_t* out_dev) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !cams || n <= 0 || !seeds || !out_dev) return MANTIS_ERR_ARG;
+  static_assert(sizeof(mantis_synth_cam) == sizeof(mantis_synth::Cam), "synth cam layout");
+  mantis_synth::Cam* d_c;
+  uint64_t* d_s;
+  if (dalloc(c, &d_c, (size_t)n) || dalloc(c, &d_s, (size_t)n)) return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpyAsync(d_c, cams, sizeof(mantis_synth::Cam) * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_s, seeds, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->s));
+  size_t plane = (size_t)cams[0].w * cams[0].h * 3;
+  dim3 g(blocks_for((size_t)cams[0].w * cams[0].h), n);
+  k_synth<<<g, 256, 0, c->s>>>(d_c, d_s, out_dev, plane);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(c->s));
+  (void)hipFree(d_c);
+  (void)hipFree(d_s);
+  return MANTIS_OK;
+}
+
+mantis_status mantis_device_alloc(void* ctx, size_t bytes, void** dev_ptr) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !dev_ptr) return MANTIS_ERR_ARG;
+  if (hipMalloc(dev_ptr, bytes) != hipSuccess) { c->err = "hipMalloc failed"; return MANTIS_ERR_OOM; }
+  c->user_allocs.push_back(*dev_ptr);
+  return MANTIS_OK;
+}
+mantis_status mantis_device_free(void* ctx, void* dev_ptr) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  auto it = std::find(c->user_allocs.begin(), c->user_allocs.end(), dev_ptr);
+  if (it == c->user_allocs.end()) return MANTIS_ERR_ARG;
+  c->user_allocs.erase(it);
+  HIP_OK(hipFree(dev_ptr));
+  return MANTIS_OK;
+}
+mantis_status mantis_memcpy_h2d(void* ctx, void* dst, const void* src, size_t bytes) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  return MANTIS_OK;
+}
+mantis_status mantis_memcpy_d2h(void* ctx, void* dst, const void* src, size_t bytes) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  return MANTIS_OK;
+}
+mantis_status mantis_synchronize(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  HIP_OK(hipStreamSynchronize(c->s));
+  return MANTIS_OK;
+}
+int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t max) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return 0;
+  int n = (int)c->last_ms.size();
+  for (int i = 0; i < n && i < max; i++) {
+    if (names) names[i] = c->last_names[i].c_str();
+    if (ms) ms[i] = c->last_ms[i];
+  }
+  return n;
+}
+mantis_status mantis_set_profiling(void* ctx, int32_t on) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  c->prof = on != 0;
+  return MANTIS_OK;
+}
+
+}  // extern "C"
+
+#include "gn_impl.hip"

@@ -1,0 +1,1139 @@
+// HIP kernels (gfx950) of the mantis3 per-frame hot path. Host side: api.hip.
+//
+// Stage map (reference -> kernel):
+//   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_cls
+//   Canny hysteresis                 (OpenCV, [3P])                  k_uf_merge8 / k_hyst_flatten / k_hyst_edge
+//   dilate x2 / erode x1             QuadDetection.h:213-214         k_morph_h / k_morph_v
+//   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_grad_border + k_morph_*
+//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_cc_merge + k_border_emit + k_frame_contours
+//   approxPolyDP / Quadrilateral /
+//   removeDuplicateQuads / undistort QuadDetection.h:13-171, 219-228, 289-298   k_frame_contours
+//   CoPlanarPoseEstimator -> RPP     CoPlanarPoseEstimator.cpp:16-58 k_rpp
+//   generateCentralHypotheses +
+//   PoseClusterer                    HypothesisGeneration.h:57-109, PoseClusterer.cpp:33-116  k_frame_hyps
+//   evaluate / PF / shifts / yaw /
+//   publish gate                     src/mantis3.cpp:102-132          k_frame_score
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "mk_contour.h"
+#include "mk_math.h"
+#include "mk_rpp.h"
+#include "mk_sort.h"
+#include "mk_types.h"
+#include "synth.h"
+
+namespace mk {
+
+// ============================================================ image stage 1
+constexpr int TX = 64, TY = 16;
+
+__device__ inline int refl101(int i, int n) {
+  if (n == 1) return 0;
+  if (i < 0) return -i;
+  if (i >= n) return 2 * n - 2 - i;
+  return i;
+}
+
+// gray -> 3x3 Gaussian (x256 kernel [84,89,84], OpenCV <= 3.3) -> Sobel 3x3
+// (REPLICATE) -> L1 magnitude -> non-maximum suppression. cls: 0 none,
+// 1 weak candidate, 2 strong. lab: union-find init (p or -1).
+__global__ __launch_bounds__(256) void k_canny_cls(const FrameDesc* __restrict__ frames, uint8_t* __restrict__ cls,
+                                                   int32_t* __restrict__ lab, size_t plane, int low, int high) {
+  const int f = blockIdx.z;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
+  if (x0 >= W || y0 >= H) return;
+  __shared__ uint8_t g[TY + 6][TX + 6];
+  __shared__ int32_t rowb[TY + 6][TX + 4];
+  __shared__ uint8_t bl[TY + 4][TX + 4];
+  __shared__ int16_t sdx[TY + 2][TX + 2], sdy[TY + 2][TX + 2];
+  __shared__ int32_t mag[TY + 2][TX + 2];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < (TY + 6) * (TX + 6); i += 256) {
+    int ly = i / (TX + 6), lx = i % (TX + 6);
+    int x = x0 - 3 + lx, y = y0 - 3 + ly;
+    uint8_t v = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      const uint8_t* p = fd.bgr + ((size_t)y * W + x) * 3;
+      v = (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
+    }
+    g[ly][lx] = v;
+  }
+  __syncthreads();
+  // horizontal pass of the blur on rows y0-3 .. y0+TY+2, columns x0-2 .. x0+TX+1
+  for (int i = tid; i < (TY + 6) * (TX + 4); i += 256) {
+    int ly = i / (TX + 4), lx = i % (TX + 4);
+    int x = x0 - 2 + lx, y = y0 - 3 + ly;
+    int v = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      int xm = refl101(x - 1, W) - (x0 - 3), xc = x - (x0 - 3), xp = refl101(x + 1, W) - (x0 - 3);
+      v = 84 * g[ly][xm] + 89 * g[ly][xc] + 84 * g[ly][xp];
+    }
+    rowb[ly][lx] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < (TY + 4) * (TX + 4); i += 256) {
+    int ly = i / (TX + 4), lx = i % (TX + 4);
+    int x = x0 - 2 + lx, y = y0 - 2 + ly;
+    uint8_t v = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      int ym = refl101(y - 1, H) - (y0 - 3), yc = y - (y0 - 3), yp = refl101(y + 1, H) - (y0 - 3);
+      int acc = 84 * rowb[ym][lx] + 89 * rowb[yc][lx] + 84 * rowb[yp][lx];
+      int r = (acc + (1 << 15)) >> 16;
+      v = (uint8_t)(r > 255 ? 255 : (r < 0 ? 0 : r));
+    }
+    bl[ly][lx] = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < (TY + 2) * (TX + 2); i += 256) {
+    int ly = i / (TX + 2), lx = i % (TX + 2);
+    int x = x0 - 1 + lx, y = y0 - 1 + ly;
+    int gx = 0, gy = 0, m = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      auto B = [&](int xx, int yy) -> int {
+        xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
+        yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
+        return bl[yy - (y0 - 2)][xx - (x0 - 2)];
+      };
+      gx = (B(x + 1, y - 1) - B(x - 1, y - 1)) + 2 * (B(x + 1, y) - B(x - 1, y)) + (B(x + 1, y + 1) - B(x - 1, y + 1));
+      gy = (B(x - 1, y + 1) - B(x - 1, y - 1)) + 2 * (B(x, y + 1) - B(x, y - 1)) + (B(x + 1, y + 1) - B(x + 1, y - 1));
+      m = abs(gx) + abs(gy);
+    }
+    sdx[ly][lx] = (int16_t)gx;
+    sdy[ly][lx] = (int16_t)gy;
+    mag[ly][lx] = m;
+  }
+  __syncthreads();
+  const int SHIFT = 15;
+  const int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
+  uint8_t* cf = cls + (size_t)f * plane;
+  int32_t* lf = lab + (size_t)f * plane;
+  for (int i = tid; i < TY * TX; i += 256) {
+    int ly = i / TX, lx = i % TX;
+    int x = x0 + lx, y = y0 + ly;
+    if (x >= W || y >= H) continue;
+    int cy = ly + 1, cx = lx + 1;
+    int m = mag[cy][cx];
+    uint8_t c = 0;
+    if (m > low) {
+      int xs = sdx[cy][cx], ys = sdy[cy][cx];
+      int ax = abs(xs);
+      int ay = abs(ys) << SHIFT;
+      int tg22x = ax * TG22;
+      bool push;
+      if (ay < tg22x) {
+        push = m > mag[cy][cx - 1] && m >= mag[cy][cx + 1];
+      } else {
+        int tg67x = tg22x + (ax << (SHIFT + 1));
+        if (ay > tg67x) {
+          push = m > mag[cy - 1][cx] && m >= mag[cy + 1][cx];
+        } else {
+          int s = (xs ^ ys) < 0 ? -1 : 1;
+          push = m > mag[cy - 1][cx - s] && m > mag[cy + 1][cx + s];
+        }
+      }
+      if (push) c = (m > high) ? 2 : 1;
+    }
+    size_t p = (size_t)y * W + x;
+    cf[p] = c;
+    lf[p] = c ? (int32_t)p : -1;
+  }
+}
+
+// ======================================================== union-find (CCL)
+// Concurrent union by index: roots are component minima, links point to
+// smaller indices only, so finds terminate and stale reads only cost retries.
+__device__ inline int uf_find(const int32_t* lab, int x) {
+  int p;
+  while ((p = lab[x]) != x) x = p;
+  return x;
+}
+__device__ inline void uf_union(int32_t* lab, int a, int b) {
+  while (true) {
+    a = uf_find(lab, a);
+    b = uf_find(lab, b);
+    if (a == b) return;
+    if (a < b) { int t = a; a = b; b = t; }
+    int old = atomicCAS(&lab[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+// Canny hysteresis: 8-connected components of candidates (cls > 0)
+__global__ __launch_bounds__(256) void k_uf_merge8(const uint8_t* __restrict__ cls, int32_t* lab, int W, int H,
+                                                   size_t plane) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const uint8_t* c = cls + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    if (!c[p]) continue;
+    int x = (int)(p % W), y = (int)(p / W);
+    if (x > 0 && c[p - 1]) uf_union(l, (int)p, (int)p - 1);
+    if (y > 0) {
+      if (x > 0 && c[p - W - 1]) uf_union(l, (int)p, (int)(p - W - 1));
+      if (c[p - W]) uf_union(l, (int)p, (int)(p - W));
+      if (x + 1 < W && c[p - W + 1]) uf_union(l, (int)p, (int)(p - W + 1));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_hyst_flatten(const uint8_t* __restrict__ cls, int32_t* lab,
+                                                      uint8_t* __restrict__ strong, int W, int H, size_t plane) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const uint8_t* c = cls + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  uint8_t* s = strong + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    if (!c[p]) continue;
+    int r = uf_find(l, (int)p);
+    l[p] = r;
+    if (c[p] == 2) s[r] = 1;
+  }
+}
+__global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ cls, const int32_t* __restrict__ lab,
+                                                   const uint8_t* __restrict__ strong, uint8_t* __restrict__ edge,
+                                                   int W, int H, size_t plane) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const size_t o = (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    edge[o + p] = (cls[o + p] && strong[o + lab[o + p]]) ? 1 : 0;
+}
+
+// ============================================================== morphology
+// Rectangle max/min with a clipped window: equal to OpenCV's default
+// (morphologyDefaultBorderValue) and BORDER_REPLICATE borders for rects.
+// dst may be a zero-ringed padded plane (dst_pad = 1).
+__global__ __launch_bounds__(256) void k_morph_h(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W,
+                                                 int H, size_t plane, int r, int dil) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const uint8_t* s = src + (size_t)f * plane;
+  uint8_t* d = dst + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    int x = (int)(p % W);
+    size_t row = p - x;
+    int lo = x - r < 0 ? 0 : x - r, hi = x + r >= W ? W - 1 : x + r;
+    int v = dil ? 0 : 1;
+    if (dil) {
+      for (int k = lo; k <= hi; k++) v |= s[row + k];
+    } else {
+      for (int k = lo; k <= hi; k++) v &= s[row + k];
+    }
+    d[p] = (uint8_t)v;
+  }
+}
+__global__ __launch_bounds__(256) void k_morph_v(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W,
+                                                 int H, size_t plane, int r, int dil, int dst_pad) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const uint8_t* s = src + (size_t)f * plane;
+  uint8_t* d = dst + (size_t)f * plane;
+  const int Wp = W + 2;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    int x = (int)(p % W), y = (int)(p / W);
+    int lo = y - r < 0 ? 0 : y - r, hi = y + r >= H ? H - 1 : y + r;
+    int v = dil ? 0 : 1;
+    if (dil) {
+      for (int k = lo; k <= hi; k++) v |= s[(size_t)k * W + x];
+    } else {
+      for (int k = lo; k <= hi; k++) v &= s[(size_t)k * W + x];
+    }
+    if (dst_pad) d[(size_t)(y + 1) * Wp + (x + 1)] = (uint8_t)v;
+    else d[p] = (uint8_t)v;
+  }
+}
+// M0 = canny | (border pixels of NOT(morph gradient, 3x3 cross)):
+// equal to drawing every RETR_LIST contour of the inverted gradient with
+// thickness 1 (HypothesisEvaluation.h:337-351).
+__device__ inline int ng_at(const uint8_t* e, int W, int H, int x, int y) {
+  int v = e[(size_t)y * W + x];
+  int mx = v, mn = v;
+  if (x > 0) { int u = e[(size_t)y * W + x - 1]; mx |= u; mn &= u; }
+  if (x + 1 < W) { int u = e[(size_t)y * W + x + 1]; mx |= u; mn &= u; }
+  if (y > 0) { int u = e[(size_t)(y - 1) * W + x]; mx |= u; mn &= u; }
+  if (y + 1 < H) { int u = e[(size_t)(y + 1) * W + x]; mx |= u; mn &= u; }
+  return (mx == mn) ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void k_grad_border(const uint8_t* __restrict__ edge, uint8_t* __restrict__ m0,
+                                                     int W, int H, size_t plane) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)W * H;
+  const uint8_t* e = edge + (size_t)f * plane;
+  uint8_t* m = m0 + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    int x = (int)(p % W), y = (int)(p / W);
+    int b = 0;
+    if (ng_at(e, W, H, x, y)) {
+      if (x == 0 || y == 0 || x == W - 1 || y == H - 1) b = 1;
+      else if (!ng_at(e, W, H, x - 1, y) || !ng_at(e, W, H, x + 1, y) || !ng_at(e, W, H, x, y - 1) ||
+               !ng_at(e, W, H, x, y + 1))
+        b = 1;
+    }
+    m[p] = (uint8_t)(e[p] | b);
+  }
+}
+
+// ==================================================== contour components
+// On the zero-ringed detector binary (Wp x Hp): foreground 8-connected,
+// background 4-connected; the ring makes the outside background component 0.
+__global__ __launch_bounds__(256) void k_cc_init(int32_t* lab, size_t n, size_t plane) {
+  const int f = blockIdx.y;
+  int32_t* l = lab + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    l[p] = (int32_t)p;
+}
+__global__ __launch_bounds__(256) void k_cc_merge(const uint8_t* __restrict__ det, int32_t* lab, int Wp, int Hp,
+                                                  size_t plane) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)Wp * Hp;
+  const uint8_t* d = det + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    int x = (int)(p % Wp), y = (int)(p / Wp);
+    if (d[p]) {
+      if (x > 0 && d[p - 1]) uf_union(l, (int)p, (int)p - 1);
+      if (y > 0) {
+        if (x > 0 && d[p - Wp - 1]) uf_union(l, (int)p, (int)(p - Wp - 1));
+        if (d[p - Wp]) uf_union(l, (int)p, (int)(p - Wp));
+        if (x + 1 < Wp && d[p - Wp + 1]) uf_union(l, (int)p, (int)(p - Wp + 1));
+      }
+    } else {
+      if (x > 0 && !d[p - 1]) uf_union(l, (int)p, (int)p - 1);
+      if (y > 0 && !d[p - Wp]) uf_union(l, (int)p, (int)(p - Wp));
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_cc_flatten(int32_t* lab, size_t n, size_t plane) {
+  const int f = blockIdx.y;
+  int32_t* l = lab + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    l[p] = uf_find(l, (int)p);
+}
+// One border per fg component (outer, at its root) and per enclosed bg
+// component (hole, left of its root).
+__global__ __launch_bounds__(256) void k_border_emit(const uint8_t* __restrict__ det, const int32_t* __restrict__ lab,
+                                                     Border* __restrict__ borders, FrameState* st, int Wp, int Hp,
+                                                     size_t plane, int cap) {
+  const int f = blockIdx.y;
+  const size_t n = (size_t)Wp * Hp;
+  const uint8_t* d = det + (size_t)f * plane;
+  const int32_t* l = lab + (size_t)f * plane;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+    if (l[p] != (int32_t)p) continue;
+    Border b;
+    if (d[p]) {
+      b.key = (int32_t)p; b.start = (int32_t)p; b.hole = 0; b.parent = (int32_t)p;
+    } else {
+      if (p == 0) continue;
+      b.key = (int32_t)p; b.start = (int32_t)p - 1; b.hole = 1; b.parent = l[p - 1];
+    }
+    int idx = atomicAdd(&st[f].n_borders, 1);
+    if (idx < cap) borders[(size_t)f * cap + idx] = b;
+    else atomicOr(&st[f].overflow, 1);
+  }
+}
+
+// ============================================ per-frame contour -> quads
+struct ByteNZ {
+  const uint8_t* d;
+  __device__ bool operator()(int i) const { return d[i] != 0; }
+};
+struct BitNZ {
+  const uint32_t* b;
+  __device__ bool operator()(int i) const { return (b[i >> 5] >> (i & 31)) & 1u; }
+};
+
+template <class NZ>
+__device__ void contour_pass(const NZ& nz, int Wp, const Border* bs, int nb, int32_t* counts, int32_t* offs,
+                             int32_t* pool, int pool_cap, int pass) {
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const Border b = bs[i];
+    int sx = b.start % Wp, sy = b.start / Wp;
+    if (pass == 0) {
+      counts[i] = trace_border(nz, Wp, sx, sy, b.hole != 0, nullptr, 0);
+    } else {
+      int o = offs[i], c = counts[i];
+      if (o + c <= pool_cap) trace_border(nz, Wp, sx, sy, b.hole != 0, pool + 2 * (size_t)o, c);
+    }
+  }
+}
+
+// CCOMP output order (OpenCV tree pre-order): outers by key descending, each
+// followed by its holes by key descending.
+__device__ inline bool ccomp_before(int pa, int ha, int ka, int pb, int hb, int kb) {
+  if (pa != pb) return pa > pb;
+  if (ha != hb) return ha < hb;
+  return ka > kb;
+}
+
+struct RawQuad {
+  int32_t c[8];
+  int32_t parent, hole, key;
+};
+
+__global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restrict__ det, const Border* __restrict__ borders,
+                                                         FrameState* st, int32_t* __restrict__ counts,
+                                                         int32_t* __restrict__ offs, int32_t* __restrict__ pool,
+                                                         int32_t* __restrict__ scratch, int pool_cap,
+                                                         QuadRec* __restrict__ quads, FrameDebug* dbg,
+                                                         const FrameDesc* __restrict__ frames, int Wp, int Hp,
+                                                         size_t plane, int border_cap, double eps, double search_mult,
+                                                         int use_lds) {
+  extern __shared__ uint32_t bits[];
+  __shared__ int32_t scan[1024];
+  __shared__ RawQuad raw[kMaxQuads];
+  __shared__ int32_t nraw, total, nkeep;
+  __shared__ int32_t idx4[kMaxQuads][4];
+  __shared__ int32_t nbr[kMaxQuads];
+  __shared__ int32_t kpos[kMaxQuads];
+  __shared__ int32_t ord[kMaxQuads];
+  __shared__ float qcx[kMaxQuads], qcy[kMaxQuads];
+  __shared__ double qside[kMaxQuads];
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint8_t* d = det + (size_t)f * plane;
+  const Border* bs = borders + (size_t)f * border_cap;
+  int32_t* cnt = counts + (size_t)f * border_cap;
+  int32_t* off = offs + (size_t)f * border_cap;
+  int32_t* pl = pool + 2 * (size_t)f * pool_cap;
+  int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
+  int nb = st[f].n_borders;
+  if (nb > border_cap) nb = border_cap;
+  const size_t npx = (size_t)Wp * Hp;
+  if (use_lds) {
+    const size_t nw = (npx + 31) / 32;
+    for (size_t w = tid; w < nw; w += blockDim.x) {
+      uint32_t v = 0;
+      size_t base = w * 32;
+      for (int k = 0; k < 32; k++)
+        if (base + k < npx && d[base + k]) v |= 1u << k;
+      bits[w] = v;
+    }
+  }
+  if (tid == 0) { nraw = 0; total = 0; }
+  __syncthreads();
+  if (use_lds) contour_pass(BitNZ{bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
+  else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
+  __syncthreads();
+  // exclusive scan of the point counts, blockDim at a time
+  for (int base = 0; base < nb; base += blockDim.x) {
+    int i = base + tid;
+    int v = i < nb ? cnt[i] : 0;
+    scan[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+      int t = tid >= o ? scan[tid - o] : 0;
+      __syncthreads();
+      scan[tid] += t;
+      __syncthreads();
+    }
+    if (i < nb) off[i] = total + scan[tid] - v;
+    __syncthreads();
+    if (tid == blockDim.x - 1) total += scan[tid];
+    __syncthreads();
+  }
+  if (total > pool_cap) {
+    if (tid == 0) {
+      atomicOr(&st[f].overflow, 2);
+      st[f].n_points = total;
+      st[f].n_quads = 0;
+      st[f].n_raw_quads = 0;
+    }
+    return;
+  }
+  if (use_lds) contour_pass(BitNZ{bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
+  else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
+  __syncthreads();
+  // approxPolyDP per border (eps = POLYGON_EPSILON, closed); keep 4-vertex results
+  for (int i = tid; i < nb; i += blockDim.x) {
+    int o = off[i], c = cnt[i];
+    int32_t* dst = sc + 4 * (size_t)o;
+    int32_t* stk = dst + 2 * (size_t)c;
+    int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk);
+    if (m == 4) {
+      int q = atomicAdd(&nraw, 1);
+      if (q < kMaxQuads) {
+        for (int k = 0; k < 8; k++) raw[q].c[k] = dst[k];
+        raw[q].parent = bs[i].parent;
+        raw[q].hole = bs[i].hole;
+        raw[q].key = bs[i].key;
+      } else {
+        atomicOr(&st[f].overflow, 4);
+      }
+    }
+  }
+  __syncthreads();
+  const int nq = nraw < kMaxQuads ? nraw : kMaxQuads;
+  // position in the CCOMP output order (keys are distinct)
+  for (int i = tid; i < nq; i += blockDim.x) {
+    int r = 0;
+    for (int j = 0; j < nq; j++)
+      if (ccomp_before(raw[j].parent, raw[j].hole, raw[j].key, raw[i].parent, raw[i].hole, raw[i].key)) r++;
+    ord[r] = i;
+  }
+  __syncthreads();
+  // Quadrilateral(approx) (QuadDetection.h:23-61): float centre, int side
+  for (int r = tid; r < nq; r += blockDim.x) {
+    const RawQuad& q = raw[ord[r]];
+    int dx = q.c[0] - q.c[2], dy = q.c[1] - q.c[3];
+    qside[r] = sqrt((double)(dx * dx + dy * dy));
+    float xs = 0, ys = 0;
+    for (int k = 0; k < 4; k++) { xs += (float)q.c[2 * k]; ys += (float)q.c[2 * k + 1]; }
+    qcx[r] = xs / (float)4;
+    qcy[r] = ys / (float)4;
+  }
+  __syncthreads();
+  // removeDuplicateQuads (QuadDetection.h:115-171) with an exact radius
+  // search: squared float distance <= radius, the 4 smallest (dist, index)
+  // hits per query zero-padded; then the order-dependent sweep.
+  for (int i = tid; i < nq; i += blockDim.x) {
+    float radius = (float)(search_mult * qside[i]);
+    float bd[4] = {0, 0, 0, 0};
+    int bi[4] = {0, 0, 0, 0};
+    int nh = 0;
+    for (int j = 0; j < nq; j++) {
+      float d0 = qcx[j] - qcx[i], d1 = qcy[j] - qcy[i];
+      float dist = 0.0f;
+      dist += d0 * d0;
+      dist += d1 * d1;
+      if (dist <= radius) {
+        int pos = nh < 4 ? nh : 4;
+        while (pos > 0 && (dist < bd[pos - 1] || (dist == bd[pos - 1] && j < bi[pos - 1]))) {
+          if (pos < 4) { bd[pos] = bd[pos - 1]; bi[pos] = bi[pos - 1]; }
+          pos--;
+        }
+        if (pos < 4) { bd[pos] = dist; bi[pos] = j; }
+        if (nh < 4) nh++;
+      }
+    }
+    for (int k = 0; k < 4; k++) idx4[i][k] = k < nh ? bi[k] : 0;
+    nbr[i] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int i = 0; i < nq; i++) {
+      if (nbr[i]) continue;
+      for (int k = 1; k < 4; k++) nbr[idx4[i][k]] = 1;
+    }
+    int n = 0;
+    for (int i = 0; i < nq; i++) {
+      kpos[i] = nbr[i] ? -1 : n;
+      if (!nbr[i]) n++;
+    }
+    nkeep = n;
+    st[f].n_raw_quads = nraw;
+    st[f].n_quads = n;
+    st[f].n_points = total;
+    dbg[f].n_raw_quads = nraw;
+    dbg[f].n_quads = n;
+  }
+  __syncthreads();
+  const FrameDesc fd = frames[f];
+  for (int r = tid; r < nq; r += blockDim.x) {
+    int k = kpos[r];
+    if (k < 0) continue;
+    const RawQuad& rq = raw[ord[r]];
+    QuadRec q;
+    for (int c = 0; c < 8; c++) q.c[c] = rq.c[c];
+    q.parent = rq.parent; q.hole = rq.hole; q.key = rq.key; q.keep = 1;
+    q.cx = qcx[r]; q.cy = qcy[r]; q.side = qside[r];
+    for (int c = 0; c < 4; c++) {
+      // test points: float((pt - centre) * 1.3) + centre, widened to double
+      float dxf = (float)q.c[2 * c] - q.cx, dyf = (float)q.c[2 * c + 1] - q.cy;
+      float sx = (float)(dxf * 1.3), sy = (float)(dyf * 1.3);
+      double ox, oy;
+      undistort(fd.cam, (double)(sx + q.cx), (double)(sy + q.cy), &ox, &oy);
+      q.tp[2 * c] = ox;
+      q.tp[2 * c + 1] = oy;
+    }
+    quads[(size_t)f * kMaxQuads + k] = q;
+    for (int c = 0; c < 8; c++) { dbg[f].quads[k][c] = q.c[c]; dbg[f].test_pts[k][c] = q.tp[c]; }
+  }
+}
+
+// ================================================================ RPP
+// One work-item per (frame, quad, orientation); gridSquarePossibilities
+// (Mantis3Params.h:102-123): #0 CCW, #1 mirrored.
+__global__ __launch_bounds__(256, 4) void k_rpp(const QuadRec* __restrict__ quads, const FrameState* __restrict__ st,
+                                            RppOut* __restrict__ out, double half) {
+  const int f = blockIdx.y;
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = item >> 1, o = item & 1;
+  if (q >= st[f].n_quads) return;
+  const QuadRec& Q = quads[(size_t)f * kMaxQuads + q];
+  double model[12], ip[12];
+  const double sx0[4] = {half, -half, -half, half};
+  const double sy0[4] = {half, half, -half, -half};
+  const double sy1[4] = {-half, -half, half, half};
+  for (int k = 0; k < 4; k++) {
+    model[k] = sx0[k];
+    model[4 + k] = o == 0 ? sy0[k] : sy1[k];
+    model[8 + k] = 0.0;
+    ip[k] = Q.tp[2 * k];
+    ip[4 + k] = Q.tp[2 * k + 1];
+    ip[8 + k] = 1.0;
+  }
+  rpp::Result r = rpp::solve(model, ip);
+  RppOut& R = out[((size_t)f * kMaxQuads + q) * 2 + o];
+  for (int k = 0; k < 9; k++) R.R[k] = r.R[k];
+  for (int k = 0; k < 3; k++) R.t[k] = r.t[k];
+  R.img_err = r.img_err;
+  R.status = r.status;
+  R.error = r.error;
+}
+
+// ===================================== hypotheses generation + clustering
+__device__ inline Xf xf_from_rpp(const RppOut& r) {
+  Xf t;
+  for (int k = 0; k < 9; k++) t.R[k] = r.R[k];
+  for (int k = 0; k < 3; k++) t.t[k] = r.t[k];
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ rpp, FrameState* st,
+                                                    HypRec* __restrict__ gen, HypRec* __restrict__ hyps,
+                                                    FrameDebug* dbg, double max_quad_error, double max_angle) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ int32_t pass_slot[kMaxQuads];
+  __shared__ float ax[kMaxHyps], ay[kMaxHyps], az[kMaxHyps];
+  __shared__ int32_t cid[kMaxHyps];
+  __shared__ int32_t flag[kMaxHyps];
+  __shared__ int32_t csize[kMaxHyps];
+  __shared__ float cen[3];
+  __shared__ int32_t ngen_s, nclus;
+  const int nq = st[f].n_quads;
+  HypRec* G = gen + (size_t)f * kMaxHyps;
+  // per quad: orientation loop with break on camera z >= 0, gate on the last img_err
+  for (int q = tid; q < nq; q += blockDim.x) {
+    const RppOut& r0 = rpp[((size_t)f * kMaxQuads + q) * 2 + 0];
+    const RppOut& r1 = rpp[((size_t)f * kMaxQuads + q) * 2 + 1];
+    int ok = 1;
+    double err;
+    Hyp h;
+    if (r0.error == 1) {
+      ok = 0;
+      err = 0;
+    } else {
+      hyp_set_c2w(h, xf_from_rpp(r0));
+      err = r0.img_err;
+      if (!(h.w2c.t[2] >= 0)) {
+        if (r1.error == 1) ok = 0;
+        else { hyp_set_c2w(h, xf_from_rpp(r1)); err = r1.img_err; }
+      }
+    }
+    pass_slot[q] = (ok && !(err > max_quad_error)) ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int q = 0; q < nq; q++) {
+      int p = pass_slot[q];
+      pass_slot[q] = p ? n : -1;
+      n += p;
+    }
+    ngen_s = 4 * n;
+  }
+  __syncthreads();
+  const Xf rz = make_rot_z90();
+  for (int q = tid; q < nq; q += blockDim.x) {
+    int slot = pass_slot[q];
+    if (slot < 0) continue;
+    const RppOut& r0 = rpp[((size_t)f * kMaxQuads + q) * 2 + 0];
+    const RppOut& r1 = rpp[((size_t)f * kMaxQuads + q) * 2 + 1];
+    Hyp h;
+    hyp_set_c2w(h, xf_from_rpp(r0));
+    if (!(h.w2c.t[2] >= 0)) hyp_set_c2w(h, xf_from_rpp(r1));
+    for (int k = 0; k < 4; k++) {
+      if (k > 0) {
+        Hyp n2;
+        hyp_set_w2c(n2, xf_mul(rz, h.w2c));
+        h = n2;
+      }
+      HypRec& o = G[4 * slot + k];
+      o.c2w = h.c2w; o.w2c = h.w2c; o.q = h.q; o.error = 0; o.nproj = 0;
+    }
+  }
+  __syncthreads();
+  const int n = ngen_s;
+  // PoseClusterer: RPY (tf getRPY of Matrix3x3(q)) as float
+  for (int i = tid; i < n; i += blockDim.x) {
+    double m[9], r, p, y;
+    basis_from_quat(G[i].q, m);
+    basis_to_rpy(m, &r, &p, &y);
+    ax[i] = (float)r; ay[i] = (float)p; az[i] = (float)y;
+    cid[i] = -1;
+  }
+  if (tid == 0) nclus = 0;
+  __syncthreads();
+  for (int i = 0; i < n; i++) {
+    if (cid[i] >= 0) continue;  // uniform: cid[] is shared and stable here
+    // neighbours within 1.5 * radius (double distance of float differences)
+    for (int j = tid; j < n; j += blockDim.x) {
+      int hit = 0;
+      if (cid[j] < 0) {
+        double dx = ax[i] - ax[j], dy = ay[i] - ay[j], dz = az[i] - az[j];
+        hit = sqrt(dx * dx + dy * dy + dz * dz) <= max_angle * 1.5;
+      }
+      flag[j] = hit;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float cx = 0, cy = 0, cz = 0;
+      int cntm = 0;
+      for (int j = 0; j < n; j++)
+        if (flag[j]) { cx += ax[j]; cy += ay[j]; cz += az[j]; cntm++; }
+      double sz = (double)cntm;
+      cen[0] = (float)(cx / sz); cen[1] = (float)(cy / sz); cen[2] = (float)(cz / sz);
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += blockDim.x) {
+      int hit = 0;
+      if (cid[j] < 0) {
+        double dx = cen[0] - ax[j], dy = cen[1] - ay[j], dz = cen[2] - az[j];
+        hit = sqrt(dx * dx + dy * dy + dz * dz) <= max_angle;
+      }
+      flag[j] = hit;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int c = nclus, s = 0;
+      for (int j = 0; j < n; j++)
+        if (flag[j]) { cid[j] = c; s++; }
+      csize[c] = s;
+      nclus = c + 1;
+    }
+    __syncthreads();
+  }
+  __shared__ int32_t best_c, nC;
+  if (tid == 0) {
+    int b = 0;
+    for (int c = 1; c < nclus; c++)
+      if (csize[c] > csize[b]) b = c;
+    best_c = nclus > 0 ? b : -1;
+    int k = 0;
+    HypRec* Hh = hyps + (size_t)f * kMaxHyps;
+    for (int j = 0; j < n; j++)
+      if (best_c >= 0 && cid[j] == best_c) Hh[k++] = G[j];
+    nC = k;
+    st[f].n_gen = n;
+    st[f].n_hyps = k;
+    st[f].reaches_pf = (nq > 0 && k > 0) ? 1 : 0;
+    dbg[f].n_gen = n;
+    dbg[f].n_hyps = k;
+  }
+}
+
+// prefix over frames: draws of the shared cv::RNG stream happen only for
+// frames that reach the particle filter, in frame order
+__global__ void k_gauss_offsets(FrameState* st, int nf, int per_frame, int32_t* total) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int acc = 0;
+  for (int f = 0; f < nf; f++) {
+    st[f].gauss_offset = acc;
+    if (st[f].reaches_pf) acc += per_frame;
+  }
+  *total = acc;
+}
+
+// ============================================================== scoring
+struct Landmarks {
+  const double* xyz;  // n x 3 (white, red, green in map order)
+  int32_t nw, nr, ng;
+};
+
+// cleaned (mask != nullptr) or original BGR pixel, linear-offset semantics
+// for cvRound(px) == W / == H: out-of-buffer reads are 0.
+__device__ inline void fetch_px(const uint8_t* bgr, const uint8_t* mask, int W, int H, int x, int y, int& b, int& g,
+                                int& r) {
+  long lin = (long)y * W + x;
+  if (lin < 0 || lin >= (long)W * H || (mask && !mask[lin])) { b = g = r = 0; return; }
+  const uint8_t* p = bgr + 3 * lin;
+  b = p[0]; g = p[1]; r = p[2];
+}
+
+// fast error terms of one landmark: returns 1 if counted
+__device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, const uint8_t* bgr, const uint8_t* mask,
+                                int W, int H, int& e) {
+  double rp[3];
+  xf_apply(c2w, X, rp);
+  if (!(rp[2] > 0)) return 0;
+  double u, v;
+  distort(cm, rp[0], rp[1], rp[2], &u, &v);
+  if (!in_frame(u, v, H, W)) return 0;
+  int b, g, r;
+  fetch_px(bgr, mask, W, H, cv_round(u), cv_round(v), b, g, r);
+  int e0 = b - 255, e1 = g - 255, e2 = r - 255;
+  e = e0 * e0 + e1 * e1 + e2 * e2;
+  return 1;
+}
+
+// one wave scores one hypothesis over all landmarks (64 lanes, int64 sum)
+__device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
+                                       const uint8_t* mask, int W, int H, double* err_out, int* n_out) {
+  const int lane = threadIdx.x & 63;
+  long long s = 0;
+  int n = 0;
+  for (int l = lane; l < nl; l += 64) {
+    int e;
+    if (fast_term(c2w, lm + 3 * l, cm, bgr, mask, W, H, e)) { s += e; n++; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    n += __shfl_xor(n, o);
+  }
+  if (lane == 0) {
+    *n_out = n;
+    *err_out = n <= 0 ? DBL_MAX : (double)s / ((double)n * 1.1);
+  }
+}
+
+// COLOR (slow) error of one hypothesis, green landmarks, 10x10 window;
+// lanes take landmarks, lane 0 sums the per-landmark means in map order.
+__device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
+                                        const uint8_t* bgr, int W, int H, double* sh_terms, double* err_out,
+                                        int* n_out) {
+  const int lane = threadIdx.x & 63;
+  for (int base = 0; base < ngr; base += 64) {
+    int l = base + lane;
+    double term = -1.0;
+    if (l < ngr) {
+      double rp[3];
+      xf_apply(c2w, green + 3 * l, rp);
+      if (rp[2] > 0) {
+        double u, v;
+        distort(cm, rp[0], rp[1], rp[2], &u, &v);
+        if (in_frame(u, v, H, W)) {
+          double err = 0;
+          for (double ox = -5.0; ox < 5.0; ox += 1)
+            for (double oy = -5.0; oy < 5.0; oy += 1) {
+              int b, g, r;
+              fetch_px(bgr, nullptr, W, H, cv_round(u + ox), cv_round(v + oy), b, g, r);
+              int e0 = b - 50, e1 = g - 255, e2 = r - 85;
+              err += (double)(e0 * e0 + e1 * e1 + e2 * e2);
+            }
+          term = err / (double)(10 * 10);
+        }
+      }
+    }
+    if (l < ngr) sh_terms[l] = term;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __threadfence_block();
+  if (lane == 0) {
+    double total = 0;
+    int n = 0;
+    for (int l = 0; l < ngr; l++)
+      if (sh_terms[l] >= 0) { total += sh_terms[l]; n++; }
+    *n_out = n;
+    *err_out = n <= 0 ? DBL_MAX : total / ((double)n * 1.1);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+constexpr int kScoreThreads = 512;
+constexpr int kWaves = kScoreThreads / 64;
+
+struct PoseLds {
+  Xf c2w, w2c;
+  Quat q;
+  double err;
+};
+
+__global__ __launch_bounds__(kScoreThreads) void k_frame_score(
+    const FrameDesc* __restrict__ frames, const uint8_t* __restrict__ masks, size_t plane, Landmarks lmk,
+    FrameState* st, HypRec* __restrict__ hyps, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
+    FrameDebug* dbg, int particles, int iterations, double grid_spacing, int grid_size) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const uint8_t* mask = masks + (size_t)f * plane;
+  mantis_cam_result& R = res[f];
+  FrameDebug& D = dbg[f];
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  __shared__ double lm[3 * 768];
+  __shared__ PoseLds P[96];
+  __shared__ ErrIdx ei[kMaxHyps];
+  __shared__ double terms[kWaves][64];
+  __shared__ int32_t np_s[96];
+  __shared__ PoseLds cur;
+  __shared__ double shv[9];
+  __shared__ double yerr[4];
+  __shared__ int32_t nsc;
+  if (!st[f].reaches_pf) {
+    if (tid == 0) {
+      R.status = 0;
+      R.reason = st[f].n_quads == 0 ? MANTIS_NO_QUADS : MANTIS_NO_HYPS;
+      R.publish = 0;
+      R.n_quads = st[f].n_quads;
+      R.n_hyps = st[f].n_hyps;
+      R.n_scored = 0;
+      D.reason = R.reason;
+      D.publish = 0;
+    }
+    return;
+  }
+  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  __syncthreads();
+  HypRec* Hh = hyps + (size_t)f * kMaxHyps;
+  const int C = st[f].n_hyps;
+  // evaluateHypotheses(hyps, cleaned)
+  for (int h = wave; h < C; h += kWaves) {
+    double e;
+    int n;
+    wave_score_fast(Hh[h].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+    if (lane == 0) {
+      Hh[h].error = e;
+      Hh[h].nproj = n;
+      ei[h].e = e;
+      ei[h].i = h;
+      for (int k = 0; k < 9; k++) D.hyp_c2w[h][k] = Hh[h].c2w.R[k];
+      for (int k = 0; k < 3; k++) D.hyp_c2w[h][9 + k] = Hh[h].c2w.t[k];
+      D.hyp_err[h] = e;
+      D.hyp_n[h] = n;
+    }
+  }
+  __syncthreads();
+  // getBestNHypotheses(1): std::sort, keep back()
+  if (tid == 0) {
+    int bi = 0;
+    if (C > 1) {
+      std_sort_desc(ei, ei + C);
+      bi = ei[C - 1].i;
+    }
+    cur.c2w = Hh[bi].c2w; cur.w2c = Hh[bi].w2c; cur.q = Hh[bi].q; cur.err = Hh[bi].error;
+    for (int k = 0; k < 9; k++) D.best1_c2w[k] = cur.c2w.R[k];
+    for (int k = 0; k < 3; k++) D.best1_c2w[9 + k] = cur.c2w.t[k];
+    D.best1_err = cur.err;
+    D.pf_iter_err[0] = cur.err;
+    nsc = C + 1;
+  }
+  __syncthreads();
+  // optimizeHypothesisWithParticleFilter: particles are w2c_sample * rand,
+  // rand = Transform(setRPY(g,g,g), (g,g,g)) drawn yaw, pitch, roll, z, y, x.
+  const float* gs = gauss + st[f].gauss_offset;
+  for (int it = 0; it < iterations; it++) {
+    if (tid < particles) {
+      const float* g6 = gs + (size_t)(it * particles + tid) * 6;
+      double yaw = (double)g6[0] * 0.03, pitch = (double)g6[1] * 0.03, roll = (double)g6[2] * 0.03;
+      double tz = (double)g6[3] * 0.01, ty = (double)g6[4] * 0.01, tx = (double)g6[5] * 0.01;
+      Xf rnd;
+      basis_from_rpy(roll, pitch, yaw, rnd.R);
+      rnd.t[0] = tx; rnd.t[1] = ty; rnd.t[2] = tz;
+      Hyp h;
+      hyp_set_w2c(h, xf_mul(cur.w2c, rnd));
+      P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
+    }
+    __syncthreads();
+    for (int j = wave; j < particles; j += kWaves) {
+      double e;
+      int n;
+      wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+      if (lane == 0) P[j].err = e;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int j = 0; j < particles; j++)
+        if (P[j].err < cur.err) cur = P[j];
+      D.pf_iter_err[it + 1] = cur.err;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    nsc += iterations * particles;
+    for (int k = 0; k < 9; k++) D.pf_c2w[k] = cur.c2w.R[k];
+    for (int k = 0; k < 3; k++) D.pf_c2w[9 + k] = cur.c2w.t[k];
+    D.pf_err = cur.err;
+    R.pf_error = cur.err;
+    // shift values accumulate in double exactly as the reference loop does
+    double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
+    int k = 0;
+    for (; x < ((double)grid_size / 2.0) * grid_spacing && k < 9; x += grid_spacing) shv[k++] = x;
+  }
+  __syncthreads();
+  // computeAllShiftedHypothesesFAST: 81 shifted copies of the optimum
+  const int NS = 81;
+  if (tid < NS) {
+    Xf nw = cur.w2c;
+    nw.t[0] += shv[tid / 9];
+    nw.t[1] += shv[tid % 9];
+    nw.t[2] += 0.0;
+    Hyp h;
+    hyp_set_w2c(h, nw);
+    P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
+  }
+  __syncthreads();
+  for (int j = wave; j < NS; j += kWaves) {
+    double e;
+    int n;
+    wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+    if (lane == 0) { P[j].err = e; ei[j].e = e; ei[j].i = j; D.shift_err[j] = e; }
+  }
+  __syncthreads();
+  __shared__ int32_t top[20];
+  if (tid == 0) {
+    std_sort_desc(ei, ei + NS);
+    for (int k = 0; k < 20; k++) { top[k] = ei[NS - 20 + k].i; D.top20_err[k] = ei[NS - 20 + k].e; }
+    nsc += NS;
+  }
+  __syncthreads();
+  // determineBestYaw: 4 yaw sets (rotZ^k * w2c, left-multiplied), COLOR errors
+  // on the original image. P[0..19] keep the shifts; yaw sets go to P[81..]
+  // one set at a time (set k derives from set k-1).
+  __shared__ PoseLds Y[20];
+  __shared__ double ysum[4];
+  if (tid < 20) {
+    const PoseLds& s = P[top[tid]];
+    Y[tid] = s;
+  }
+  __syncthreads();
+  const Xf rz = make_rot_z90();
+  const double* green = lm + 3 * (lmk.nw + lmk.nr);
+  __shared__ double yset_err[20];
+  __shared__ PoseLds last_best[1];
+  __shared__ double best_error;
+  __shared__ int32_t best_k;
+  if (tid == 0) { best_error = DBL_MAX; best_k = -1; }
+  for (int k = 0; k < 4; k++) {
+    if (k > 0 && tid < 20) {
+      Hyp h;
+      hyp_set_w2c(h, xf_mul(rz, Y[tid].w2c));
+      Y[tid].c2w = h.c2w; Y[tid].w2c = h.w2c; Y[tid].q = h.q;
+    }
+    __syncthreads();
+    for (int j = wave; j < 20; j += kWaves) {
+      double e;
+      int n;
+      wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, terms[wave], &e, &n);
+      if (lane == 0) yset_err[j] = e;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double tot = 0;
+      int succ = 0;
+      for (int j = 0; j < 20; j++)
+        if (fabs(yset_err[j] - DBL_MAX) > 0.001) { succ++; tot += yset_err[j]; }
+      double te = succ == 0 ? DBL_MAX : tot / (double)succ;
+      yerr[k] = te;
+      D.yaw_err[k] = te;
+      if (te < best_error) {
+        best_error = te;
+        best_k = k;
+        last_best[0] = Y[19];
+        last_best[0].err = yset_err[19];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    nsc += 80;
+    double min1 = DBL_MAX, min2 = DBL_MAX;
+    for (int k = 0; k < 4; k++) {
+      double diff = yerr[k] - best_error;
+      if (diff < min1) { min2 = min1; min1 = diff; }
+      else if (diff < min2) { min2 = diff; }
+    }
+    R.status = 0;
+    R.n_quads = st[f].n_quads;
+    R.n_hyps = st[f].n_hyps;
+    R.n_scored = nsc;
+    R.min_yaw_diff = min2;
+    D.min_yaw_diff = min2;
+    D.yaw_best = best_k;
+    D.n_scored = nsc;
+    for (int i = 0; i < 36; i++) R.covariance[i] = 0;
+    if (best_k < 0) {
+      R.reason = MANTIS_NO_YAW;
+      R.publish = 0;
+      D.reason = R.reason;
+      D.publish = 0;
+    } else {
+      const PoseLds& pb = last_best[0];
+      for (int k = 0; k < 3; k++) { R.position[k] = pb.w2c.t[k]; D.position[k] = pb.w2c.t[k]; }
+      R.orientation_xyzw[0] = pb.q.x; R.orientation_xyzw[1] = pb.q.y;
+      R.orientation_xyzw[2] = pb.q.z; R.orientation_xyzw[3] = pb.q.w;
+      for (int k = 0; k < 4; k++) D.orientation_xyzw[k] = R.orientation_xyzw[k];
+      for (int k = 0; k < 9; k++) { R.c2w[k] = pb.c2w.R[k]; D.pub_c2w[k] = pb.c2w.R[k]; }
+      for (int k = 0; k < 3; k++) { R.c2w[9 + k] = pb.c2w.t[k]; D.pub_c2w[9 + k] = pb.c2w.t[k]; }
+      R.error = pb.err;
+      D.pub_error = pb.err;
+      if (min2 > 4000) {
+        double var = pb.err * (1.0 / 600.0);
+        for (int i = 0; i < 6; i++) R.covariance[i * 6 + i] = var;
+        R.publish = 1;
+        R.reason = MANTIS_PUBLISHED;
+      } else {
+        R.publish = 0;
+        R.reason = MANTIS_YAW_AMBIGUOUS;
+      }
+      for (int i = 0; i < 36; i++) D.covariance[i] = R.covariance[i];
+      D.reason = R.reason;
+      D.publish = R.publish;
+    }
+  }
+}
+
+// ================================================ standalone scoring API
+__global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__ frames, const uint8_t* mask,
+                                                   Landmarks lmk, const double* __restrict__ c2w, int n, int fast,
+                                                   double* __restrict__ err, int32_t* __restrict__ nproj) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.x * 4 + wave;
+  __shared__ double terms[4][64];
+  if (h >= n) return;
+  const FrameDesc fd = frames[0];
+  Xf T;
+  for (int k = 0; k < 9; k++) T.R[k] = c2w[12 * h + k];
+  for (int k = 0; k < 3; k++) T.t[k] = c2w[12 * h + 9 + k];
+  double e;
+  int np;
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  if (fast) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, mask, fd.w, fd.h, &e, &np);
+  else wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, terms[wave], &e, &np);
+  if (lane == 0) {
+    err[h] = e;
+    nproj[h] = np;
+  }
+}
+
+// ================================================================= RPP API
+__global__ __launch_bounds__(256, 4) void k_rpp_api(const double* __restrict__ img_pts, const double* __restrict__ obj_pts,
+                                                int n, double* R, double* t, double* errs, int32_t* status) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double model[12], ip[12];
+  for (int k = 0; k < 4; k++) {
+    model[k] = obj_pts[12 * i + 3 * k];
+    model[4 + k] = obj_pts[12 * i + 3 * k + 1];
+    model[8 + k] = obj_pts[12 * i + 3 * k + 2];
+    ip[k] = img_pts[8 * i + 2 * k];
+    ip[4 + k] = img_pts[8 * i + 2 * k + 1];
+    ip[8 + k] = 1.0;
+  }
+  rpp::Result r = rpp::solve(model, ip);
+  for (int k = 0; k < 9; k++) R[9 * i + k] = r.R[k];
+  for (int k = 0; k < 3; k++) t[3 * i + k] = r.t[k];
+  errs[2 * i] = r.obj_err;
+  errs[2 * i + 1] = r.img_err;
+  status[i] = r.error == 1 ? -1 : r.status;
+}
+
+// ============================================================ synth render
+__global__ __launch_bounds__(256) void k_synth(const mantis_synth::Cam* __restrict__ cams, const uint64_t* seeds,
+                                               uint8_t* out, size_t plane) {
+  const int f = blockIdx.y;
+  const mantis_synth::Cam c = cams[f];
+  const size_t n = (size_t)c.w * c.h;
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
+    mantis_synth::render_pixel(c, (int)(p % c.w), (int)(p / c.w), seeds[f], out + (size_t)f * plane + 3 * p);
+}
+
+}  // namespace mk

@@ -1,0 +1,163 @@
+"""GPU parity: libmantis_amd.so (HIP, gfx950) against the CPU oracle.
+
+Bar: bit-exact for integer/byte/index work (Canny, masks, quad corners,
+projection counts, integer error sums => identical fast errors); poses from
+identical decisions compared with an FP64 tolerance (1e-9 absolute) because
+device libm (atan/sin/cos/tan/sqrt) may differ from glibc by an ulp.
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+from mantis_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def mantis(landmark_map):
+    import mantis_amd as M
+
+    m = M.Mantis(max_cams=8, max_width=1280, max_height=720)
+    m.set_map(*landmark_map)
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def frames():
+    rng = np.random.default_rng(1234)
+    out = []
+    for f in range(6):
+        R, pos = synth.random_pose(rng)
+        img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(2, f))
+        out.append((img, R, pos))
+    return out
+
+
+def _img(frame):
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    return M.make_image(frame[0], K, D)
+
+
+def test_canny_bit_exact(mantis, frames):
+    for fr in frames[:3]:
+        got = mantis.canny(_img(fr))
+        ref = O.canny(fr[0])
+        assert np.array_equal(got, ref), f"canny differs at {np.argwhere(got != ref)[:10]}"
+
+
+def test_detector_binary_and_mask_bit_exact(mantis, frames):
+    for fr in frames[:3]:
+        det, mask = mantis.masks(_img(fr))
+        cn = O.canny(fr[0])
+        ref_det = O.detector_binary(cn)
+        ref_mask = O.clean_mask(cn)
+        assert np.array_equal(det, ref_det), f"detector binary differs: {np.count_nonzero(det != ref_det)} px"
+        assert np.array_equal(mask, ref_mask), f"clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
+
+
+def test_quads_bit_exact(mantis, frames, landmark_map):
+    orc = O.Oracle(*landmark_map)
+    K, D = synth.intrinsics()
+    for fr in frames[:3]:
+        got = mantis.detect_quads(_img(fr))
+        dbg = orc.process(fr[0], K, D)
+        ref = np.array(dbg.quads)[: dbg.n_quads]
+        assert got.shape == ref.shape, f"quad count {len(got)} vs oracle {len(ref)}"
+        assert np.array_equal(got, ref)
+
+
+def test_rpp_batch_matches_oracle(mantis):
+    rng = np.random.default_rng(7)
+    s = 0.16
+    sq = [np.array([[s, -s, -s, s], [s, s, -s, -s], [0, 0, 0, 0.0]]),
+          np.array([[s, -s, -s, s], [-s, -s, s, s], [0, 0, 0, 0.0]])]
+    img_pts, obj_pts, refs = [], [], []
+    for k in range(256):
+        R = synth.rot_z(rng.uniform(0, 6.28)) @ synth.NADIR @ synth.rot_x(rng.normal() * 0.3)
+        t = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(0.8, 3)])
+        m = sq[k % 2]
+        Q = R.T @ m + t[:, None]
+        ip = np.vstack([Q[0] / Q[2], Q[1] / Q[2], np.ones(4)])
+        ip[:2] += rng.normal(size=(2, 4)) * 0.003
+        img_pts.append(ip[:2].T.copy())
+        obj_pts.append(m.T.copy())
+        refs.append(O.rpp(m, ip))
+    R, t, e, st = mantis.rpp(np.array(img_pts), np.array(obj_pts))
+    for k, (rs, rR, rt, re, _) in enumerate(refs):
+        assert st[k] == rs
+        np.testing.assert_allclose(R[k], rR, atol=POSE_TOL, rtol=0)
+        np.testing.assert_allclose(t[k], rt, atol=POSE_TOL, rtol=0)
+        np.testing.assert_allclose(e[k], re[:2], rtol=1e-9, atol=1e-15)
+
+
+def test_scoring_matches_oracle(mantis, frames, landmark_map):
+    orc = O.Oracle(*landmark_map)
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(3)
+    for fr in frames[:2]:
+        img, R, pos = fr
+        base = synth.truth_c2w(R, pos)
+        c2w = [base]
+        for _ in range(255):
+            Rp = synth.rot_x(rng.normal() * 0.03) @ synth.rot_y(rng.normal() * 0.03) @ synth.rot_z(rng.normal() * 0.03)
+            Rw = R @ Rp
+            c2w.append(synth.truth_c2w(Rw, pos + rng.normal(size=3) * 0.01))
+        c2w = np.array(c2w)
+        for fast in (True, False):
+            ge, gn = mantis.score(_img(fr), c2w, fast=fast)
+            oe, on = orc.score(img, K, D, c2w, fast=fast)
+            assert np.array_equal(gn, on)
+            if fast:
+                assert np.array_equal(ge, oe), "fast errors are integer sums / (n*1.1): must be identical"
+            else:
+                np.testing.assert_allclose(ge, oe, rtol=1e-13)
+
+
+def _cmp_debug(g, o, label):
+    assert g.reason == o.reason, f"{label}: reason {g.reason} vs {o.reason}"
+    assert g.n_raw_quads == o.n_raw_quads, f"{label}: raw quads {g.n_raw_quads} vs {o.n_raw_quads}"
+    assert g.n_quads == o.n_quads
+    n = g.n_quads
+    assert np.array_equal(np.array(g.quads)[:n], np.array(o.quads)[:n])
+    np.testing.assert_allclose(np.array(g.test_pts)[:n], np.array(o.test_pts)[:n], atol=1e-12, rtol=0)
+    assert g.n_gen == o.n_gen, f"{label}: generated hyps {g.n_gen} vs {o.n_gen}"
+    assert g.n_hyps == o.n_hyps, f"{label}: clustered hyps {g.n_hyps} vs {o.n_hyps}"
+    if o.reason in (1, 2):
+        return
+    c = g.n_hyps
+    np.testing.assert_allclose(np.array(g.hyp_c2w)[:c], np.array(o.hyp_c2w)[:c], atol=POSE_TOL, rtol=0)
+    assert np.array_equal(np.array(g.hyp_n)[:c], np.array(o.hyp_n)[:c])
+    assert np.array_equal(np.array(g.hyp_err)[:c], np.array(o.hyp_err)[:c])
+    assert g.best1_err == o.best1_err
+    np.testing.assert_array_equal(np.array(g.pf_iter_err), np.array(o.pf_iter_err))
+    np.testing.assert_allclose(np.array(g.pf_c2w), np.array(o.pf_c2w), atol=POSE_TOL, rtol=0)
+    np.testing.assert_array_equal(np.array(g.shift_err), np.array(o.shift_err))
+    np.testing.assert_array_equal(np.array(g.top20_err), np.array(o.top20_err))
+    np.testing.assert_allclose(np.array(g.yaw_err), np.array(o.yaw_err), rtol=1e-12)
+    assert g.yaw_best == o.yaw_best
+    assert g.publish == o.publish
+    np.testing.assert_allclose(np.array(g.position), np.array(o.position), atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(np.array(g.orientation_xyzw), np.array(o.orientation_xyzw), atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(g.pub_error, o.pub_error, rtol=1e-12)
+
+
+def test_full_pipeline_matches_oracle(mantis, frames, landmark_map):
+    """Whole callback on a batch of frames; RNG stream shared across frames."""
+    orc = O.Oracle(*landmark_map, seed=1)
+    K, D = synth.intrinsics()
+    mantis.rng_state = 1
+    imgs = [_img(fr) for fr in frames]
+    rig, cams = mantis.process(imgs, rigs=len(imgs))
+    for i, fr in enumerate(frames):
+        o = orc.process(fr[0], K, D)
+        g = mantis.frame_debug(i)
+        _cmp_debug(g, o, f"frame {i}")
+        assert cams[i].reason == o.reason
+        assert cams[i].publish == o.publish
+    assert mantis.rng_state == orc.rng_state, "cv::RNG stream must advance exactly as the reference's"
