@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark: mantis3 rig poses/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the metric's "1280x720 4-cam batch"): rigs
+of 4 fisheye cameras at 1280x720 over the IARC-style grid, shared map
+(params/map.yaml, 720 landmarks); the full reference per-camera path
+(detector -> RPP -> clustering -> scoring -> particle filter -> shifts ->
+yaw -> publish gate) plus the rig fusion, batched `--rigs` rigs per step.
+A step = one mantis_process_batch over the batch; frames are synthetic,
+rendered once into HBM before timing (inputs resident in HBM).
+
+Multi-GPU: one process per GPU (torchrun); rigs are independent units, each
+rank processes its own batch (weak scaling, no collective on the data path);
+barrier + device sync bracket the timed region and the max time over ranks is
+reported. value = rig poses/s of the whole job.
+
+Also reported: p50 single-rig latency (host submit -> result), the dominant
+kernel's roofline (HIP events on the library stream during the timed region)
+and the CPU oracle baseline timed on this host (rank 0, N=1 only).
+"""
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
+W, H = 1280, 720
+CAMS = 4
+LANDMARKS = 720
+FLOPS_PER_PROJ = 51         # BASELINE.md roofline formulas
+FLOPS_PER_WINDOW = 200
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--rigs", type=int, default=32, help="rigs per step per GPU")
+    p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
+    p.add_argument("--latency-iters", type=int, default=15)
+    p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        tdist.init_process_group(backend=backend)
+        dist = tdist
+
+    import mantis_amd as M
+    from mantis_amd import synth
+
+    white, red, green = synth.load_map()
+    K, D = synth.intrinsics(W, H)
+    n_frames = a.rigs * CAMS
+    m = M.Mantis(M.default_config(device=local, max_cams=n_frames, max_width=W, max_height=H))
+    m.set_map(white, red, green)
+
+    # ---- synthetic rigs rendered into HBM once
+    rng = np.random.default_rng(1000 + rank)
+    ext = synth.rig_extrinsics(CAMS)
+    cams, Tbc = [], []
+    for r in range(a.distinct):
+        Twb = synth.random_base_pose(rng)
+        for c in range(CAMS):
+            Twc = Twb @ ext[c]
+            cams.append(synth.make_cam(Twc[:3, :3], Twc[:3, 3], W, H))
+            Tbc.append(ext[c])
+    nd = len(cams)
+    fb = W * H * 3
+    dev = m.device_alloc(nd * fb)
+    seeds = [synth.frame_seed(3, i + 100000 * rank) for i in range(nd)]
+    m.synth_render(cams, seeds, dev)
+    imgs = []
+    for i in range(n_frames):
+        j = i % nd
+        imgs.append(M.make_image(None, K, D, T_base_cam=Tbc[j], device_ptr=dev + j * fb, width=W, height=H))
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+        m.synchronize()
+
+    # ---- warmup
+    for _ in range(a.warmup):
+        m.process(imgs, rigs=a.rigs)
+
+    # ---- timed region: stage events on the library stream
+    m.set_profiling(True)
+    stage_ms = {}
+    scored = 0
+    published = 0
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        rig, cam = m.process(imgs, rigs=a.rigs)
+        for name, ms in m.kernel_times():
+            stage_ms[name] = stage_ms.get(name, 0.0) + ms
+        scored += sum(c.n_scored for c in cam)
+        published += sum(r.publish for r in rig)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    m.set_profiling(False)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        if torch.cuda.is_available():
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    poses = a.rigs * a.steps * world
+    value = poses / elapsed
+    ms_per_step = elapsed / a.steps * 1e3
+
+    # ---- dominant kernel roofline (per launch = per step)
+    avg = {k: v / a.steps for k, v in stage_ms.items()}
+    dom = max(avg, key=avg.get) if avg else None
+    frames_step = n_frames
+    scored_per_frame = scored / max(1, a.steps * n_frames)
+    slow_per_frame = 80.0
+    fast_per_frame = max(0.0, scored_per_frame - slow_per_frame)
+    s_fast = LANDMARKS * fast_per_frame
+    s_slow = 3700.0 * slow_per_frame
+    # algorithmic bytes per launch of each stage
+    alg_bytes = {
+        "canny_nms": frames_step * (3 * W * H + W * H),
+        "score_pf_yaw": frames_step * (3 * (s_fast + s_slow) + s_fast),
+        "contours_quads": frames_step * ((W + 2) * (H + 2)),
+        "mask_morph": frames_step * (2 * W * H),
+        "det_morph": frames_step * (2 * W * H),
+        "hysteresis": frames_step * (2 * W * H),
+        "components": frames_step * (5 * (W + 2) * (H + 2)),
+    }
+    roof = None
+    if dom:
+        dur_s = avg[dom] * 1e-3
+        b = alg_bytes.get(dom, 0.0)
+        achieved = b / dur_s / 1e9 if dur_s > 0 else 0.0
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                tj = json.load(open(pmc))
+                if tj.get("stage") == dom and tj.get("rigs") == a.rigs:
+                    traffic = tj.get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "avg_launch_ms": round(avg[dom], 4),
+                "fp64_tflops": round(frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
+                                                    FLOPS_PER_WINDOW * 37 * slow_per_frame) / dur_s / 1e12, 4)
+                if dom == "score_pf_yaw" else None,
+                "stages_ms": {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}}
+    path_bytes = frames_step * (6 * W * H + 3 * (s_fast + s_slow))
+
+    # ---- p50 latency of one rig (host submit -> result on host)
+    lat = []
+    one = imgs[:CAMS]
+    for _ in range(a.latency_iters):
+        t1 = time.perf_counter()
+        m.process(one, rigs=1)
+        lat.append(time.perf_counter() - t1)
+    p50 = float(np.median(lat)) * 1e3
+
+    # ---- CPU baseline: the oracle (C++ -O2 restatement) on a bounded sample, 1 core
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        try:
+            import _oracle as O
+
+            orc = O.Oracle(white, red, green, seed=1)
+            host = [np.zeros((H, W, 3), np.uint8) for _ in range(a.cpu_rigs * CAMS)]
+            for i in range(len(host)):
+                m.d2h(host[i], dev + (i % nd) * fb)
+            t1 = time.perf_counter()
+            for i in range(len(host)):
+                orc.process(host[i], K, D)
+            dt = time.perf_counter() - t1
+            cpu = {"value": round(a.cpu_rigs / dt, 4), "unit": "rig poses/s", "cores": 1, "kind": "port",
+                   "sample": f"{a.cpu_rigs} rigs x {CAMS} cams 1280x720 through oracle/liboracle.so "
+                             f"(full mantis3 callback per camera), {dt:.1f} s on 1 host core"}
+        except Exception as e:  # the oracle is optional on a box without it
+            cpu = {"value": None, "unit": "rig poses/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+
+    if rank == 0:
+        line = {
+            "metric": "poses/sec + p50 per-frame latency, 1280x720 4-cam batch",
+            "value": round(value, 3), "unit": "rig poses/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic fisheye grid frames rendered in HBM (SURVEY §8d scene), map.yaml landmarks",
+            "config": {"workload": "config3: 4-cam 1280x720 rig, shared map, full mantis3 path per camera",
+                       "rigs_per_step_per_gpu": a.rigs, "cams_per_rig": CAMS, "frames_per_step_per_gpu": n_frames,
+                       "resolution": [W, H], "landmarks": LANDMARKS, "parallelism": f"rig-data-parallel x{world}"},
+            "p50_latency_ms": round(p50, 3),
+            "camera_frames_per_s": round(value * CAMS, 2),
+            "published_frac": round(published / max(1, a.rigs * a.steps), 4),
+            "path_alg_GBps": round(path_bytes * a.steps / elapsed / 1e9, 3),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    m.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
