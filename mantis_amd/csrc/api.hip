@@ -118,11 +118,15 @@ struct Ctx {
   uint8_t *d_bgr = nullptr, *d_cls = nullptr, *d_strong = nullptr, *d_edge = nullptr, *d_t0 = nullptr,
           *d_t1 = nullptr, *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
+  uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
+  size_t bstride = 0;                                           // words per frame
   FrameDesc* d_frames = nullptr;
   Border* d_borders = nullptr;
   int32_t *d_bcount = nullptr, *d_boff = nullptr, *d_pool = nullptr, *d_scratch = nullptr;
   QuadRec* d_quads = nullptr;
   RppOut* d_rpp = nullptr;
+  RppItem* d_items = nullptr;
+  rpp::Refine* d_refine = nullptr;
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   FrameDebug* d_dbg = nullptr;
@@ -205,7 +209,7 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
 }
 
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
-mantis_status run_image_stages(Ctx* c, int n, int W, int H) {
+mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false) {
   const size_t P = c->plane;
   const size_t npx = (size_t)W * H;
   const int Wp = W + 2, Hp = H + 2;
@@ -218,25 +222,29 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H) {
   dim3 gp(blocks_for(npx), n);
   k_uf_merge8<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, W, H, P);
   k_hyst_flatten<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
-  k_hyst_edge<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, c->d_edge, W, H, P);
+  const size_t nw = (size_t)((W + 31) / 32) * H;
+  dim3 gw(blocks_for(nw), n);
+  const size_t B = c->bstride;
+  k_hyst_edge<<<gw, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H,
+                                    P, B);
   mark(c, "hysteresis");
-  // detector: dilate(iter 2) = 5x5 rect, erode(iter 1) = 3x3 rect
-  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_edge, c->d_t0, W, H, P, 2, 1);
-  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, 2, 1, 0);
-  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, 1, 0);
-  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_det, W, H, P, 1, 0, 1);
+  // detector: dilate(iter 2) = 5x5 rect, erode(iter 1) = 3x3 rect -> zero-ringed det bytes
+  k_bh<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B, 2, 1);
+  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, nullptr, W, H, B, P, 2, 1, 0);
+  k_bh<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, W, H, B, 1, 0);
+  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, nullptr, c->d_det, W, H, B, P, 1, 0, 2);
   mark(c, "det_morph");
-  // cleanImageByEdge mask: M0 then 3 x {dilate, erode}(3+i) and erode(3)
-  k_grad_border<<<gp, 256, 0, c->s>>>(c->d_edge, c->d_t0, W, H, P);
+  // cleanImageByEdge mask: M0 then 3 x {dilate, erode}(3+i) and erode(3) -> mask bytes
+  k_bm0<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B);
   for (int i = 0; i < 3; i++) {
-    int r = 3 + i;
-    k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, r, 1);
-    k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, r, 1, 0);
-    k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, r, 0);
-    k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_t0, W, H, P, r, 0, 0);
+    const int r = 3 + i;
+    k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, r, 1);
+    k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, nullptr, W, H, B, P, r, 1, 0);
+    k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, r, 0);
+    k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, nullptr, W, H, B, P, r, 0, 0);
   }
-  k_morph_h<<<gp, 256, 0, c->s>>>(c->d_t0, c->d_t1, W, H, P, 3, 0);
-  k_morph_v<<<gp, 256, 0, c->s>>>(c->d_t1, c->d_mask, W, H, P, 3, 0, 0);
+  k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, 3, 0);
+  k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, nullptr, c->d_mask, W, H, B, P, 3, 0, 1);
   mark(c, "mask_morph");
   (void)Wp;
   (void)Hp;
@@ -250,8 +258,10 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   const size_t np = (size_t)Wp * Hp;
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
   dim3 gp(blocks_for(np), n);
-  k_cc_init<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
-  k_cc_merge<<<gp, 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
+  dim3 gtile((Wp + CW - 1) / CW, (Hp + CH - 1) / CH, n);
+  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
+  const size_t nseam = (size_t)((Wp - 1) / CW) * Hp + (size_t)((Hp - 1) / CH) * Wp;
+  k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
   k_cc_flatten<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
   k_border_emit<<<gp, 256, 0, c->s>>>(c->d_det, c->d_lab, c->d_borders, c->d_st, Wp, Hp, P, kMaxBorders);
   mark(c, "components");
@@ -268,7 +278,11 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
 
 mantis_status run_pose(Ctx* c, int n) {
   dim3 gr((kMaxQuads * 2 + 255) / 256, n);
-  k_rpp<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_rpp, c->cfg.grid_spacing / 2);
+  k_rpp_s1<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_items, c->cfg.grid_spacing / 2);
+  const size_t ni = (size_t)n * kMaxQuads * 2;
+  k_rpp_s1b<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(c->d_items, ni);
+  k_rpp_refine<<<(unsigned)((ni * rpp::kCand + 255) / 256), 256, 0, c->s>>>(c->d_items, ni, c->d_refine);
+  k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(c->d_items, ni, c->d_refine, c->d_rpp);
   mark(c, "rpp");
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
@@ -504,6 +518,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
   c->plane = (size_t)(c->Wmax + 2) * (c->Hmax + 2);
+  c->bstride = (size_t)((c->Wmax + 31) / 32) * c->Hmax;
   c->pool_cap = cfg.max_contour_points;
   const int F = c->F;
   const int per = cfg.particles * cfg.iterations * 6;
@@ -516,6 +531,9 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_t0, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_t1, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_det, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_eb, (size_t)F * c->bstride));
+  chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
+  chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_frames, (size_t)F));
@@ -526,6 +544,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_scratch, (size_t)F * 4 * c->pool_cap));
   chk(dalloc(c, &c->d_quads, (size_t)F * kMaxQuads));
   chk(dalloc(c, &c->d_rpp, (size_t)F * kMaxQuads * 2));
+  chk(dalloc(c, &c->d_items, (size_t)F * kMaxQuads * 2));
+  chk(dalloc(c, &c->d_refine, (size_t)F * kMaxQuads * 2 * rpp::kCand));
   chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_st, (size_t)F));
@@ -565,8 +585,8 @@ mantis_status mantis_destroy(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_t0, c->d_t1, c->d_det, c->d_mask, c->d_lab,
-                   c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_t0, c->d_t1, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2,
+                   c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine,
                    c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
@@ -691,7 +711,7 @@ mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_ou
   int W, H;
   mantis_status st = stage_frames(c, img, 1, W, H);
   if (st != MANTIS_OK) return st;
-  if ((st = run_image_stages(c, 1, W, H)) != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, 1, W, H, true)) != MANTIS_OK) return st;
   HIP_OK(hipMemcpyAsync(canny_out, c->d_edge, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   for (size_t i = 0; i < (size_t)W * H; i++) canny_out[i] = canny_out[i] ? 255 : 0;
@@ -777,21 +797,31 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
                                double* t, double* errs, int32_t* rpp_status) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !img_pts || !obj_pts || n <= 0 || !R || !t || !errs || !rpp_status) return MANTIS_ERR_ARG;
-  double *d_ip, *d_op, *d_R, *d_t, *d_e;
-  int32_t* d_s;
-  if (dalloc(c, &d_ip, (size_t)8 * n) || dalloc(c, &d_op, (size_t)12 * n) || dalloc(c, &d_R, (size_t)9 * n) ||
-      dalloc(c, &d_t, (size_t)3 * n) || dalloc(c, &d_e, (size_t)2 * n) || dalloc(c, &d_s, (size_t)n))
+  double *d_ip, *d_op;
+  RppItem* d_it;
+  rpp::Refine* d_rf;
+  RppOut* d_out;
+  if (dalloc(c, &d_ip, (size_t)8 * n) || dalloc(c, &d_op, (size_t)12 * n) || dalloc(c, &d_it, (size_t)n) ||
+      dalloc(c, &d_rf, (size_t)n * rpp::kCand) || dalloc(c, &d_out, (size_t)n))
     return MANTIS_ERR_OOM;
   HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 8 * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
-  k_rpp_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_R, d_t, d_e, d_s);
+  k_rpp_s1_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it);
+  k_rpp_s1b<<<(n + 255) / 256, 256, 0, c->s>>>(d_it, n);
+  k_rpp_refine<<<(unsigned)(((size_t)n * rpp::kCand + 255) / 256), 256, 0, c->s>>>(d_it, n, d_rf);
+  k_rpp_merge<<<(n + 255) / 256, 256, 0, c->s>>>(d_it, n, d_rf, d_out);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipMemcpyAsync(R, d_R, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(t, d_t, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(errs, d_e, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(rpp_status, d_s, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->s));
+  std::vector<RppOut> h(n);
+  HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
-  void* ps[] = {d_ip, d_op, d_R, d_t, d_e, d_s};
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 9; k++) R[9 * i + k] = h[i].R[k];
+    for (int k = 0; k < 3; k++) t[3 * i + k] = h[i].t[k];
+    errs[2 * i] = h[i].obj_err;
+    errs[2 * i + 1] = h[i].img_err;
+    rpp_status[i] = h[i].error == 1 ? -1 : h[i].status;
+  }
+  void* ps[] = {d_ip, d_op, d_it, d_rf, d_out};
   for (void* p : ps) (void)hipFree(p);
   return MANTIS_OK;
 }

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <vector>
 
+#include "mk_bits.h"
 #include "mk_contour.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
@@ -109,6 +110,44 @@ int hc_find_contours(const uint8_t* bin, int w, int h, int mode, int32_t* pts, i
     off += n;
   }
   return (int)bs.size();
+}
+
+// The bit-packed detector/mask chains (what the GPU passes compute), word by word.
+void hc_masks_bits(const uint8_t* edge, int W, int H, uint8_t* det, uint8_t* mask) {
+  namespace B = mk::bits;
+  const int WW = B::words(W);
+  std::vector<uint32_t> E((size_t)WW * H, 0), a((size_t)WW * H), b((size_t)WW * H);
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++)
+      if (edge[(size_t)y * W + x]) E[(size_t)y * WW + (x >> 5)] |= 1u << (x & 31);
+  auto hpass = [&](const std::vector<uint32_t>& src, std::vector<uint32_t>& dst, int r, bool dil) {
+    for (int y = 0; y < H; y++)
+      for (int w = 0; w < WW; w++) dst[(size_t)y * WW + w] = B::hword(src.data() + (size_t)y * WW, w, W, r, dil);
+  };
+  auto vpass = [&](const std::vector<uint32_t>& src, std::vector<uint32_t>& dst, int r, bool dil) {
+    for (int y = 0; y < H; y++)
+      for (int w = 0; w < WW; w++) dst[(size_t)y * WW + w] = B::vword(src.data(), w, y, W, H, r, dil);
+  };
+  auto unpack = [&](const std::vector<uint32_t>& src, uint8_t* out) {
+    for (int y = 0; y < H; y++)
+      for (int x = 0; x < W; x++) out[(size_t)y * W + x] = (src[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
+  };
+  hpass(E, a, 2, true);
+  vpass(a, b, 2, true);
+  hpass(b, a, 1, false);
+  vpass(a, b, 1, false);
+  unpack(b, det);
+  for (int y = 0; y < H; y++)
+    for (int w = 0; w < WW; w++) a[(size_t)y * WW + w] = B::m0word(E.data(), w, y, W, H);
+  for (int i = 0; i < 3; i++) {
+    hpass(a, b, 3 + i, true);
+    vpass(b, a, 3 + i, true);
+    hpass(a, b, 3 + i, false);
+    vpass(b, a, 3 + i, false);
+  }
+  hpass(a, b, 3, false);
+  vpass(b, a, 3, false);
+  unpack(a, mask);
 }
 
 void hc_distort(const double* xyz, int n, const double* K, const double* D, double* px) {

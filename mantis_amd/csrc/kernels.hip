@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <cstdint>
 
+#include "mk_bits.h"
 #include "mk_contour.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
@@ -196,117 +197,210 @@ __global__ __launch_bounds__(256) void k_hyst_flatten(const uint8_t* __restrict_
     if (c[p] == 2) s[r] = 1;
   }
 }
+// edge = candidate whose component holds a strong pixel, written as a
+// bit plane (one 32-pixel word per work-item) and optionally as bytes
 __global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ cls, const int32_t* __restrict__ lab,
-                                                   const uint8_t* __restrict__ strong, uint8_t* __restrict__ edge,
-                                                   int W, int H, size_t plane) {
+                                                   const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
+                                                   uint8_t* __restrict__ edge, int W, int H, size_t plane,
+                                                   size_t bstride) {
   const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
+  const int WW = bits::words(W);
+  const size_t n = (size_t)WW * H;
   const size_t o = (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
-    edge[o + p] = (cls[o + p] && strong[o + lab[o + p]]) ? 1 : 0;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(k % WW), y = (int)(k / WW);
+    const int xe = min(32, W - 32 * w);
+    const size_t p0 = o + (size_t)y * W + 32 * w;
+    uint32_t word = 0;
+    for (int b = 0; b < xe; b++) {
+      const uint32_t e = (cls[p0 + b] && strong[o + lab[p0 + b]]) ? 1u : 0u;
+      word |= e << b;
+      if (edge) edge[p0 + b] = (uint8_t)e;
+    }
+    ebits[(size_t)f * bstride + k] = word;
+  }
 }
 
 // ============================================================== morphology
-// Rectangle max/min with a clipped window: equal to OpenCV's default
-// (morphologyDefaultBorderValue) and BORDER_REPLICATE borders for rects.
-// dst may be a zero-ringed padded plane (dst_pad = 1).
-__global__ __launch_bounds__(256) void k_morph_h(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W,
-                                                 int H, size_t plane, int r, int dil) {
+// Bit-packed rectangle dilate/erode passes and the cleanImageByEdge M0 plane
+// (mk_bits.h); one 32-pixel word per work-item.
+__global__ __launch_bounds__(256) void k_bh(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W, int H,
+                                            size_t bstride, int r, int dil) {
   const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
-  const uint8_t* s = src + (size_t)f * plane;
-  uint8_t* d = dst + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    int x = (int)(p % W);
-    size_t row = p - x;
-    int lo = x - r < 0 ? 0 : x - r, hi = x + r >= W ? W - 1 : x + r;
-    int v = dil ? 0 : 1;
-    if (dil) {
-      for (int k = lo; k <= hi; k++) v |= s[row + k];
-    } else {
-      for (int k = lo; k <= hi; k++) v &= s[row + k];
-    }
-    d[p] = (uint8_t)v;
+  const int WW = bits::words(W);
+  const size_t n = (size_t)WW * H;
+  const uint32_t* s = src + (size_t)f * bstride;
+  uint32_t* d = dst + (size_t)f * bstride;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(k % WW), y = (int)(k / WW);
+    d[k] = bits::hword(s + (size_t)y * WW, w, W, r, dil != 0);
   }
 }
-__global__ __launch_bounds__(256) void k_morph_v(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W,
-                                                 int H, size_t plane, int r, int dil, int dst_pad) {
+// mode 0: bits to dst; 1: bytes to out (W x H); 2: bytes into the interior of
+// the zero-ringed (W+2) x (H+2) plane out
+__global__ __launch_bounds__(256) void k_bv(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                            uint8_t* __restrict__ out, int W, int H, size_t bstride, size_t plane,
+                                            int r, int dil, int mode) {
   const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
-  const uint8_t* s = src + (size_t)f * plane;
-  uint8_t* d = dst + (size_t)f * plane;
-  const int Wp = W + 2;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    int x = (int)(p % W), y = (int)(p / W);
-    int lo = y - r < 0 ? 0 : y - r, hi = y + r >= H ? H - 1 : y + r;
-    int v = dil ? 0 : 1;
-    if (dil) {
-      for (int k = lo; k <= hi; k++) v |= s[(size_t)k * W + x];
+  const int WW = bits::words(W);
+  const size_t n = (size_t)WW * H;
+  const uint32_t* s = src + (size_t)f * bstride;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(k % WW), y = (int)(k / WW);
+    const uint32_t v = bits::vword(s, w, y, W, H, r, dil != 0);
+    if (mode == 0) {
+      dst[(size_t)f * bstride + k] = v;
     } else {
-      for (int k = lo; k <= hi; k++) v &= s[(size_t)k * W + x];
+      uint8_t* o = out + (size_t)f * plane +
+                   (mode == 1 ? (size_t)y * W + 32 * w : (size_t)(y + 1) * (W + 2) + 1 + 32 * w);
+      const int xe = min(32, W - 32 * w);
+      for (int b = 0; b < xe; b++) o[b] = (uint8_t)((v >> b) & 1u);
     }
-    if (dst_pad) d[(size_t)(y + 1) * Wp + (x + 1)] = (uint8_t)v;
-    else d[p] = (uint8_t)v;
   }
 }
-// M0 = canny | (border pixels of NOT(morph gradient, 3x3 cross)):
-// equal to drawing every RETR_LIST contour of the inverted gradient with
-// thickness 1 (HypothesisEvaluation.h:337-351).
-__device__ inline int ng_at(const uint8_t* e, int W, int H, int x, int y) {
-  int v = e[(size_t)y * W + x];
-  int mx = v, mn = v;
-  if (x > 0) { int u = e[(size_t)y * W + x - 1]; mx |= u; mn &= u; }
-  if (x + 1 < W) { int u = e[(size_t)y * W + x + 1]; mx |= u; mn &= u; }
-  if (y > 0) { int u = e[(size_t)(y - 1) * W + x]; mx |= u; mn &= u; }
-  if (y + 1 < H) { int u = e[(size_t)(y + 1) * W + x]; mx |= u; mn &= u; }
-  return (mx == mn) ? 1 : 0;
-}
-__global__ __launch_bounds__(256) void k_grad_border(const uint8_t* __restrict__ edge, uint8_t* __restrict__ m0,
-                                                     int W, int H, size_t plane) {
+__global__ __launch_bounds__(256) void k_bm0(const uint32_t* __restrict__ E, uint32_t* __restrict__ dst, int W, int H,
+                                             size_t bstride) {
   const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
-  const uint8_t* e = edge + (size_t)f * plane;
-  uint8_t* m = m0 + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    int x = (int)(p % W), y = (int)(p / W);
-    int b = 0;
-    if (ng_at(e, W, H, x, y)) {
-      if (x == 0 || y == 0 || x == W - 1 || y == H - 1) b = 1;
-      else if (!ng_at(e, W, H, x - 1, y) || !ng_at(e, W, H, x + 1, y) || !ng_at(e, W, H, x, y - 1) ||
-               !ng_at(e, W, H, x, y + 1))
-        b = 1;
-    }
-    m[p] = (uint8_t)(e[p] | b);
+  const int WW = bits::words(W);
+  const size_t n = (size_t)WW * H;
+  const uint32_t* e = E + (size_t)f * bstride;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(k % WW), y = (int)(k / WW);
+    dst[(size_t)f * bstride + k] = bits::m0word(e, w, y, W, H);
   }
 }
 
 // ==================================================== contour components
 // On the zero-ringed detector binary (Wp x Hp): foreground 8-connected,
 // background 4-connected; the ring makes the outside background component 0.
-__global__ __launch_bounds__(256) void k_cc_init(int32_t* lab, size_t n, size_t plane) {
-  const int f = blockIdx.y;
-  int32_t* l = lab + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
-    l[p] = (int32_t)p;
+// Labels end as the component's minimum padded index. Three launches:
+//   k_cc_tile  64x32 tiles, union-find in LDS (row runs first, redundant
+//              unions skipped), each pixel labelled with its tile-local root
+//   k_cc_seam  unions across tile seams only, global union-find
+//   k_cc_flatten  every pixel -> its global root
+constexpr int CW = 64, CH = 32;
+
+// find with path halving: only non-roots are rewritten (with an ancestor),
+// roots change only through the CAS in uf_union, so this is race-safe
+__device__ inline int uf_find_c(int32_t* lab, int x) {
+  while (true) {
+    int p = lab[x];
+    if (p == x) return x;
+    int g = lab[p];
+    if (g == p) return p;
+    lab[x] = g;
+    x = g;
+  }
 }
-__global__ __launch_bounds__(256) void k_cc_merge(const uint8_t* __restrict__ det, int32_t* lab, int Wp, int Hp,
-                                                  size_t plane) {
-  const int f = blockIdx.y;
-  const size_t n = (size_t)Wp * Hp;
+__device__ inline void uf_union_c(int32_t* lab, int a, int b) {
+  while (true) {
+    a = uf_find_c(lab, a);
+    b = uf_find_c(lab, b);
+    if (a == b) return;
+    if (a < b) { int t = a; a = b; b = t; }
+    int old = atomicCAS(&lab[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+__device__ inline int lds_find(const int* L, int x) {
+  int p;
+  while ((p = L[x]) != x) x = p;
+  return x;
+}
+__device__ inline void lds_union(int* L, int a, int b) {
+  while (true) {
+    a = lds_find(L, a);
+    b = lds_find(L, b);
+    if (a == b) return;
+    if (a < b) { int t = a; a = b; b = t; }
+    int old = atomicCAS(&L[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cc_tile(const uint8_t* __restrict__ det, int32_t* __restrict__ lab, int Wp,
+                                                 int Hp, size_t plane) {
+  __shared__ uint8_t C[CH * CW];  // 0 background, 1 foreground, 2 outside the image
+  __shared__ int L[CH * CW];
+  const int f = blockIdx.z;
+  const int x0 = blockIdx.x * CW, y0 = blockIdx.y * CH;
   const uint8_t* d = det + (size_t)f * plane;
   int32_t* l = lab + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    int x = (int)(p % Wp), y = (int)(p / Wp);
-    if (d[p]) {
-      if (x > 0 && d[p - 1]) uf_union(l, (int)p, (int)p - 1);
-      if (y > 0) {
-        if (x > 0 && d[p - Wp - 1]) uf_union(l, (int)p, (int)(p - Wp - 1));
-        if (d[p - Wp]) uf_union(l, (int)p, (int)(p - Wp));
-        if (x + 1 < Wp && d[p - Wp + 1]) uf_union(l, (int)p, (int)(p - Wp + 1));
+  const int t = threadIdx.x;
+  for (int i = t; i < CH * CW; i += 256) {
+    const int x = x0 + (i % CW), y = y0 + (i / CW);
+    C[i] = (x < Wp && y < Hp) ? (d[(size_t)y * Wp + x] ? 1 : 0) : 2;
+  }
+  __syncthreads();
+  {  // row runs: 8 threads per row, 8 pixels each, sequential within the segment
+    const int base = (t >> 3) * CW + (t & 7) * 8;
+    int run = base;
+    L[base] = base;
+    for (int k = 1; k < 8; k++) {
+      const int i = base + k;
+      if (C[i] != C[i - 1]) run = i;
+      L[i] = run;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < CH * CW; i += 256) {
+    const int c = C[i];
+    if (c == 2) continue;
+    const int lx = i % CW, ly = i / CW;
+    const int left = lx > 0 ? C[i - 1] : 3;
+    if ((lx & 7) == 0 && left == c) lds_union(L, i, i - 1);
+    if (ly == 0) continue;
+    const int up = C[i - CW];
+    const int upl = lx > 0 ? C[i - CW - 1] : 3;
+    if (c == 1) {
+      if (up == 1) {
+        if (!(left == 1 && upl == 1)) lds_union(L, i, i - CW);
+      } else {
+        if (upl == 1 && left != 1) lds_union(L, i, i - CW - 1);
+        if (lx + 1 < CW && C[i - CW + 1] == 1) lds_union(L, i, i - CW + 1);
+      }
+    } else if (up == 0) {
+      if (!(left == 0 && upl == 0)) lds_union(L, i, i - CW);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < CH * CW; i += 256) {
+    if (C[i] == 2) continue;
+    const int r = lds_find(L, i);
+    const int x = x0 + (i % CW), y = y0 + (i / CW);
+    l[(size_t)y * Wp + x] = (y0 + r / CW) * Wp + x0 + (r % CW);
+  }
+}
+
+// one thread per seam pixel: vertical seams (x = k*CW) then horizontal (y = k*CH)
+__global__ __launch_bounds__(256) void k_cc_seam(const uint8_t* __restrict__ det, int32_t* lab, int Wp, int Hp,
+                                                 size_t plane) {
+  const int f = blockIdx.y;
+  const uint8_t* d = det + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  const int nvs = (Wp - 1) / CW, nhs = (Hp - 1) / CH;
+  const size_t nv = (size_t)nvs * Hp, n = nv + (size_t)nhs * Wp;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    int x, y;
+    const bool vert = k < nv;
+    if (vert) { x = (int)(k / Hp + 1) * CW; y = (int)(k % Hp); }
+    else { const size_t h = k - nv; y = (int)(h / Wp + 1) * CH; x = (int)(h % Wp); }
+    const int p = y * Wp + x;
+    const int c = d[p] ? 1 : 0;
+    if (vert) {
+      if ((d[p - 1] ? 1 : 0) == c) uf_union_c(l, p, p - 1);
+      if (c) {
+        if (y > 0 && d[p - Wp - 1]) uf_union_c(l, p, p - Wp - 1);
+        if (y + 1 < Hp && d[p + Wp - 1]) uf_union_c(l, p, p + Wp - 1);
       }
     } else {
-      if (x > 0 && !d[p - 1]) uf_union(l, (int)p, (int)p - 1);
-      if (y > 0 && !d[p - Wp]) uf_union(l, (int)p, (int)(p - Wp));
+      if ((d[p - Wp] ? 1 : 0) == c) uf_union_c(l, p, p - Wp);
+      if (c) {
+        if (x > 0 && d[p - Wp - 1]) uf_union_c(l, p, p - Wp - 1);
+        if (x + 1 < Wp && d[p - Wp + 1]) uf_union_c(l, p, p - Wp + 1);
+      }
     }
   }
 }
@@ -314,7 +408,7 @@ __global__ __launch_bounds__(256) void k_cc_flatten(int32_t* lab, size_t n, size
   const int f = blockIdx.y;
   int32_t* l = lab + (size_t)f * plane;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
-    l[p] = uf_find(l, (int)p);
+    l[p] = uf_find_c(l, l[p]);
 }
 // One border per fg component (outer, at its root) and per enclosed bg
 // component (hole, left of its root).
@@ -386,7 +480,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
                                                          const FrameDesc* __restrict__ frames, int Wp, int Hp,
                                                          size_t plane, int border_cap, double eps, double search_mult,
                                                          int use_lds) {
-  extern __shared__ uint32_t bits[];
+  extern __shared__ uint32_t lds_bits[];
   __shared__ int32_t scan[1024];
   __shared__ RawQuad raw[kMaxQuads];
   __shared__ int32_t nraw, total, nkeep;
@@ -414,12 +508,12 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
       size_t base = w * 32;
       for (int k = 0; k < 32; k++)
         if (base + k < npx && d[base + k]) v |= 1u << k;
-      bits[w] = v;
+      lds_bits[w] = v;
     }
   }
   if (tid == 0) { nraw = 0; total = 0; }
   __syncthreads();
-  if (use_lds) contour_pass(BitNZ{bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
+  if (use_lds) contour_pass(BitNZ{lds_bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
   else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
   __syncthreads();
   // exclusive scan of the point counts, blockDim at a time
@@ -448,7 +542,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
     }
     return;
   }
-  if (use_lds) contour_pass(BitNZ{bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
+  if (use_lds) contour_pass(BitNZ{lds_bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
   else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
   __syncthreads();
   // approxPolyDP per border (eps = POLYGON_EPSILON, closed); keep 4-vertex results
@@ -559,19 +653,31 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
 }
 
 // ================================================================ RPP
-// One work-item per (frame, quad, orientation); gridSquarePossibilities
-// (Mantis3Params.h:102-123): #0 CCW, #1 mirrored.
-__global__ __launch_bounds__(256, 4) void k_rpp(const QuadRec* __restrict__ quads, const FrameState* __restrict__ st,
-                                            RppOut* __restrict__ out, double half) {
+// Three phases (mk_rpp.h): stage1 per (frame, quad, orientation) — the first
+// ObjPose and the 2nd-pose candidates; refine per (item, candidate); merge per
+// item. Items are independent; the split keeps every phase's live state in
+// registers and runs the candidate ObjPoses in parallel.
+// gridSquarePossibilities (Mantis3Params.h:102-123): #0 CCW, #1 mirrored.
+struct RppItem {
+  rpp::Stage1 s;
+  double P[12];
+  int32_t active, pad;
+};
+
+__global__ __launch_bounds__(256, 2) void k_rpp_s1(const QuadRec* __restrict__ quads, const FrameState* __restrict__ st,
+                                               RppItem* __restrict__ items, double half) {
   const int f = blockIdx.y;
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= kMaxQuads * 2) return;
   const int q = item >> 1, o = item & 1;
-  if (q >= st[f].n_quads) return;
+  RppItem& it = items[(size_t)f * kMaxQuads * 2 + item];
+  if (q >= st[f].n_quads) { it.active = 0; return; }
   const QuadRec& Q = quads[(size_t)f * kMaxQuads + q];
   double model[12], ip[12];
   const double sx0[4] = {half, -half, -half, half};
   const double sy0[4] = {half, half, -half, -half};
   const double sy1[4] = {-half, -half, half, half};
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     model[k] = sx0[k];
     model[4 + k] = o == 0 ? sy0[k] : sy1[k];
@@ -580,13 +686,73 @@ __global__ __launch_bounds__(256, 4) void k_rpp(const QuadRec* __restrict__ quad
     ip[4 + k] = Q.tp[2 * k + 1];
     ip[8 + k] = 1.0;
   }
-  rpp::Result r = rpp::solve(model, ip);
-  RppOut& R = out[((size_t)f * kMaxQuads + q) * 2 + o];
+  rpp::stage1a(model, ip, it.s);
+#pragma unroll
+  for (int k = 0; k < 12; k++) it.P[k] = model[k];
+  it.active = 1;
+}
+
+__global__ __launch_bounds__(256, 2) void k_rpp_s1_api(const double* __restrict__ img_pts,
+                                                   const double* __restrict__ obj_pts, int n,
+                                                   RppItem* __restrict__ items) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double model[12], ip[12];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    model[k] = obj_pts[12 * i + 3 * k];
+    model[4 + k] = obj_pts[12 * i + 3 * k + 1];
+    model[8 + k] = obj_pts[12 * i + 3 * k + 2];
+    ip[k] = img_pts[8 * i + 2 * k];
+    ip[4 + k] = img_pts[8 * i + 2 * k + 1];
+    ip[8 + k] = 1.0;
+  }
+  rpp::stage1a(model, ip, items[i].s);
+#pragma unroll
+  for (int k = 0; k < 12; k++) items[i].P[k] = model[k];
+  items[i].active = 1;
+}
+
+// Get2ndPose setup (candidate rotations from the quartic) per active item
+__global__ __launch_bounds__(256, 2) void k_rpp_s1b(RppItem* __restrict__ items, size_t n_items) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items || !items[i].active) return;
+  double model[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) model[k] = items[i].P[k];
+  rpp::stage1b(model, items[i].s);
+}
+
+// one work-item per (item, candidate slot)
+__global__ __launch_bounds__(256, 2) void k_rpp_refine(const RppItem* __restrict__ items, size_t n_items,
+                                                   rpp::Refine* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items * rpp::kCand) return;
+  const size_t p = i / rpp::kCand;
+  const int j = (int)(i - p * rpp::kCand);
+  const RppItem& it = items[p];
+  if (!it.active || it.s.error == 1 || !((it.s.keep_mask >> j) & 1)) return;
+  double model[12], Q[12], sR[9];
+#pragma unroll
+  for (int k = 0; k < 12; k++) { model[k] = it.P[k]; Q[k] = it.s.Q[k]; }
+#pragma unroll
+  for (int k = 0; k < 9; k++) sR[k] = it.s.sR[j][k];
+  rpp::refine(model, Q, sR, out[i]);
+}
+
+__global__ __launch_bounds__(256) void k_rpp_merge(const RppItem* __restrict__ items, size_t n_items,
+                                                   const rpp::Refine* __restrict__ rf, RppOut* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items || !items[i].active) return;
+  rpp::Result r = rpp::merge(items[i].s, rf + i * rpp::kCand);
+  RppOut& R = out[i];
   for (int k = 0; k < 9; k++) R.R[k] = r.R[k];
   for (int k = 0; k < 3; k++) R.t[k] = r.t[k];
   R.img_err = r.img_err;
+  R.obj_err = r.obj_err;
   R.status = r.status;
   R.error = r.error;
+  R.iterations = r.iterations;
 }
 
 // ===================================== hypotheses generation + clustering
@@ -1102,28 +1268,6 @@ __global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__
     err[h] = e;
     nproj[h] = np;
   }
-}
-
-// ================================================================= RPP API
-__global__ __launch_bounds__(256, 4) void k_rpp_api(const double* __restrict__ img_pts, const double* __restrict__ obj_pts,
-                                                int n, double* R, double* t, double* errs, int32_t* status) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double model[12], ip[12];
-  for (int k = 0; k < 4; k++) {
-    model[k] = obj_pts[12 * i + 3 * k];
-    model[4 + k] = obj_pts[12 * i + 3 * k + 1];
-    model[8 + k] = obj_pts[12 * i + 3 * k + 2];
-    ip[k] = img_pts[8 * i + 2 * k];
-    ip[4 + k] = img_pts[8 * i + 2 * k + 1];
-    ip[8 + k] = 1.0;
-  }
-  rpp::Result r = rpp::solve(model, ip);
-  for (int k = 0; k < 9; k++) R[9 * i + k] = r.R[k];
-  for (int k = 0; k < 3; k++) t[3 * i + k] = r.t[k];
-  errs[2 * i] = r.obj_err;
-  errs[2 * i + 1] = r.img_err;
-  status[i] = r.error == 1 ? -1 : r.status;
 }
 
 // ============================================================ synth render

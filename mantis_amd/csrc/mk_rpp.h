@@ -431,28 +431,34 @@ MK_HD int rpoly(const double* op, int degree, double* zeror, double* zeroi) {
 }
 
 // ---------------------------------------------------------------- JacobiSVD
-// OpenCV JacobiSVDImpl_ on At (n rows of length m), eps = 10 DBL_EPSILON,
-// minval = DBL_MIN, null singular vectors from cv::RNG(0x12345678).
-MK_HD void jacobi_svd(double* At, int m, int n, double* Wout, double* Vt, int n1) {
+// Compile-time sizes throughout so every matrix stays in VGPRs (no scratch):
+// At is N rows of length M (A^T), W the N singular values, Vt N x N.
+template <int M, int N>
+MK_HD void jacobi_svd(double (&At)[N * M], double (&Wout)[N], double* Vt) {
   const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
-  double W[3];
-  int max_iter = m > 30 ? m : 30;
-  for (int i = 0; i < n; i++) {
+  double W[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
     double sd = 0;
-    for (int k = 0; k < m; k++) { double t = At[i * m + k]; sd += t * t; }
+#pragma unroll
+    for (int k = 0; k < M; k++) { double t = At[i * M + k]; sd += t * t; }
     W[i] = sd;
     if (Vt) {
-      for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
-      Vt[i * n + i] = 1;
+#pragma unroll
+      for (int k = 0; k < N; k++) Vt[i * N + k] = (k == i) ? 1.0 : 0.0;
     }
   }
+  const int max_iter = M > 30 ? M : 30;
+#pragma unroll 1
   for (int iter = 0; iter < max_iter; iter++) {
     bool changed = false;
-    for (int i = 0; i < n - 1; i++)
-      for (int j = i + 1; j < n; j++) {
-        double *Ai = At + i * m, *Aj = At + j * m;
+#pragma unroll
+    for (int i = 0; i < N - 1; i++)
+#pragma unroll
+      for (int j = i + 1; j < N; j++) {
         double a = W[i], p = 0, b = W[j];
-        for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+#pragma unroll
+        for (int k = 0; k < M; k++) p += At[i * M + k] * At[j * M + k];
         if (fabs(p) <= eps * sqrt(a * b)) continue;
         p *= 2;
         double beta = a - b, gamma = hypot(p, beta), c, s;
@@ -465,202 +471,301 @@ MK_HD void jacobi_svd(double* At, int m, int n, double* Wout, double* Vt, int n1
           s = p / (gamma * c * 2);
         }
         a = b = 0;
-        for (int k = 0; k < m; k++) {
-          double t0 = c * Ai[k] + s * Aj[k];
-          double t1 = -s * Ai[k] + c * Aj[k];
-          Ai[k] = t0; Aj[k] = t1;
+#pragma unroll
+        for (int k = 0; k < M; k++) {
+          double t0 = c * At[i * M + k] + s * At[j * M + k];
+          double t1 = -s * At[i * M + k] + c * At[j * M + k];
+          At[i * M + k] = t0; At[j * M + k] = t1;
           a += t0 * t0; b += t1 * t1;
         }
         W[i] = a; W[j] = b;
         changed = true;
         if (Vt) {
-          double *Vi = Vt + i * n, *Vj = Vt + j * n;
-          for (int k = 0; k < n; k++) {
-            double t0 = c * Vi[k] + s * Vj[k];
-            double t1 = -s * Vi[k] + c * Vj[k];
-            Vi[k] = t0; Vj[k] = t1;
+#pragma unroll
+          for (int k = 0; k < N; k++) {
+            double t0 = c * Vt[i * N + k] + s * Vt[j * N + k];
+            double t1 = -s * Vt[i * N + k] + c * Vt[j * N + k];
+            Vt[i * N + k] = t0; Vt[j * N + k] = t1;
           }
         }
       }
     if (!changed) break;
   }
-  for (int i = 0; i < n; i++) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
     double sd = 0;
-    for (int k = 0; k < m; k++) { double t = At[i * m + k]; sd += t * t; }
+#pragma unroll
+    for (int k = 0; k < M; k++) { double t = At[i * M + k]; sd += t * t; }
     W[i] = sqrt(sd);
   }
-  for (int i = 0; i < n - 1; i++) {
+  // selection sort by descending W; the swap partner is chosen with
+  // predicates so every index stays a compile-time constant
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) {
     int j = i;
-    for (int k = i + 1; k < n; k++) if (W[j] < W[k]) j = k;
-    if (i != j) {
-      swp(W[i], W[j]);
-      if (Vt) {
-        for (int k = 0; k < m; k++) swp(At[i * m + k], At[j * m + k]);
-        for (int k = 0; k < n; k++) swp(Vt[i * n + k], Vt[j * n + k]);
+    double wj = W[i];
+#pragma unroll
+    for (int k = i + 1; k < N; k++)
+      if (wj < W[k]) { j = k; wj = W[k]; }
+#pragma unroll
+    for (int k = i + 1; k < N; k++) {
+      if (j == k) {
+        swp(W[i], W[k]);
+        if (Vt) {
+#pragma unroll
+          for (int q = 0; q < M; q++) swp(At[i * M + q], At[k * M + q]);
+#pragma unroll
+          for (int q = 0; q < N; q++) swp(Vt[i * N + q], Vt[k * N + q]);
+        }
       }
     }
   }
-  for (int i = 0; i < n; i++) Wout[i] = W[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) Wout[i] = W[i];
   if (!Vt) return;
   uint64_t rs = 0x12345678ULL;
-  for (int i = 0; i < n1; i++) {
-    double sd = i < n ? W[i] : 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    double sd = W[i];
+#pragma unroll 1
     for (int ii = 0; ii < 100 && sd <= minval; ii++) {
-      const double val0 = 1. / m;
-      for (int k = 0; k < m; k++) {
+      const double val0 = 1. / M;
+#pragma unroll
+      for (int k = 0; k < M; k++) {
         rs = (uint64_t)(uint32_t)rs * 4164903690ULL + (rs >> 32);
-        At[i * m + k] = (((uint32_t)rs) & 256) != 0 ? val0 : -val0;
+        At[i * M + k] = (((uint32_t)rs) & 256) != 0 ? val0 : -val0;
       }
-      for (int it = 0; it < 2; it++)
+#pragma unroll 1
+      for (int it = 0; it < 2; it++) {
+#pragma unroll
         for (int j = 0; j < i; j++) {
           sd = 0;
-          for (int k = 0; k < m; k++) sd += At[i * m + k] * At[j * m + k];
+#pragma unroll
+          for (int k = 0; k < M; k++) sd += At[i * M + k] * At[j * M + k];
           double asum = 0;
-          for (int k = 0; k < m; k++) {
-            double t = At[i * m + k] - sd * At[j * m + k];
-            At[i * m + k] = t;
+#pragma unroll
+          for (int k = 0; k < M; k++) {
+            double t = At[i * M + k] - sd * At[j * M + k];
+            At[i * M + k] = t;
             asum += fabs(t);
           }
           asum = asum > eps * 100 ? 1 / asum : 0;
-          for (int k = 0; k < m; k++) At[i * m + k] *= asum;
+#pragma unroll
+          for (int k = 0; k < M; k++) At[i * M + k] *= asum;
         }
+      }
       sd = 0;
-      for (int k = 0; k < m; k++) { double t = At[i * m + k]; sd += t * t; }
+#pragma unroll
+      for (int k = 0; k < M; k++) { double t = At[i * M + k]; sd += t * t; }
       sd = sqrt(sd);
     }
     double s = sd > minval ? 1 / sd : 0.;
-    for (int k = 0; k < m; k++) At[i * m + k] *= s;
+#pragma unroll
+    for (int k = 0; k < M; k++) At[i * M + k] *= s;
   }
 }
-// SVD of an m x n (m >= n, m <= 3) row-major A: w, u (m x n), vt (n x n)
-MK_HD void cv_svd(const double* A, int m, int n, double* w, double* u, double* vt) {
-  double At[9], Vt[9];
-  for (int i = 0; i < n; i++)
-    for (int k = 0; k < m; k++) At[i * m + k] = A[k * n + i];
-  jacobi_svd(At, m, n, w, Vt, n);
-  if (u)
-    for (int r = 0; r < m; r++)
-      for (int c = 0; c < n; c++) u[r * n + c] = At[c * m + r];
-  if (vt)
-    for (int k = 0; k < n * n; k++) vt[k] = Vt[k];
-}
 
-// ------------------------------------------------------------- small Mats
-struct Mx {
-  int r, c;
-  double a[12];
+// ------------------------------------------------------- fixed-size Mats
+template <int R, int C>
+struct Mt {
+  double a[R * C];
+  MK_HD double& operator()(int i, int j) { return a[i * C + j]; }
+  MK_HD double operator()(int i, int j) const { return a[i * C + j]; }
 };
-MK_HD Mx mx(int r, int c) {
-  Mx m;
-  m.r = r; m.c = c;
-  for (int i = 0; i < 12; i++) m.a[i] = 0;
+template <int R, int C>
+MK_HD Mt<R, C> zeros() {
+  Mt<R, C> m;
+#pragma unroll
+  for (int i = 0; i < R * C; i++) m.a[i] = 0;
   return m;
 }
-MK_HD double& at(Mx& m, int i, int j) { return m.a[i * m.c + j]; }
-MK_HD double at(const Mx& m, int i, int j) { return m.a[i * m.c + j]; }
-MK_HD Mx eye3() { Mx m = mx(3, 3); m.a[0] = m.a[4] = m.a[8] = 1; return m; }
-MK_HD Mx mm(const Mx& A, const Mx& B, double alpha = 1.0) {
-  Mx o = mx(A.r, B.c);
-  for (int i = 0; i < A.r; i++)
-    for (int j = 0; j < B.c; j++) {
+MK_HD Mt<3, 3> eye3() {
+  Mt<3, 3> m = zeros<3, 3>();
+  m.a[0] = m.a[4] = m.a[8] = 1;
+  return m;
+}
+// gemm: sum_k A(i,k) B(k,j) from 0, times alpha
+template <int R, int K, int C>
+MK_HD Mt<R, C> mm(const Mt<R, K>& A, const Mt<K, C>& B, double alpha = 1.0) {
+  Mt<R, C> o;
+#pragma unroll
+  for (int i = 0; i < R; i++)
+#pragma unroll
+    for (int j = 0; j < C; j++) {
       double s = 0;
-      for (int k = 0; k < A.c; k++) s += at(A, i, k) * at(B, k, j);
-      at(o, i, j) = s * alpha;
+#pragma unroll
+      for (int k = 0; k < K; k++) s += A(i, k) * B(k, j);
+      o(i, j) = s * alpha;
     }
   return o;
 }
-MK_HD Mx mmc(const Mx& A, const Mx& B, const Mx& C) {
-  Mx o = mm(A, B);
-  for (int i = 0; i < o.r * o.c; i++) o.a[i] = o.a[i] + C.a[i];
+template <int R, int K, int C>
+MK_HD Mt<R, C> mmc(const Mt<R, K>& A, const Mt<K, C>& B, const Mt<R, C>& Cc) {
+  Mt<R, C> o = mm(A, B);
+#pragma unroll
+  for (int i = 0; i < R * C; i++) o.a[i] = o.a[i] + Cc.a[i];
   return o;
 }
-MK_HD Mx tr(const Mx& A) { Mx o = mx(A.c, A.r); for (int i = 0; i < A.r; i++) for (int j = 0; j < A.c; j++) at(o, j, i) = at(A, i, j); return o; }
-MK_HD Mx add(const Mx& A, const Mx& B) { Mx o = mx(A.r, A.c); for (int i = 0; i < A.r * A.c; i++) o.a[i] = A.a[i] + B.a[i]; return o; }
-MK_HD Mx sub(const Mx& A, const Mx& B) { Mx o = mx(A.r, A.c); for (int i = 0; i < A.r * A.c; i++) o.a[i] = A.a[i] - B.a[i]; return o; }
-MK_HD Mx scl(const Mx& A, double s) { Mx o = mx(A.r, A.c); for (int i = 0; i < A.r * A.c; i++) o.a[i] = A.a[i] * s; return o; }
-MK_HD Mx col(const Mx& A, int j) { Mx o = mx(3, 1); for (int i = 0; i < 3; i++) o.a[i] = at(A, i, j); return o; }
-MK_HD double det3(const Mx& m) {
-  return at(m, 0, 0) * (at(m, 1, 1) * at(m, 2, 2) - at(m, 1, 2) * at(m, 2, 1)) -
-         at(m, 0, 1) * (at(m, 1, 0) * at(m, 2, 2) - at(m, 1, 2) * at(m, 2, 0)) +
-         at(m, 0, 2) * (at(m, 1, 0) * at(m, 2, 1) - at(m, 1, 1) * at(m, 2, 0));
+template <int R, int C>
+MK_HD Mt<C, R> tr(const Mt<R, C>& A) {
+  Mt<C, R> o;
+#pragma unroll
+  for (int i = 0; i < R; i++)
+#pragma unroll
+    for (int j = 0; j < C; j++) o(j, i) = A(i, j);
+  return o;
 }
-MK_HD Mx inv3(const Mx& M) {
-  Mx D = mx(3, 3);
+template <int R, int C>
+MK_HD Mt<R, C> add(const Mt<R, C>& A, const Mt<R, C>& B) {
+  Mt<R, C> o;
+#pragma unroll
+  for (int i = 0; i < R * C; i++) o.a[i] = A.a[i] + B.a[i];
+  return o;
+}
+template <int R, int C>
+MK_HD Mt<R, C> sub(const Mt<R, C>& A, const Mt<R, C>& B) {
+  Mt<R, C> o;
+#pragma unroll
+  for (int i = 0; i < R * C; i++) o.a[i] = A.a[i] - B.a[i];
+  return o;
+}
+template <int R, int C>
+MK_HD Mt<R, C> scl(const Mt<R, C>& A, double s) {
+  Mt<R, C> o;
+#pragma unroll
+  for (int i = 0; i < R * C; i++) o.a[i] = A.a[i] * s;
+  return o;
+}
+template <int C>
+MK_HD Mt<3, 1> col(const Mt<3, C>& A, int j) {
+  Mt<3, 1> o;
+#pragma unroll
+  for (int i = 0; i < 3; i++) o.a[i] = A(i, j);
+  return o;
+}
+MK_HD double det3(const Mt<3, 3>& m) {
+  return m(0, 0) * (m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1)) - m(0, 1) * (m(1, 0) * m(2, 2) - m(1, 2) * m(2, 0)) +
+         m(0, 2) * (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0));
+}
+MK_HD Mt<3, 3> inv3(const Mt<3, 3>& M) {
+  Mt<3, 3> D = zeros<3, 3>();
   double d = det3(M);
   if (d == 0.) return D;
   d = 1. / d;
-  at(D, 0, 0) = (at(M, 1, 1) * at(M, 2, 2) - at(M, 1, 2) * at(M, 2, 1)) * d;
-  at(D, 0, 1) = (at(M, 0, 2) * at(M, 2, 1) - at(M, 0, 1) * at(M, 2, 2)) * d;
-  at(D, 0, 2) = (at(M, 0, 1) * at(M, 1, 2) - at(M, 0, 2) * at(M, 1, 1)) * d;
-  at(D, 1, 0) = (at(M, 1, 2) * at(M, 2, 0) - at(M, 1, 0) * at(M, 2, 2)) * d;
-  at(D, 1, 1) = (at(M, 0, 0) * at(M, 2, 2) - at(M, 0, 2) * at(M, 2, 0)) * d;
-  at(D, 1, 2) = (at(M, 0, 2) * at(M, 1, 0) - at(M, 0, 0) * at(M, 1, 2)) * d;
-  at(D, 2, 0) = (at(M, 1, 0) * at(M, 2, 1) - at(M, 1, 1) * at(M, 2, 0)) * d;
-  at(D, 2, 1) = (at(M, 0, 1) * at(M, 2, 0) - at(M, 0, 0) * at(M, 2, 1)) * d;
-  at(D, 2, 2) = (at(M, 0, 0) * at(M, 1, 1) - at(M, 0, 1) * at(M, 1, 0)) * d;
+  D(0, 0) = (M(1, 1) * M(2, 2) - M(1, 2) * M(2, 1)) * d;
+  D(0, 1) = (M(0, 2) * M(2, 1) - M(0, 1) * M(2, 2)) * d;
+  D(0, 2) = (M(0, 1) * M(1, 2) - M(0, 2) * M(1, 1)) * d;
+  D(1, 0) = (M(1, 2) * M(2, 0) - M(1, 0) * M(2, 2)) * d;
+  D(1, 1) = (M(0, 0) * M(2, 2) - M(0, 2) * M(2, 0)) * d;
+  D(1, 2) = (M(0, 2) * M(1, 0) - M(0, 0) * M(1, 2)) * d;
+  D(2, 0) = (M(1, 0) * M(2, 1) - M(1, 1) * M(2, 0)) * d;
+  D(2, 1) = (M(0, 1) * M(2, 0) - M(0, 0) * M(2, 1)) * d;
+  D(2, 2) = (M(0, 0) * M(1, 1) - M(0, 1) * M(1, 0)) * d;
   return D;
 }
-MK_HD Mx rowsum(const Mx& P) {
-  Mx o = mx(P.r, 1);
-  for (int i = 0; i < P.r; i++) { double s = 0; for (int j = 0; j < P.c; j++) s += at(P, i, j); o.a[i] = s; }
+template <int C>
+MK_HD Mt<3, 1> rowsum(const Mt<3, C>& P) {
+  Mt<3, 1> o;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    double s = 0;
+#pragma unroll
+    for (int j = 0; j < C; j++) s += P(i, j);
+    o.a[i] = s;
+  }
   return o;
 }
-MK_HD double sqnorm3(const Mx& v) { double x = v.a[0], y = v.a[1], z = v.a[2]; return x * x + y * y + z * z; }
+MK_HD double sqnorm3(const Mt<3, 1>& v) { double x = v.a[0], y = v.a[1], z = v.a[2]; return x * x + y * y + z * z; }
 MK_HD int sgn(double x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); }
-MK_HD double norm_svd(const Mx& A) {
-  double w[3];
-  if (A.c == 1) { cv_svd(A.a, A.r, 1, w, nullptr, nullptr); return w[0]; }
-  double u[9], vt[9];
-  cv_svd(A.a, A.r, A.c, w, u, vt);
+// RPP Norm(): largest singular value (cv::SVD of the matrix, flags 0)
+MK_HD double norm_svd(const Mt<3, 3>& A) {
+  double At[9], w[3], vt[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) At[i * 3 + k] = A(k, i);
+  jacobi_svd<3, 3>(At, w, vt);
   return w[0];
 }
-MK_HD Mx xform(const Mx& P, const Mx& R, const Mx& t) {
-  Mx o = mx(3, P.c);
-  for (int i = 0; i < P.c; i++) {
-    double x = at(P, 0, i), y = at(P, 1, i), z = at(P, 2, i);
-    for (int r = 0; r < 3; r++) at(o, r, i) = at(R, r, 0) * x + at(R, r, 1) * y + at(R, r, 2) * z + t.a[r];
-  }
-  return o;
+MK_HD double norm_svd(const Mt<3, 1>& A) {
+  double At[3] = {A.a[0], A.a[1], A.a[2]}, w[1];
+  jacobi_svd<3, 1>(At, w, (double*)nullptr);
+  return w[0];
 }
-MK_HD Mx rpy_mat(double a0, double a1, double a2) {
+// SVD of a 3x3: u (3x3) and V (3x3 = vt^T)
+MK_HD void svd3(const Mt<3, 3>& A, Mt<3, 3>& U, Mt<3, 3>& V) {
+  double At[9], w[3], vt[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) At[i * 3 + k] = A(k, i);
+  jacobi_svd<3, 3>(At, w, vt);
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) { U(r, c) = At[c * 3 + r]; V(r, c) = vt[c * 3 + r]; }
+}
+// SVD API kept for the host checks: m x n with (m,n) in {(3,3),(3,1)}
+MK_HD void cv_svd(const double* A, int m, int n, double* w, double* u, double* vt) {
+  if (n == 1) {
+    double At[3] = {A[0], A[1], A[2]}, ww[1], V1[1];
+    jacobi_svd<3, 1>(At, ww, V1);
+    w[0] = ww[0];
+    if (u) for (int r = 0; r < 3; r++) u[r] = At[r];
+    if (vt) vt[0] = V1[0];
+    return;
+  }
+  double At[9], ww[3], V[9];
+  for (int i = 0; i < 3; i++)
+    for (int k = 0; k < 3; k++) At[i * 3 + k] = A[k * 3 + i];
+  jacobi_svd<3, 3>(At, ww, V);
+  for (int i = 0; i < 3; i++) w[i] = ww[i];
+  if (u)
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) u[r * 3 + c] = At[c * 3 + r];
+  if (vt)
+    for (int k = 0; k < 9; k++) vt[k] = V[k];
+}
+MK_HD Mt<3, 3> rpy_mat(double a0, double a1, double a2) {
   double cosA = cos(a2), sinA = sin(a2), cosB = cos(a1), sinB = sin(a1), cosC = cos(a0), sinC = sin(a0);
   double cosAsinB = cosA * sinB, sinAsinB = sinA * sinB;
-  Mx R = mx(3, 3);
-  at(R, 0, 0) = cosA * cosB;
-  at(R, 0, 1) = cosAsinB * sinC - sinA * cosC;
-  at(R, 0, 2) = cosAsinB * cosC + sinA * sinC;
-  at(R, 1, 0) = sinA * cosB;
-  at(R, 1, 1) = sinAsinB * sinC + cosA * cosC;
-  at(R, 1, 2) = sinAsinB * cosC - cosA * sinC;
-  at(R, 2, 0) = -sinB;
-  at(R, 2, 1) = cosB * sinC;
-  at(R, 2, 2) = cosB * cosC;
+  Mt<3, 3> R;
+  R(0, 0) = cosA * cosB;
+  R(0, 1) = cosAsinB * sinC - sinA * cosC;
+  R(0, 2) = cosAsinB * cosC + sinA * sinC;
+  R(1, 0) = sinA * cosB;
+  R(1, 1) = sinAsinB * sinC + cosA * cosC;
+  R(1, 2) = sinAsinB * cosC - cosA * sinC;
+  R(2, 0) = -sinB;
+  R(2, 1) = cosB * sinC;
+  R(2, 2) = cosB * cosC;
   return R;
 }
-MK_HD bool rpy_ang(const Mx& R, double* ang) {
-  double R11 = at(R, 0, 0), R12 = at(R, 0, 1), R13 = at(R, 0, 2), R21 = at(R, 1, 0), R22 = at(R, 1, 1),
-         R23 = at(R, 1, 2), R31 = at(R, 2, 0), R32 = at(R, 2, 1), R33 = at(R, 2, 2);
-  double sinB = -R31, cosB = sqrt(R11 * R11 + R21 * R21), a[3];
+MK_HD bool rpy_ang(const Mt<3, 3>& R, double* ang) {
+  double R11 = R(0, 0), R12 = R(0, 1), R13 = R(0, 2), R21 = R(1, 0), R22 = R(1, 1), R23 = R(1, 2), R31 = R(2, 0),
+         R32 = R(2, 1), R33 = R(2, 2);
+  double sinB = -R31, cosB = sqrt(R11 * R11 + R21 * R21), a0, a1, a2;
   if (fabs(cosB) > 1e-15) {
     double sinA = R21 / cosB, cosA = R11 / cosB, sinC = R32 / cosB, cosC = R33 / cosB;
-    a[0] = atan2(sinC, cosC);
-    a[1] = atan2(sinB, cosB);
-    a[2] = atan2(sinA, cosA);
+    a0 = atan2(sinC, cosC);
+    a1 = atan2(sinB, cosB);
+    a2 = atan2(sinA, cosA);
   } else {
     double sinC = (R12 - R23) / 2, cosC = (R22 + R13) / 2;
-    a[0] = atan2(sinC, cosC);
-    a[1] = M_PI_2;
-    a[2] = 0;
-    if (sinB < 0) { a[0] = -a[0]; a[1] = -a[1]; a[2] = -a[2]; }
+    a0 = atan2(sinC, cosC);
+    a1 = M_PI_2;
+    a2 = 0;
+    if (sinB < 0) { a0 = -a0; a1 = -a1; a2 = -a2; }
   }
-  if (norm_svd(sub(R, rpy_mat(a[0], a[1], a[2]))) > 1e-6) return false;
-  ang[0] = a[0]; ang[1] = a[1]; ang[2] = a[2];
+  if (norm_svd(sub(R, rpy_mat(a0, a1, a2))) > 1e-6) return false;
+  ang[0] = a0; ang[1] = a1; ang[2] = a2;
   return true;
 }
-MK_HD bool rpy_ang_x(const Mx& R, double* a) {
+MK_HD bool rpy_ang_x(const Mt<3, 3>& R, double* a) {
   if (!rpy_ang(R, a)) return false;
   if (fabs(a[0]) > M_PI_2) {
-    while (fabs(a[0]) > M_PI_2) {
+    int guard = 0;
+    while (fabs(a[0]) > M_PI_2 && guard++ < 64) {
       if (a[0] > 0) {
         a[0] = a[0] + M_PI; a[1] = 3 * M_PI - a[1]; a[2] = a[2] + M_PI;
         a[0] -= 2 * M_PI; a[1] -= 2 * M_PI; a[2] -= 2 * M_PI;
@@ -671,218 +776,287 @@ MK_HD bool rpy_ang_x(const Mx& R, double* a) {
   }
   return true;
 }
-MK_HD Mx norm_rv(const Mx& R) {
-  Mx o = mx(R.r, R.c);
-  for (int i = 0; i < R.c; i++) {
-    double mag = at(R, 0, i) * at(R, 0, i) + at(R, 1, i) * at(R, 1, i) + at(R, 2, i) * at(R, 2, i);
+template <int C>
+MK_HD Mt<3, C> norm_rv(const Mt<3, C>& R) {
+  Mt<3, C> o;
+#pragma unroll
+  for (int i = 0; i < C; i++) {
+    double mag = R(0, i) * R(0, i) + R(1, i) * R(1, i) + R(2, i) * R(2, i);
     double m = 1.0 / sqrt(mag);
-    for (int r = 0; r < 3; r++) at(o, r, i) = at(R, r, i) * m;
+#pragma unroll
+    for (int r = 0; r < 3; r++) o(r, i) = R(r, i) * m;
   }
   return o;
 }
 
 constexpr int NP = 4;  // points per problem (a square's 4 corners)
+typedef Mt<3, NP> M34;
+typedef Mt<3, 3> M33;
+typedef Mt<3, 1> M31;
 
-MK_HD void abs_kernel(Mx& P, Mx& Q, const Mx* F, const Mx& G, Mx& R, Mx& t, Mx& Qout, double& err2) {
-  const int n = NP;
-  for (int i = 0; i < n; i++) {
-    Mx q = mm(F[i], col(Q, i));
-    for (int r = 0; r < 3; r++) at(Q, r, i) = q.a[r];
+// AbsKernel (RPP.cpp:229-332): overwrites P (re-centred) and Q (F_i q_i) in place
+MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t, M34& Qout, double& err2) {
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    M31 q = mm(F[i], col(Q, i));
+#pragma unroll
+    for (int r = 0; r < 3; r++) Q(r, i) = q.a[r];
   }
-  Mx pbar = scl(rowsum(P), 1.0 / n);
-  for (int i = 0; i < n; i++)
-    for (int r = 0; r < 3; r++) at(P, r, i) -= pbar.a[r];
-  Mx M = mx(3, 3);
-  for (int i = 0; i < n; i++)
+  M31 pbar = scl(rowsum(P), 1.0 / NP);
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int r = 0; r < 3; r++) P(r, i) -= pbar.a[r];
+  M33 M = zeros<3, 3>();
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
     for (int a = 0; a < 3; a++)
-      for (int b = 0; b < 3; b++) at(M, a, b) += at(P, a, i) * at(Q, b, i);
-  double w[3], u[9], vt[9];
-  cv_svd(M.a, 3, 3, w, u, vt);
-  Mx U = mx(3, 3), V = mx(3, 3);
-  for (int i = 0; i < 9; i++) U.a[i] = u[i];
-  for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) at(V, i, j) = vt[j * 3 + i];
-  Mx Ut = tr(U);
-  auto estimate_t = [&](const Mx& Rr) {
-    Mx sum = mx(3, 1);
-    for (int i = 0; i < n; i++) sum = add(sum, mm(mm(F[i], Rr), col(P, i)));
-    return mm(G, sum);
-  };
-  R = mm(V, Ut);
-  if (sgn(det3(R)) == 1) {
-    t = estimate_t(R);
-    if (t.a[2] < 0) {
-      for (int r = 0; r < 3; r++) at(V, r, 2) = -at(V, r, 2);
-      R = mm(V, Ut, -1.0);
-      t = estimate_t(R);
-    }
-  } else {
-    for (int r = 0; r < 3; r++) at(V, r, 2) = -at(V, r, 2);
-    R = mm(V, Ut);
-    t = estimate_t(R);
-    if (t.a[2] < 0) {
-      R = mm(V, Ut, -1.0);
-      t = estimate_t(R);
-    }
+#pragma unroll
+      for (int b = 0; b < 3; b++) M(a, b) += P(a, i) * Q(b, i);
+  M33 U, V;
+  svd3(M, U, V);
+  M33 Ut = tr(U);
+  // ref: RPP.cpp:296-318. det(V U^T) > 0: try R = V U^T, and if t_z < 0
+  // flip V's 3rd column and take R = -(V U^T). Otherwise flip first, take
+  // R = V U^T and, if t_z < 0, R = -(V U^T). One EstimateT call site.
+  const bool pos = sgn(det3(mm(V, Ut))) == 1;
+  if (!pos) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) V(r, 2) = -V(r, 2);
   }
-  Mx I = eye3();
+  R = mm(V, Ut);
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    M31 sum = zeros<3, 1>();
+#pragma unroll
+    for (int i = 0; i < NP; i++) sum = add(sum, mm(mm(F[i], R), col(P, i)));
+    t = mm(G, sum);
+    if (pass == 1 || !(t.a[2] < 0)) break;
+    if (pos) {
+#pragma unroll
+      for (int r = 0; r < 3; r++) V(r, 2) = -V(r, 2);
+    }
+    R = mm(V, Ut, -1.0);
+  }
+  M33 I = eye3();
   err2 = 0;
-  Qout = xform(P, R, t);
-  for (int i = 0; i < n; i++) err2 += sqnorm3(mm(sub(I, F[i]), col(Qout, i)));
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    double x = P(0, i), y = P(1, i), z = P(2, i);
+    M31 qo;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      qo.a[r] = R(r, 0) * x + R(r, 1) * y + R(r, 2) * z + t.a[r];
+      Qout(r, i) = qo.a[r];
+    }
+    err2 += sqnorm3(mm(sub(I, F[i]), qo));
+  }
 }
 
-// returns 1 when the (reference-unbounded) iteration hit the cap
-MK_HD int obj_pose(const Mx& P0, Mx& Qp, const Mx* initR, Mx& R, Mx& t, int& it, double& obj_err, double& img_err) {
+// ObjPose (RPP.cpp:66-208); returns 1 when the (reference-unbounded) loop hit the cap
+MK_HD int obj_pose(const M34& P0, M34& Qp, const M33* initR, M33& R, M31& t, int& it, double& obj_err,
+                   double& img_err) {
   const double TOL = 1E-5, EPS = 1E-8;
-  const int n = NP;
-  Mx P = P0;
+  M34 P = P0;
   it = 0;
-  Mx pbar = scl(rowsum(P), 1.0 / n);
-  for (int i = 0; i < n; i++)
-    for (int r = 0; r < 3; r++) at(P, r, i) -= pbar.a[r];
-  Mx F[NP];
-  for (int i = 0; i < n; i++) {
-    Mx V = col(Qp, i);
+  M31 pbar = scl(rowsum(P), 1.0 / NP);
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int r = 0; r < 3; r++) P(r, i) -= pbar.a[r];
+  M33 F[NP];
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    M31 V = col(Qp, i);
     double ret = mm(tr(V), V).a[0];
     F[i] = mm(V, tr(V), 1.0 / ret);
   }
-  Mx sumF = mx(3, 3);
-  for (int i = 0; i < n; i++) sumF = add(sumF, F[i]);
-  Mx I = eye3();
-  Mx tFactor = scl(inv3(sub(I, scl(sumF, 1.0 / n))), 1.0 / n);
-  double old_err, new_err;
-  Mx Qi, Ri, ti;
+  M33 sumF = zeros<3, 3>();
+#pragma unroll
+  for (int i = 0; i < NP; i++) sumF = add(sumF, F[i]);
+  M33 I = eye3();
+  M33 tFactor = scl(inv3(sub(I, scl(sumF, 1.0 / NP))), 1.0 / NP);
+  double old_err = 0, new_err;
+  M34 Qi;
+  M33 Ri;
+  M31 ti;
+  // Without an initial rotation the reference's first AbsKernel runs on Qp
+  // itself (and rewrites it with F_i q_i, RPP.cpp:105-110); it is folded into
+  // the iteration below as pass -1 so AbsKernel has a single call site.
+  bool init_pass = initR == nullptr;
   if (initR) {
     Ri = *initR;
-    Mx s = mx(3, 1);
-    for (int i = 0; i < n; i++) s = mmc(mm(sub(F[i], I), Ri), col(P, i), s);
+    M31 s = zeros<3, 1>();
+#pragma unroll
+    for (int i = 0; i < NP; i++) s = mmc(mm(sub(F[i], I), Ri), col(P, i), s);
     ti = mm(tFactor, s);
-    Qi = xform(P, Ri, ti);
-    old_err = 0;
-    for (int i = 0; i < n; i++) old_err += sqnorm3(mm(sub(I, F[i]), col(Qi, i)));
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+      double x = P(0, i), y = P(1, i), z = P(2, i);
+      M31 qo;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        qo.a[r] = Ri(r, 0) * x + Ri(r, 1) * y + Ri(r, 2) * z + ti.a[r];
+        Qi(r, i) = qo.a[r];
+      }
+      old_err += sqnorm3(mm(sub(I, F[i]), qo));
+    }
   } else {
-    abs_kernel(P, Qp, F, tFactor, Ri, ti, Qi, old_err);
-    it = 1;
+    Qi = Qp;
   }
-  abs_kernel(P, Qi, F, tFactor, Ri, ti, Qi, new_err);
-  it = it + 1;
   int capped = 0;
-  while (fabs((old_err - new_err) / old_err) > TOL && (new_err > EPS)) {
-    if (it >= 100000) { capped = 1; break; }
-    old_err = new_err;
+  // the reference computes one AbsKernel before testing the stop rule
+  new_err = old_err;
+  bool first = true;
+#pragma unroll 1
+  while (true) {
+    if (!first) {
+      if (!(fabs((old_err - new_err) / old_err) > TOL && (new_err > EPS))) break;
+      if (it >= 100000) { capped = 1; break; }
+      old_err = new_err;
+    }
     abs_kernel(P, Qi, F, tFactor, Ri, ti, Qi, new_err);
     it = it + 1;
+    if (init_pass) {
+      // abs_kernel rewrote its input Q (= Qp) before forming Qi; recover Qp's
+      // new content: F_i q_i is recomputed exactly as abs_kernel did
+#pragma unroll
+      for (int i = 0; i < NP; i++) {
+        M31 q = mm(F[i], col(Qp, i));
+#pragma unroll
+        for (int r = 0; r < 3; r++) Qp(r, i) = q.a[r];
+      }
+      init_pass = false;
+      old_err = new_err;
+      continue;
+    }
+    first = false;
   }
   R = Ri;
   t = ti;
-  obj_err = sqrt(new_err / n);
+  obj_err = sqrt(new_err / NP);
   img_err = 0;
-  for (int i = 0; i < n; i++) {
-    Mx Qproj = mmc(Ri, col(P, i), ti);
-    double xx = (Qproj.a[0] / Qproj.a[2]) - at(Qp, 0, 0);
-    double yy = (Qproj.a[1] / Qproj.a[2]) - at(Qp, 1, 0);
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    M31 Qproj = mmc(Ri, col(P, i), ti);
+    double xx = (Qproj.a[0] / Qproj.a[2]) - Qp(0, 0);
+    double yy = (Qproj.a[1] / Qproj.a[2]) - Qp(1, 0);
     img_err += (xx * xx + yy * yy);
   }
-  img_err = sqrt(img_err / n);
+  img_err = sqrt(img_err / NP);
   t = sub(t, mm(Ri, pbar));
   return capped;
 }
 
-MK_HD bool rot_by_vector(const double* v1, const double* v2, Mx& R) {
+MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
   double d = v2[0] * v1[0] + v2[1] * v1[1] + v2[2] * v1[2];
   double winkel = acos(d);
-  Mx axm = mx(3, 1);
+  M31 axm;
   axm.a[0] = v2[1] * v1[2] - v2[2] * v1[1];
   axm.a[1] = v2[2] * v1[0] - v2[0] * v1[2];
   axm.a[2] = v2[0] * v1[1] - v2[1] * v1[0];
   double nn = norm_svd(axm);
   double ra[3] = {axm.a[0], axm.a[1], axm.a[2]};
+#pragma unroll
   for (int i = 0; i < 3; i++) ra[i] /= nn;
+#pragma unroll
   for (int i = 0; i < 3; i++) ra[i] *= sin(winkel * 0.5);
   double qs = cos(winkel * 0.5);
   double qn = sqrt(ra[0] * ra[0] + ra[1] * ra[1] + ra[2] * ra[2] + qs * qs);
   double inv = 1 / qn;
   double a = qs * inv, b = ra[0] * inv, c = ra[1] * inv, dd = ra[2] * inv;
-  R = mx(3, 3);
-  at(R, 0, 0) = a * a + b * b - c * c - dd * dd;
-  at(R, 0, 1) = 2 * (b * c - a * dd);
-  at(R, 0, 2) = 2 * (b * dd + a * c);
-  at(R, 1, 0) = 2 * (b * c + a * dd);
-  at(R, 1, 1) = a * a + c * c - b * b - dd * dd;
-  at(R, 1, 2) = 2 * (c * dd - a * b);
-  at(R, 2, 0) = 2 * (b * dd - a * c);
-  at(R, 2, 1) = 2 * (c * dd + a * b);
-  at(R, 2, 2) = a * a + dd * dd - b * b - c * c;
-  Mx n1 = mx(3, 1), n2 = mx(3, 1);
+  R(0, 0) = a * a + b * b - c * c - dd * dd;
+  R(0, 1) = 2 * (b * c - a * dd);
+  R(0, 2) = 2 * (b * dd + a * c);
+  R(1, 0) = 2 * (b * c + a * dd);
+  R(1, 1) = a * a + c * c - b * b - dd * dd;
+  R(1, 2) = 2 * (c * dd - a * b);
+  R(2, 0) = 2 * (b * dd - a * c);
+  R(2, 1) = 2 * (c * dd + a * b);
+  R(2, 2) = a * a + dd * dd - b * b - c * c;
+  M31 n1, n2;
   double m1 = sqrt(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]);
   double m2 = sqrt(v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2]);
+#pragma unroll
   for (int i = 0; i < 3; i++) { n1.a[i] = v1[i] / m1; n2.a[i] = v2[i] / m2; }
-  Mx diff = sub(n1, mm(R, n2));
+  M31 diff = sub(n1, mm(R, n2));
   double s = 0;
+#pragma unroll
   for (int i = 0; i < 3; i++) s += diff.a[i] * diff.a[i];
   return !(s * s > 1e-3);
 }
 
-MK_HD bool decompose_r(const Mx& R, Mx& RzN) {
-  double cl = atan2(at(R, 2, 1), at(R, 2, 0));
-  Mx Rz = rpy_mat(0, 0, cl);
-  Mx R_ = mm(R, Rz);
-  if (at(R_, 2, 1) > 1e-3) return false;
+MK_HD bool decompose_r(const M33& R, M33& RzN) {
+  double cl = atan2(R(2, 1), R(2, 0));
+  M33 Rz = rpy_mat(0, 0, cl);
+  M33 R_ = mm(R, Rz);
+  if (R_(2, 1) > 1e-3) return false;
   double ang[3];
   if (!rpy_ang_x(R_, ang)) return false;
   if (fabs(ang[0]) > 1e-3) return false;
-  Mx Rz2 = mm(Rz, rpy_mat(0, 0, M_PI));
+  M33 Rz2 = mm(Rz, rpy_mat(0, 0, M_PI));
   R_ = mm(R, Rz2);
-  if (at(R_, 2, 1) > 1e-3) return false;
+  if (R_(2, 1) > 1e-3) return false;
   if (!rpy_ang_x(R_, ang)) return false;
   RzN = Rz;
   return true;
 }
 
-// GetRotationY_wrtT: returns the number of kept solutions (<= 5)
-MK_HD int rot_y_wrt_t(const Mx& v, const Mx& p, const Mx& Rz, double* al, Mx* tnew, double* at_out) {
-  const int n = NP;
-  Mx V[NP];
-  for (int i = 0; i < n; i++) {
-    Mx vv = col(v, i);
+// GetRotationY_wrtT (RPP.cpp:947-1222): the 5 root slots of the quartic in
+// order with a keep flag (the reference's translation candidates are
+// overwritten by the following ObjPose and are not formed here).
+MK_HD void rot_y_wrt_t(const M34& v, const M34& p, const M33& Rz, double* al, bool* keep) {
+  M33 V[NP];
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    M31 vv = col(v, i);
     double a = mm(tr(vv), vv).a[0];
     V[i] = mm(vv, tr(vv), 1.0 / a);
   }
-  Mx G = mx(3, 3);
-  for (int i = 0; i < n; i++) G = add(G, V[i]);
-  Mx I = eye3();
-  G = scl(inv3(sub(I, scl(G, 1.0 / n))), 1.0 / n);
-  Mx opt = mx(3, 3);
-  const double r1 = at(Rz, 0, 0), r2 = at(Rz, 0, 1), r3 = at(Rz, 0, 2), r4 = at(Rz, 1, 0), r5 = at(Rz, 1, 1),
-               r6 = at(Rz, 1, 2), r7 = at(Rz, 2, 0), r8 = at(Rz, 2, 1), r9 = at(Rz, 2, 2);
-  for (int i = 0; i < n; i++) {
+  M33 G = zeros<3, 3>();
+#pragma unroll
+  for (int i = 0; i < NP; i++) G = add(G, V[i]);
+  M33 I = eye3();
+  G = scl(inv3(sub(I, scl(G, 1.0 / NP))), 1.0 / NP);
+  M33 opt = zeros<3, 3>();
+  const double r1 = Rz(0, 0), r2 = Rz(0, 1), r3 = Rz(0, 2), r4 = Rz(1, 0), r5 = Rz(1, 1), r6 = Rz(1, 2),
+               r7 = Rz(2, 0), r8 = Rz(2, 1), r9 = Rz(2, 2);
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+#pragma unroll
     for (int k = 0; k < 3; k++) {
-      double w1 = at(V[i], k, 0), w2 = at(V[i], k, 1), w3 = at(V[i], k, 2);
+      double w1 = V[i](k, 0), w2 = V[i](k, 1), w3 = V[i](k, 2);
       if (k == 0) w1 = w1 - 1; else if (k == 1) w2 = w2 - 1; else w3 = w3 - 1;
-      double px = at(p, 0, i), py = at(p, 1, i), pz = at(p, 2, i);
-      at(opt, k, 0) += ((w1 * r2 + w2 * r5 + w3 * r8) * py + (-w1 * r1 - w2 * r4 - w3 * r7) * px +
-                        (-w1 * r3 - w2 * r6 - w3 * r9) * pz);
-      at(opt, k, 1) += ((2 * w1 * r1 + 2 * w2 * r4 + 2 * w3 * r7) * pz + (-2 * w1 * r3 - 2 * w2 * r6 - 2 * w3 * r9) * px);
-      at(opt, k, 2) += (w1 * r1 + w2 * r4 + w3 * r7) * px + (w1 * r3 + w2 * r6 + w3 * r9) * pz +
-                       (w1 * r2 + w2 * r5 + w3 * r8) * py;
+      double px = p(0, i), py = p(1, i), pz = p(2, i);
+      opt(k, 0) += ((w1 * r2 + w2 * r5 + w3 * r8) * py + (-w1 * r1 - w2 * r4 - w3 * r7) * px +
+                    (-w1 * r3 - w2 * r6 - w3 * r9) * pz);
+      opt(k, 1) += ((2 * w1 * r1 + 2 * w2 * r4 + 2 * w3 * r7) * pz + (-2 * w1 * r3 - 2 * w2 * r6 - 2 * w3 * r9) * px);
+      opt(k, 2) += (w1 * r1 + w2 * r4 + w3 * r7) * px + (w1 * r3 + w2 * r6 + w3 * r9) * pz +
+                   (w1 * r2 + w2 * r5 + w3 * r8) * py;
     }
   }
   opt = mm(G, opt);
   double E2[5] = {0, 0, 0, 0, 0};
-  for (int i = 0; i < n; i++) {
-    double px = at(p, 0, i), py = at(p, 1, i), pz = at(p, 2, i);
-    Mx Rpi = mx(3, 3);
-    at(Rpi, 0, 0) = -px; at(Rpi, 0, 1) = 2 * pz; at(Rpi, 0, 2) = px;
-    at(Rpi, 1, 0) = py;  at(Rpi, 1, 1) = 0;      at(Rpi, 1, 2) = py;
-    at(Rpi, 2, 0) = -pz; at(Rpi, 2, 1) = -2 * px; at(Rpi, 2, 2) = pz;
-    Mx E = mm(sub(I, V[i]), mmc(Rz, Rpi, opt));
-    double e0[3], e1[3], e2[3];
-    for (int r = 0; r < 3; r++) { e0[r] = at(E, r, 2); e1[r] = at(E, r, 1); e2[r] = at(E, r, 0); }
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+    double px = p(0, i), py = p(1, i), pz = p(2, i);
+    M33 Rpi;
+    Rpi(0, 0) = -px; Rpi(0, 1) = 2 * pz; Rpi(0, 2) = px;
+    Rpi(1, 0) = py;  Rpi(1, 1) = 0;      Rpi(1, 2) = py;
+    Rpi(2, 0) = -pz; Rpi(2, 1) = -2 * px; Rpi(2, 2) = pz;
+    M33 E = mm(sub(I, V[i]), mmc(Rz, Rpi, opt));
     double s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
-    for (int r = 0; r < 3; r++) s1 += e2[r] * e2[r];
-    for (int r = 0; r < 3; r++) s2 += 2 * (e1[r] * e2[r]);
-    for (int r = 0; r < 3; r++) s3 += (e0[r] * e2[r]) * 2 + e1[r] * e1[r] + 0.0;
-    for (int r = 0; r < 3; r++) s4 += 2 * (e0[r] * e1[r]);
-    for (int r = 0; r < 3; r++) s5 += e0[r] * e0[r];
+#pragma unroll
+    for (int r = 0; r < 3; r++) s1 += E(r, 0) * E(r, 0);
+#pragma unroll
+    for (int r = 0; r < 3; r++) s2 += 2 * (E(r, 1) * E(r, 0));
+#pragma unroll
+    for (int r = 0; r < 3; r++) s3 += (E(r, 2) * E(r, 0)) * 2 + E(r, 1) * E(r, 1) + 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; r++) s4 += 2 * (E(r, 2) * E(r, 1));
+#pragma unroll
+    for (int r = 0; r < 3; r++) s5 += E(r, 2) * E(r, 2);
     E2[0] += s1; E2[1] += s2; E2[2] += s3; E2[3] += s4; E2[4] += s5;
   }
   double e4 = E2[0], e3 = E2[1], e2 = E2[2], e1 = E2[3], e0 = E2[4];
@@ -890,29 +1064,17 @@ MK_HD int rot_y_wrt_t(const Mx& v, const Mx& p, const Mx& Rz, double* al, Mx* tn
   double coeffs[5] = {a4, a3, a2, a1, a0};
   double zr[5] = {0, 0, 0, 0, 0}, zi[5] = {0, 0, 0, 0, 0};
   rpoly(coeffs, 4, zr, zi);
-  double atv[5];
-  int nat = 0;
+#pragma unroll
   for (int i = 0; i < 5; i++) {
-    double _at = zr[i];
-    double p1 = pow(1.0 + _at * _at, 3.0);
-    if (fabs(p1) > 0.1 && zi[i] == 0) atv[nat++] = _at;
-  }
-  int nk = 0;
-  for (int q = 0; q < nat; q++) {
-    double a = atv[q];
+    double a = zr[i];
+    double p1 = pow(1.0 + a * a, 3.0);
+    bool k1 = fabs(p1) > 0.1 && zi[i] == 0;
     double sa = (2.0 * a) / (1.0 + a * a);
     double ca = (1.0 - a * a) / (1.0 + a * a);
-    double alv = atan2(sa, ca) * 180 / M_PI;
+    al[i] = atan2(sa, ca) * 180 / M_PI;
     double tMaxMin = (4 * a4 * a * a * a + 3 * a3 * a * a + 2 * a2 * a + a1);
-    if (tMaxMin > 0) { al[nk] = alv; at_out[nk] = a; nk++; }
+    keep[i] = k1 && tMaxMin > 0;
   }
-  for (int k = 0; k < nk; k++) {
-    Mx R = mm(Rz, rpy_mat(0, (al[k] * M_PI / 180), 0));
-    Mx t_opt = mx(3, 1);
-    for (int i = 0; i < n; i++) t_opt = add(t_opt, mm(mm(sub(V[i], I), R), col(p, i)));
-    tnew[k] = mm(G, t_opt);
-  }
-  return nk;
 }
 
 struct Result {
@@ -923,68 +1085,163 @@ struct Result {
   int error;   // 0; 1 GetRotationbyVector failed (reference exit(1)); 2 iteration cap; 3 no best
 };
 
-// RPP::Rpp (RPP.cpp:13-64) on model/iprts given as 3 x 4 row-major
-MK_HD Result solve(const double* model, const double* iprts) {
-  Result res;
-  res.status = 0;
-  res.error = 0;
-  Mx P = mx(3, NP), Q = mx(3, NP);
+// RPP::Rpp (RPP.cpp:13-64) split in three phases so the GPU runs each with a
+// small live state: stage1 = first ObjPose + Get2ndPose_Exact up to the
+// candidate rotations; refine = one ObjPose per candidate (independent work
+// items); merge = the reference's ordered lowest-obj_err selection.
+constexpr int kCand = 5;
+struct Stage1 {
+  double Q[3 * NP];         // iprts after the first ObjPose (AbsKernel rewrote it)
+  double R[9], t[3], obj_err, img_err;
+  double sR[kCand][9];      // initial rotations of the 2nd-pose candidates
+  int iterations, error;    // error: 0 / 1 (GetRotationbyVector) / 2 (cap)
+  int keep_mask;            // bit j: candidate j enters the search
+  int pad;
+};
+struct Refine {
+  double R[9], t[3], obj_err, img_err;
+  int iterations, capped;
+};
+
+// first ObjPose (no initial rotation)
+MK_HD void stage1a(const double* model, const double* iprts, Stage1& s) {
+  M34 P, Q;
+#pragma unroll
   for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Q.a[i] = iprts[i]; }
-  Mx R, t;
+  M33 R;
+  M31 t;
   int it = 0;
   double oe = 0, ie = 0;
   int capped = obj_pose(P, Q, nullptr, R, t, it, oe, ie);
-  auto fill = [&](const Mx& Rr, const Mx& tt, double o, double i2) {
-    for (int k = 0; k < 9; k++) res.R[k] = Rr.a[k];
-    for (int k = 0; k < 3; k++) res.t[k] = tt.a[k];
-    res.obj_err = o;
-    res.img_err = i2;
-    res.iterations = it;
-  };
-  fill(R, t, oe, ie);
-  res.error = capped ? 2 : 0;
-  // Get2ndPose_Exact
-  const int n = NP;
-  Mx nv = tr(norm_rv(Q));
-  Mx mean = mx(3, 1);
+#pragma unroll
+  for (int k = 0; k < 3 * NP; k++) s.Q[k] = Q.a[k];
+#pragma unroll
+  for (int k = 0; k < 9; k++) s.R[k] = R.a[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) s.t[k] = t.a[k];
+  s.obj_err = oe;
+  s.img_err = ie;
+  s.iterations = it;
+  s.error = capped ? 2 : 0;
+  s.keep_mask = 0;
+}
+
+// Get2ndPose_Exact up to the candidate rotations (RPP.cpp:693-753)
+MK_HD void stage1b(const double* model, Stage1& s) {
+  M34 P, Q;
+  M33 R;
+#pragma unroll
+  for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Q.a[i] = s.Q[i]; }
+#pragma unroll
+  for (int k = 0; k < 9; k++) R.a[k] = s.R[k];
+  Mt<NP, 3> nv = tr(norm_rv(Q));
+  M31 mean;
+#pragma unroll
   for (int j = 0; j < 3; j++) {
-    double s = 0;
-    for (int i = 0; i < n; i++) s += at(nv, i, j);
-    mean.a[j] = s / 3;
+    double sm = 0;
+#pragma unroll
+    for (int i = 0; i < NP; i++) sm += nv(i, j);
+    mean.a[j] = sm / 3;
   }
-  Mx cent = norm_rv(mean);
+  M31 cent = norm_rv(mean);
   double c3[3] = {cent.a[0], cent.a[1], cent.a[2]}, z[3] = {0, 0, 1};
-  Mx Rim;
-  if (!rot_by_vector(z, c3, Rim)) { res.error = 1; return res; }
-  Mx v_ = mm(Rim, Q), R_ = mm(Rim, R), t_ = mm(Rim, t);
-  Mx RzN;
-  if (!decompose_r(R_, RzN)) return res;
-  Mx R2 = mm(R_, RzN);
-  Mx P_ = mm(tr(RzN), P);
+  M33 Rim;
+  if (!rot_by_vector(z, c3, Rim)) { s.error = 1; return; }
+  M34 v_ = mm(Rim, Q);
+  M33 R_ = mm(Rim, R);
+  M33 RzN;
+  if (!decompose_r(R_, RzN)) return;
+  M33 R2 = mm(R_, RzN);
+  M34 P_ = mm(tr(RzN), P);
   double ang[3];
-  if (!rpy_ang_x(R2, ang)) return res;
-  Mx Rz = rpy_mat(0, 0, ang[2]);
-  double bl[5], atv[5];
-  Mx tn[5];
-  int nb = rot_y_wrt_t(v_, P_, Rz, bl, tn, atv);
-  if (nb == 0) return res;
-  Mx RimT = tr(Rim);
+  if (!rpy_ang_x(R2, ang)) return;
+  M33 Rz = rpy_mat(0, 0, ang[2]);
+  double bl[kCand];
+  bool keep[kCand];
+  rot_y_wrt_t(v_, P_, Rz, bl, keep);
+  M33 RimT = tr(Rim);
+  M33 RzNt = tr(RzN);
+  int mask = 0;
+#pragma unroll 1
+  for (int j = 0; j < kCand; j++) {
+    if (!keep[j]) continue;
+    double b = bl[j] / 180 * M_PI;
+    M33 sR = mm(RimT, mm(mm(Rz, rpy_mat(0, b, 0)), RzNt));
+#pragma unroll
+    for (int k = 0; k < 9; k++) s.sR[j][k] = sR.a[k];
+    mask |= 1 << j;
+  }
+  s.keep_mask = mask;
+}
+
+MK_HD void stage1(const double* model, const double* iprts, Stage1& s) {
+  stage1a(model, iprts, s);
+  stage1b(model, s);
+}
+
+MK_HD void refine(const double* model, const double* Q, const double* sR, Refine& r) {
+  M34 P, Qp;
+#pragma unroll
+  for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Qp.a[i] = Q[i]; }
+  M33 R0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) R0.a[k] = sR[k];
+  M33 Rl;
+  M31 tl;
+  int it = 0;
+  double oe = 0, ie = 0;
+  r.capped = obj_pose(P, Qp, &R0, Rl, tl, it, oe, ie);
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.R[k] = Rl.a[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) r.t[k] = tl.a[k];
+  r.obj_err = oe;
+  r.img_err = ie;
+  r.iterations = it;
+}
+
+// ref: RPP.cpp:40-63 — candidates in order, strict "<" on obj_err from 1e6;
+// the reported iteration count is the last ObjPose's (the variable is shared)
+MK_HD Result merge(const Stage1& s, const Refine* rf) {
+  Result res;
+  for (int k = 0; k < 9; k++) res.R[k] = s.R[k];
+  for (int k = 0; k < 3; k++) res.t[k] = s.t[k];
+  res.obj_err = s.obj_err;
+  res.img_err = s.img_err;
+  res.iterations = s.iterations;
+  res.status = 0;
+  res.error = s.error;
+  if (s.error == 1 || s.keep_mask == 0) return res;
   int best = -1;
   double lowest = 1e6;
-  Mx bestR, bestT;
-  double bo = 0, bi = 0;
-  for (int j = 0; j < nb; j++) {
-    double b = bl[j] / 180 * M_PI;
-    Mx sR = mm(RimT, mm(mm(Rz, rpy_mat(0, b, 0)), tr(RzN)));
-    Mx st = mm(RimT, tn[j]);
-    Mx Rl, tl;
-    if (obj_pose(P, Q, &sR, Rl, tl, it, oe, ie)) res.error = 2;
-    if (oe < lowest) { lowest = oe; best = j; bestR = Rl; bestT = tl; bo = oe; bi = ie; }
+  for (int j = 0; j < kCand; j++) {
+    if (!(s.keep_mask >> j & 1)) continue;
+    if (rf[j].capped) res.error = 2;
+    if (rf[j].obj_err < lowest) { lowest = rf[j].obj_err; best = j; }
   }
   if (best < 0) { res.error = 3; return res; }
-  fill(bestR, bestT, bo, bi);
+  const Refine& b = rf[best];
+  for (int k = 0; k < 9; k++) res.R[k] = b.R[k];
+  for (int k = 0; k < 3; k++) res.t[k] = b.t[k];
+  res.obj_err = b.obj_err;
+  res.img_err = b.img_err;
+  int last = 0;
+  for (int j = 0; j < kCand; j++)
+    if (s.keep_mask >> j & 1) last = j;
+  res.iterations = rf[last].iterations;
   res.status = 1;
   return res;
+}
+
+// RPP::Rpp (RPP.cpp:13-64) on model/iprts given as 3 x 4 row-major (host checks)
+MK_HD Result solve(const double* model, const double* iprts) {
+  Stage1 s;
+  stage1(model, iprts, s);
+  Refine rf[kCand];
+  if (s.error != 1)
+    for (int j = 0; j < kCand; j++)
+      if (s.keep_mask >> j & 1) refine(model, s.Q, s.sR[j], rf[j]);
+  return merge(s, rf);
 }
 
 }  // namespace rpp

@@ -40,8 +40,8 @@ struct QuadRec {
 
 struct RppOut {
   double R[9], t[3];
-  double img_err;
-  int32_t status, error, pad;
+  double img_err, obj_err;
+  int32_t status, error, iterations, pad;
 };
 
 struct HypRec {  // mk::Hyp + bookkeeping

@@ -1,0 +1,119 @@
+"""ctypes bindings for build/libmantis_hostcheck.so: the device-logic headers
+(mantis_amd/csrc/mk_*.h) compiled for the host, so the per-work-item
+algorithms run by the HIP kernels can be checked against the oracle on CPU.
+Test infrastructure only; the product is mantis_amd/libmantis_amd.so.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HC_SO = os.path.join(ROOT, "build", "libmantis_hostcheck.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(HC_SO):
+            raise RuntimeError("hostcheck not built: run `make tools`")
+        L = C.CDLL(HC_SO)
+        L.hc_rpp.restype = C.c_int
+        L.hc_rpoly.restype = C.c_int
+        L.hc_approx.restype = C.c_int
+        L.hc_approx.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_void_p]
+        L.hc_find_contours.restype = C.c_int
+        L.hc_find_contours.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                       C.c_int]
+        L.hc_sort_desc.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.hc_distort.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.hc_undistort.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.hc_masks_bits.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def rpp(model, iprts):
+    model = np.ascontiguousarray(model, np.float64)
+    iprts = np.ascontiguousarray(iprts, np.float64)
+    assert model.shape == (3, 4) and iprts.shape == (3, 4)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    e = np.zeros(3)
+    code = C.c_int(0)
+    st = lib().hc_rpp(_d(model), _d(iprts), _d(R), _d(t), _d(e), C.byref(code))
+    return st, R.reshape(3, 3), t, e, code.value
+
+
+def rpoly(coef):
+    coef = np.ascontiguousarray(coef, np.float64)
+    deg = len(coef) - 1
+    zr = np.zeros(deg + 1)
+    zi = np.zeros(deg + 1)
+    d = lib().hc_rpoly(_d(coef), C.c_int(deg), _d(zr), _d(zi))
+    return d, zr, zi
+
+
+def sort_desc(err):
+    err = np.ascontiguousarray(err, np.float64)
+    perm = np.zeros(len(err), np.int32)
+    lib().hc_sort_desc(err.ctypes.data, len(err), perm.ctypes.data)
+    return perm
+
+
+def approx_poly(pts, eps, closed=True):
+    pts = np.ascontiguousarray(pts, np.int32).reshape(-1, 2)
+    out = np.zeros((len(pts) + 1, 2), np.int32)
+    m = lib().hc_approx(pts.ctypes.data, len(pts), float(eps), int(closed), out.ctypes.data)
+    return out[:m]
+
+
+def find_contours(binimg, mode):
+    """mode 1 = RETR_LIST, 2 = RETR_CCOMP; returns (list of (n,2) arrays, hole flags)."""
+    b = np.ascontiguousarray(binimg != 0, np.uint8)
+    h, w = b.shape
+    max_pts = 8 * (w + 2) * (h + 2)
+    max_c = (w + 2) * (h + 2) // 2 + 8
+    pts = np.zeros(2 * max_pts, np.int32)
+    meta = np.zeros(3 * max_c, np.int32)
+    n = lib().hc_find_contours(b.ctypes.data, w, h, mode, pts.ctypes.data, max_pts, meta.ctypes.data, max_c)
+    assert n >= 0
+    out, holes = [], []
+    for i in range(n):
+        off, cnt, hole = meta[3 * i: 3 * i + 3]
+        out.append(pts[2 * off: 2 * (off + cnt)].reshape(-1, 2).copy())
+        holes.append(int(hole))
+    return out, holes
+
+
+def distort(xyz, K, D):
+    xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    px = np.zeros((len(xyz), 2))
+    lib().hc_distort(xyz.ctypes.data, len(xyz), K.ctypes.data, D.ctypes.data, px.ctypes.data)
+    return px
+
+
+def undistort(px, K, D):
+    px = np.ascontiguousarray(px, np.float64).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    out = np.zeros((len(px), 2))
+    lib().hc_undistort(px.ctypes.data, len(px), K.ctypes.data, D.ctypes.data, out.ctypes.data)
+    return out
+
+
+def masks_bits(canny_img):
+    """Bit-packed detector binary (unpadded) and clean mask from a Canny image."""
+    e = np.ascontiguousarray(canny_img != 0, np.uint8)
+    h, w = e.shape
+    det = np.zeros((h, w), np.uint8)
+    mask = np.zeros((h, w), np.uint8)
+    lib().hc_masks_bits(e.ctypes.data, w, h, det.ctypes.data, mask.ctypes.data)
+    return det, mask
