@@ -196,6 +196,33 @@ def approx_poly(pts, eps, closed=True):
     return out[:n].copy()
 
 
+def sort_desc(err):
+    err = np.ascontiguousarray(err, np.float64)
+    perm = np.zeros(len(err), np.int32)
+    lib().orc_sort_desc(_p(err, C.c_double), C.c_int32(len(err)), _p(perm, C.c_int32))
+    return perm
+
+
+def distort(xyz, K, D):
+    xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    px = np.zeros((len(xyz), 2))
+    lib().orc_distort(_p(xyz, C.c_double), C.c_int32(len(xyz)), _p(K, C.c_double), _p(D, C.c_double),
+                      _p(px, C.c_double))
+    return px
+
+
+def undistort(px, K, D):
+    px = np.ascontiguousarray(px, np.float64).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    out = np.zeros((len(px), 2))
+    lib().orc_undistort(_p(px, C.c_double), C.c_int32(len(px)), _p(K, C.c_double), _p(D, C.c_double),
+                        _p(out, C.c_double))
+    return out
+
+
 class Oracle:
     """One oracle context: map + the global cv::RNG(1) of Mantis3Params.h:87."""
 

@@ -1,0 +1,84 @@
+"""N>1 paths on CPU with torch.distributed over gloo (world size 2).
+
+* Rig GN sharded by camera: each rank accumulates its cameras' 28 doubles,
+  the all-reduce sums them, every rank solves the same 6x6 system — the final
+  pose is identical on both ranks and equal to the single-process result.
+* bench.py's weak-scaling reduction: the MAX of the per-rank times is used.
+"""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _gn_ref as G
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene():
+    rng = np.random.default_rng(12)
+    T_true = G.exp_se3_right(np.eye(4), np.array([0.2, -0.1, 1.4, 0.05, -0.03, 0.7]))
+    ext = []
+    for c in range(4):
+        E = np.eye(4)
+        ang = c * np.pi / 2
+        E[:3, :3] = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1]])
+        E[:3, 3] = [0.1 * np.cos(ang), 0.1 * np.sin(ang), 0]
+        ext.append(E)
+    obs = G.synth_rig_obs(rng, T_true, ext, n_per_cam=30, noise=5e-4)
+    T0 = G.exp_se3_right(T_true, np.array([0.03, -0.02, 0.04, 0.02, -0.015, 0.03]))
+    return T_true, T0, ext, obs
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mantis_amd import rig
+
+    T_true, T0, ext, obs = _scene()
+    mine = rig.shard_cameras(len(ext), rank, world)
+    local = obs[np.isin(obs[:, 0].astype(int), mine)]
+
+    def accumulate(T):
+        return G.gn_accumulate(T, ext, local) if len(local) else np.zeros(28)
+
+    def allreduce(acc):
+        t = torch.from_numpy(acc)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+    T, costs = rig.gn_refine(T0, accumulate, allreduce, iterations=6)
+    # bench.py timing reduction: max over ranks
+    t = torch.tensor([1.0 + rank], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out[rank] = (T, costs, float(t.item()), mine)
+    dist.destroy_process_group()
+
+
+def test_camera_sharded_gn_world2():
+    from mantis_amd import rig
+
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    T_true, T0, ext, obs = _scene()
+    T1, costs1 = rig.gn_refine(T0, lambda T: G.gn_accumulate(T, ext, obs), None, iterations=6)
+    Ta, ca, ma, sa = out[0]
+    Tb, cb, mb, sb = out[1]
+    assert sa == [0, 2] and sb == [1, 3]
+    assert ma == mb == 2.0
+    assert np.array_equal(Ta, Tb)  # identical solve on every rank
+    np.testing.assert_allclose(Ta, T1, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(ca, costs1, rtol=1e-9)
+    assert costs1[-1] < 1e-3 * costs1[0]
+    np.testing.assert_allclose(Ta[:3, 3], T_true[:3, 3], atol=2e-3)

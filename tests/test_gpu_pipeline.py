@@ -1,0 +1,143 @@
+"""GPU parity, second part: reference goldens through the C-ABI, the real
+config-1 frame (test/grid1.jpg), config-4 resolution (1920x1080, contour
+tracing without the LDS bitmap), multi-rig batches with rig fusion, and the
+MFMA Gauss-Newton accumulator.
+
+Tolerances: RPP poses 1e-9 absolute (device libm vs glibc ulps in atan2/acos/
+sin/cos inside the 2nd-pose search; the decisions are exact); GN accumulators
+1e-12 relative (MFMA f64 sums in a different order than numpy's matmul).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import _gn_ref as G
+import _oracle as O
+from mantis_amd import synth
+from test_gpu_parity import POSE_TOL, _cmp_debug
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def m720(landmark_map):
+    import mantis_amd as M
+
+    m = M.Mantis(max_cams=8, max_width=1280, max_height=720)
+    m.set_map(*landmark_map)
+    yield m
+    m.close()
+
+
+def test_rpp_reference_golden_on_gpu(m720):
+    d = np.load(os.path.join(GOLD, "rpp_golden.npz"), allow_pickle=False)
+    ip = np.transpose(d["iprts"][:, :2, :], (0, 2, 1))
+    op = np.transpose(d["model"], (0, 2, 1))
+    R, t, e, st = m720.rpp(ip, op)
+    assert np.array_equal(st, d["status"])
+    np.testing.assert_allclose(R, d["R"], atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(t, d["t"], atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(e, d["errs"][:, :2], rtol=1e-9, atol=1e-15)
+
+
+def test_grid1_config1_frame(m720, landmark_map):
+    import mantis_amd as M
+
+    g = np.load(os.path.join(GOLD, "grid1.npz"), allow_pickle=False)
+    img = M.make_image(g["bgr"], g["K"], g["D"])
+    quads = m720.detect_quads(img)
+    assert np.array_equal(quads, g["quads"])
+    orc = O.Oracle(*landmark_map, seed=1)
+    m720.rng_state = 1
+    rig, cams = m720.process([img], rigs=1)
+    o = orc.process(g["bgr"], g["K"], g["D"])
+    _cmp_debug(m720.frame_debug(0), o, "grid1")
+    assert m720.rng_state == orc.rng_state == int(g["rng_state_after"])
+
+
+def test_config4_1080p_frames(landmark_map):
+    import mantis_amd as M
+
+    W, H = 1920, 1080
+    K, D = synth.intrinsics(W, H)
+    m = M.Mantis(max_cams=2, max_width=W, max_height=H)
+    m.set_map(*landmark_map)
+    orc = O.Oracle(*landmark_map, seed=1)
+    rng = np.random.default_rng(77)
+    frames = []
+    for f in range(2):
+        R, pos = synth.random_pose(rng)
+        frames.append(synth.render_host(synth.make_cam(R, pos, W, H), synth.frame_seed(4, f)))
+    m.rng_state = 1
+    m.process([M.make_image(fr, K, D) for fr in frames], rigs=2)
+    for i, fr in enumerate(frames):
+        _cmp_debug(m.frame_debug(i), orc.process(fr, K, D), f"1080p frame {i}")
+    assert m.rng_state == orc.rng_state
+    m.close()
+
+
+def _quat_mat(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def test_two_rig_batch_and_fusion(m720, landmark_map):
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    ext = synth.rig_extrinsics(4)
+    rng = np.random.default_rng(5)
+    imgs, host = [], []
+    for r in range(2):
+        Twb = synth.random_base_pose(rng)
+        for c in range(4):
+            Twc = Twb @ ext[c]
+            fr = synth.render_host(synth.make_cam(Twc[:3, :3], Twc[:3, 3]), synth.frame_seed(3, 10 * r + c))
+            host.append(fr)
+            imgs.append(M.make_image(fr, K, D, T_base_cam=ext[c]))
+    m720.rng_state = 1
+    orc = O.Oracle(*landmark_map, seed=1)
+    rigs, cams = m720.process(imgs, rigs=2)
+    states = []
+    for i, fr in enumerate(host):
+        _cmp_debug(m720.frame_debug(i), orc.process(fr, K, D), f"rig {i // 4} cam {i % 4}")
+        states.append(orc.rng_state)
+    assert rigs[0].rng_state_after == states[3] and rigs[1].rng_state_after == states[7]
+    for r in range(2):
+        cs = cams[4 * r: 4 * r + 4]
+        pub = [i for i in range(4) if cs[i].publish]
+        assert rigs[r].n_cams_published == len(pub)
+        if not pub:
+            continue
+        b = min(pub, key=lambda i: (cs[i].error, i))
+        Twc = np.eye(4)
+        Twc[:3, :3] = _quat_mat(cs[b].orientation_xyzw)
+        Twc[:3, 3] = cs[b].position
+        Twb = Twc @ np.linalg.inv(ext[b])
+        np.testing.assert_allclose(rigs[r].position, Twb[:3, 3], atol=1e-9)
+        assert rigs[r].weight == cs[b].error and rigs[r].publish == 1
+
+
+def test_gn_accumulate_mfma_vs_numpy(m720):
+    import mantis_amd as M
+
+    rng = np.random.default_rng(9)
+    T = G.exp_se3_right(np.eye(4), np.array([0.1, 0.2, 1.3, 0.1, -0.2, 0.4]))
+    ext = synth.rig_extrinsics(4)
+    for n_per in (1, 5, 24, 61):
+        obs = G.synth_rig_obs(rng, T, ext, n_per_cam=n_per, noise=1e-3)
+        Tp = G.exp_se3_right(T, rng.normal(size=6) * 0.01)
+        want = G.gn_accumulate(Tp, ext, obs)
+        acc = np.zeros(28)
+        Tc = np.ascontiguousarray(Tp)
+        E = np.ascontiguousarray(np.array(ext))
+        ob = np.ascontiguousarray(obs)
+        st = M.lib().mantis_gn_accumulate(m720.h, Tc.ctypes.data, E.ctypes.data, len(ext), ob.ctypes.data, len(obs),
+                                          acc.ctypes.data)
+        assert st == 0
+        np.testing.assert_allclose(acc, want, rtol=1e-12, atol=1e-14 * np.abs(want).max())

@@ -1,0 +1,135 @@
+"""Device-logic headers (mantis_amd/csrc/mk_*.h) compiled for the host
+(build/libmantis_hostcheck.so) against the oracle and the goldens, on CPU.
+
+These are the exact per-work-item algorithms the HIP kernels run (RPP phases,
+Jenkins-Traub, libstdc++ sort port, border following, approxPolyDP, the
+parallel contour formulation, bit-packed morphology, fisheye maps), so a
+mismatch here is a device bug found without a GPU. Bar: bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _hostcheck as H
+import _oracle as O
+from mantis_amd import synth
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_rpp_phases_vs_reference_golden():
+    d = np.load(os.path.join(GOLD, "rpp_golden.npz"), allow_pickle=False)
+    for k in range(len(d["model"])):
+        st, R, t, e, code = H.rpp(d["model"][k], d["iprts"][k])
+        assert st == d["status"][k], d["name"][k]
+        assert np.array_equal(R.reshape(-1), d["R"][k].reshape(-1)), d["name"][k]
+        assert np.array_equal(t, d["t"][k]) and np.array_equal(e, d["errs"][k]), d["name"][k]
+
+
+def test_rpp_phases_vs_oracle_hard_cases():
+    rng = np.random.default_rng(77)
+    s = 0.16
+    sq = [np.array([[s, -s, -s, s], [s, s, -s, -s], [0, 0, 0, 0.0]]),
+          np.array([[s, -s, -s, s], [-s, -s, s, s], [0, 0, 0, 0.0]])]
+    for k in range(600):
+        R = synth.rot_z(rng.uniform(0, 6.3)) @ synth.NADIR @ synth.rot_x(rng.normal() * 1.5)
+        t = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(0.5, 3)])
+        m = sq[k % 2]
+        Q = R.T @ m + t[:, None]
+        ip = np.vstack([Q[0] / Q[2], Q[1] / Q[2], np.ones(4)])
+        ip[:2] += rng.normal(size=(2, 4)) * 0.05
+        a, b = H.rpp(m, ip), O.rpp(m, ip)
+        assert a[0] == b[0] and a[4] == b[4]
+        for u, v in zip(a[1:4], b[1:4]):
+            assert np.array_equal(u, v, equal_nan=True)
+
+
+def test_rpoly_vs_reference_golden():
+    d = np.load(os.path.join(GOLD, "rpoly_golden.npz"), allow_pickle=False)
+    for k in range(len(d["coef"])):
+        deg, zr, zi = H.rpoly(d["coef"][k])
+        assert deg == d["degree"][k]
+        assert np.array_equal(zr, d["zr"][k]) and np.array_equal(zi, d["zi"][k])
+
+
+def test_sort_desc_matches_libstdcxx():
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 15, 16, 17, 81, 200, 1024):
+        for ties in (False, True):
+            e = rng.normal(size=n)
+            if ties:
+                e = np.round(e * 2) / 2
+                e[rng.random(n) < 0.1] = np.finfo(np.float64).max
+            assert np.array_equal(H.sort_desc(e), O.sort_desc(e))
+
+
+def _rand_binary(rng, h, w, p):
+    img = (rng.random((h, w)) < p).astype(np.uint8)
+    if rng.random() < 0.5:  # blobs with holes
+        for _ in range(int(rng.integers(1, 6))):
+            y0, x0 = rng.integers(0, h), rng.integers(0, w)
+            y1, x1 = min(h, y0 + int(rng.integers(3, 20))), min(w, x0 + int(rng.integers(3, 20)))
+            img[y0:y1, x0:x1] = 1
+            img[(y0 + y1) // 2, (x0 + x1) // 2] = 0
+    return img * 255
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_parallel_contours_equal_suzuki_abe(mode):
+    rng = np.random.default_rng(11 + mode)
+    for k in range(120):
+        h, w = int(rng.integers(1, 48)), int(rng.integers(1, 48))
+        img = _rand_binary(rng, h, w, rng.uniform(0.05, 0.7))
+        a, ha = H.find_contours(img, mode)
+        b, hb = O.find_contours(img, mode)
+        assert ha == hb and len(a) == len(b)
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
+def test_parallel_contours_on_detector_frame():
+    rng = np.random.default_rng(21)
+    R, pos = synth.random_pose(rng)
+    img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(9, 0))
+    det = O.detector_binary(O.canny(img))
+    a, ha = H.find_contours(det, 2)
+    b, hb = O.find_contours(det, 2)
+    assert ha == hb and len(a) == len(b) and len(a) > 50
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
+
+
+def test_approx_poly_dp():
+    rng = np.random.default_rng(8)
+    for k in range(300):
+        n = int(rng.integers(1, 200))
+        pts = np.cumsum(rng.integers(-3, 4, size=(n, 2)), axis=0).astype(np.int32) + 500
+        for closed in (True, False):
+            eps = float(rng.choice([1.0, 3.0, 10.0]))
+            assert np.array_equal(H.approx_poly(pts, eps, closed), O.approx_poly(pts, eps, closed))
+
+
+def test_bit_packed_morphology():
+    rng = np.random.default_rng(31)
+    for k in range(25):
+        h, w = int(rng.integers(2, 90)), int(rng.integers(2, 140))
+        e = (rng.random((h, w)) < rng.uniform(0.01, 0.6)).astype(np.uint8) * 255
+        det, mask = H.masks_bits(e)
+        assert np.array_equal(det, O.detector_binary(e) != 0)
+        assert np.array_equal(mask, O.clean_mask(e) != 0)
+    R, pos = synth.random_pose(rng)
+    img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(9, 1))
+    cn = O.canny(img)
+    det, mask = H.masks_bits(cn)
+    assert np.array_equal(det, O.detector_binary(cn) != 0)
+    assert np.array_equal(mask, O.clean_mask(cn) != 0)
+
+
+def test_fisheye_maps():
+    rng = np.random.default_rng(3)
+    K, D = synth.intrinsics()
+    xyz = np.column_stack([rng.uniform(-3, 3, 500), rng.uniform(-3, 3, 500), rng.uniform(0.05, 3, 500)])
+    assert np.array_equal(H.distort(xyz, K, D), O.distort(xyz, K, D))
+    px = np.column_stack([rng.uniform(-100, 1400, 500), rng.uniform(-100, 800, 500)])
+    assert np.array_equal(H.undistort(px, K, D), O.undistort(px, K, D))

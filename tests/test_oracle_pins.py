@@ -1,0 +1,94 @@
+"""The CPU oracle pinned against the reference's own known answers and the
+committed golden fixtures (tests/golden/make_golden.py), plus the reference
+RPP/Rpoly compiled in place (oracle/_ref) when it is present.
+
+Bar: bit-exact vs the reference build (same double arithmetic, same op order);
+demo.cpp's Matlab answer to its printed 5 decimals.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from mantis_amd import synth
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def test_demo_known_answer():
+    d = _load("rpp_demo.npz")
+    st, R, t, e, code = O.rpp(d["model"], d["iprts"])
+    assert st == 1 and code == 0
+    # RPP demo.cpp:28-38 (Matlab/Octave, printed to 5 decimals)
+    np.testing.assert_allclose(R, d["matlab_R"], atol=1e-4 + 5e-6, rtol=0)
+    np.testing.assert_allclose(t, d["matlab_t"], atol=1e-4 + 5e-6, rtol=0)
+    # and exactly what the reference RPP.cpp returns
+    assert np.array_equal(R.reshape(-1), d["R"].reshape(-1))
+    assert np.array_equal(t, d["t"])
+    assert np.array_equal(e, d["errs"])
+
+
+def test_rpp_golden_bit_exact():
+    d = _load("rpp_golden.npz")
+    for k in range(len(d["model"])):
+        st, R, t, e, code = O.rpp(d["model"][k], d["iprts"][k])
+        assert st == d["status"][k], d["name"][k]
+        assert np.array_equal(R.reshape(-1), d["R"][k].reshape(-1)), d["name"][k]
+        assert np.array_equal(t, d["t"][k]), d["name"][k]
+        assert np.array_equal(e, d["errs"][k]), d["name"][k]
+
+
+def test_rpoly_golden_bit_exact():
+    d = _load("rpoly_golden.npz")
+    for k in range(len(d["coef"])):
+        deg, zr, zi = O.rpoly(d["coef"][k])
+        assert deg == d["degree"][k]
+        assert np.array_equal(zr, d["zr"][k]) and np.array_equal(zi, d["zi"][k])
+    # (x-1)(x-2)(x-3)(x-4): roots 1..4 in some order and the 5th slot stays (0, 0)
+    assert sorted(np.round(d["zr"][0][:4], 9)) == [1, 2, 3, 4]
+    assert d["zr"][0][4] == 0 and d["zi"][0][4] == 0
+
+
+@pytest.mark.skipif(O.ref() is None, reason="oracle/_ref not built (needs /root/reference)")
+def test_rpp_oracle_vs_reference_build_random():
+    rng = np.random.default_rng(4242)
+    s = 0.16
+    for k in range(300):
+        n = 4 if k % 5 else int(rng.integers(5, 12))
+        model = np.vstack([rng.uniform(-s, s, size=(2, n)), np.zeros((1, n))])
+        R = synth.rot_z(rng.uniform(0, 6.3)) @ synth.NADIR @ synth.rot_x(rng.normal() * 0.5)
+        t = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(0.6, 4)])
+        Q = R.T @ model + t[:, None]
+        ip = np.vstack([Q[0] / Q[2], Q[1] / Q[2], np.ones(n)])
+        ip[:2] += rng.normal(size=(2, n)) * 0.005
+        a = O.rpp(model, ip)
+        b = O.ref_rpp(model, ip)
+        assert a[0] == b[0]
+        if b[0] < 0:
+            continue
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+
+
+def test_map_parse_matches_fixture(landmark_map):
+    white, red, green = landmark_map
+    assert (len(white), len(red), len(green)) == (646, 37, 37)
+    import yaml
+
+    y = yaml.safe_load(open(os.path.join(GOLD, "map.yaml")))
+    for key, ref in (("whiteMap", white), ("redMap", red), ("greenMap", green)):
+        assert np.array_equal(O.parse_coordinates(y[key]), ref), key
+
+
+def test_grid1_oracle_plumbing_golden(landmark_map):
+    g = _load("grid1.npz")
+    orc = O.Oracle(*landmark_map, seed=1)
+    dbg = orc.process(g["bgr"], g["K"], g["D"])
+    quads = np.array(dbg.quads, np.int32)[: dbg.n_quads]
+    assert np.array_equal(quads, g["quads"])
+    assert dbg.reason == g["reason"] and dbg.publish == g["publish"] and dbg.n_hyps == g["n_hyps"]
+    assert dbg.rng_state_after == g["rng_state_after"]
