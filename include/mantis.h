@@ -211,6 +211,11 @@ mantis_status mantis_set_profiling(void* ctx, int32_t on);
  * hypotheses, PF/shift/yaw errors); layout = oracle/oracle.h orc_frame_debug. */
 size_t mantis_frame_debug_size(void);
 mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes);
+/* Work counters of camera-frame `frame` of the last batch: borders, contour
+ * points, raw/kept quads, generated/clustered hypotheses, PF flag, gaussian
+ * offset, overflow flags, then 7 contour-kernel phase ends (10 ns ticks).
+ * Returns the number of int32 written (<= max), -1 on a bad argument. */
+int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t max);
 
 #ifdef __cplusplus
 }

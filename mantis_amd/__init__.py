@@ -108,6 +108,7 @@ _SIGS = {
     "mantis_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "mantis_frame_debug_size": (C.c_size_t, []),
     "mantis_get_frame_debug": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mantis_frame_counters": (C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
     "mantis_gn_accumulate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
                                        C.c_void_p]),
     "mantis_gn_solve": (C.c_int, [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p]),
@@ -223,6 +224,13 @@ class Mantis:
         st = lib().mantis_process_batch(self.h, cams, rigs, n // rigs, out, cam_out)
         self._chk(st, "process_batch")
         return list(out), list(cam_out)
+
+    def frame_counters(self, i):
+        out = np.zeros(16, np.int32)
+        k = lib().mantis_frame_counters(self.h, i, out.ctypes.data, 16)
+        if k < 0:
+            raise MantisError("frame_counters: bad frame index")
+        return out[:k]
 
     def frame_debug(self, i):
         d = FrameDebug()

@@ -115,11 +115,13 @@ struct Ctx {
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
-  uint8_t *d_bgr = nullptr, *d_cls = nullptr, *d_strong = nullptr, *d_edge = nullptr, *d_t0 = nullptr,
-          *d_t1 = nullptr, *d_det = nullptr, *d_mask = nullptr;
+  uint8_t *d_bgr = nullptr, *d_cls = nullptr, *d_strong = nullptr, *d_edge = nullptr,
+          *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
   size_t bstride = 0;                                           // words per frame
+  uint32_t* d_dbits = nullptr;                                  // padded detector bits
+  size_t dstride = 0;
   FrameDesc* d_frames = nullptr;
   Border* d_borders = nullptr;
   int32_t *d_bcount = nullptr, *d_boff = nullptr, *d_pool = nullptr, *d_scratch = nullptr;
@@ -209,12 +211,12 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
 }
 
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
-mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false) {
+mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false, bool det_bytes = false) {
   const size_t P = c->plane;
   const size_t npx = (size_t)W * H;
   const int Wp = W + 2, Hp = H + 2;
   HIP_OK(hipMemsetAsync(c->d_strong, 0, P * n, c->s));
-  HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
+  if (det_bytes) HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
   mark(c, "start");
   dim3 gt((W + TX - 1) / TX, (H + TY - 1) / TY, n);
   k_canny_cls<<<gt, 256, 0, c->s>>>(c->d_frames, c->d_cls, c->d_lab, P, c->cfg.canny_low, 3 * c->cfg.canny_low);
@@ -232,7 +234,10 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   k_bh<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B, 2, 1);
   k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, nullptr, W, H, B, P, 2, 1, 0);
   k_bh<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, W, H, B, 1, 0);
-  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, nullptr, c->d_det, W, H, B, P, 1, 0, 2);
+  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, nullptr, W, H, B, P, 1, 0, 0);
+  const size_t ndw = (size_t)dbits_wpw(W + 2) * (H + 2);
+  k_pack_det<<<dim3(blocks_for(ndw), n), 256, 0, c->s>>>(c->d_b2, c->d_dbits, W, H, B, c->dstride);
+  if (det_bytes) k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, nullptr, c->d_det, W, H, B, P, 1, 0, 2);
   mark(c, "det_morph");
   // cleanImageByEdge mask: M0 then 3 x {dilate, erode}(3+i) and erode(3) -> mask bytes
   k_bm0<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B);
@@ -259,16 +264,18 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
   dim3 gp(blocks_for(np), n);
   dim3 gtile((Wp + CW - 1) / CW, (Hp + CH - 1) / CH, n);
-  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
+  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp, P);
   const size_t nseam = (size_t)((Wp - 1) / CW) * Hp + (size_t)((Hp - 1) / CH) * Wp;
-  k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_det, c->d_lab, Wp, Hp, P);
+  k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp,
+                                                                         P);
   k_cc_flatten<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
-  k_border_emit<<<gp, 256, 0, c->s>>>(c->d_det, c->d_lab, c->d_borders, c->d_st, Wp, Hp, P, kMaxBorders);
+  k_border_emit<<<gp, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_borders, c->d_st, Wp, Hp, P,
+                                      kMaxBorders);
   mark(c, "components");
-  const size_t bits_bytes = ((np + 31) / 32) * 4;
+  const size_t bits_bytes = (size_t)dbits_wpw(Wp) * Hp * 4;
   const int use_lds = bits_bytes <= (size_t)c->lds_bytes ? 1 : 0;
   k_frame_contours<<<n, 1024, use_lds ? bits_bytes : 0, c->s>>>(
-      c->d_det, c->d_borders, c->d_st, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->pool_cap, c->d_quads,
+      c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->pool_cap, c->d_quads,
       c->d_dbg, c->d_frames, Wp, Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon, c->cfg.search_radius_multiplier,
       use_lds);
   mark(c, "contours_quads");
@@ -519,6 +526,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->Hmax = cfg.max_height;
   c->plane = (size_t)(c->Wmax + 2) * (c->Hmax + 2);
   c->bstride = (size_t)((c->Wmax + 31) / 32) * c->Hmax;
+  c->dstride = (size_t)dbits_wpw(c->Wmax + 2) * (c->Hmax + 2);
   c->pool_cap = cfg.max_contour_points;
   const int F = c->F;
   const int per = cfg.particles * cfg.iterations * 6;
@@ -528,12 +536,11 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_cls, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_edge, (size_t)F * c->plane));
-  chk(dalloc(c, &c->d_t0, (size_t)F * c->plane));
-  chk(dalloc(c, &c->d_t1, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_det, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_eb, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
+  chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
   chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_frames, (size_t)F));
@@ -585,7 +592,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_t0, c->d_t1, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine,
                    c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
@@ -705,6 +712,15 @@ mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t
 }
 size_t mantis_frame_debug_size(void) { return sizeof(FrameDebug); }
 
+int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t max) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !out || frame < 0 || frame >= c->F || !c->h_st) return -1;
+  const int n = (int)(sizeof(FrameState) / sizeof(int32_t));
+  const int k = max < n ? max : n;
+  std::memcpy(out, &c->h_st[frame], sizeof(int32_t) * k);
+  return k;
+}
+
 mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out) {
   Ctx* c = (Ctx*)ctx;
   if (!c || !img || !canny_out) return MANTIS_ERR_ARG;
@@ -724,7 +740,7 @@ mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out,
   int W, H;
   mantis_status st = stage_frames(c, img, 1, W, H);
   if (st != MANTIS_OK) return st;
-  if ((st = run_image_stages(c, 1, W, H)) != MANTIS_OK) return st;
+  if ((st = run_image_stages(c, 1, W, H, false, det_out != nullptr)) != MANTIS_OK) return st;
   if (det_out) {
     HIP_OK(hipMemcpy2DAsync(det_out, W, c->d_det + (W + 2) + 1, W + 2, W, H, hipMemcpyDeviceToHost, c->s));
   }

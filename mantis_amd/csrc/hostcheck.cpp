@@ -36,9 +36,10 @@ void hc_sort_desc(const double* err, int n, int* perm) {
   for (int i = 0; i < n; i++) perm[i] = v[i].i;
 }
 
-int hc_approx(const int32_t* pts, int n, double eps, int closed, int32_t* out) {
+int hc_approx(const int32_t* pts, int n, double eps, int closed, int32_t* out, int max_dp) {
   std::vector<int32_t> dst(2 * n + 2), stack(2 * n + 2);
-  int m = mk::approx_poly(pts, n, eps, closed != 0, dst.data(), stack.data());
+  int m = mk::approx_poly(pts, n, eps, closed != 0, dst.data(), stack.data(), max_dp);
+  if (m > n) return m;
   std::memcpy(out, dst.data(), sizeof(int32_t) * 2 * m);
   return m;
 }
@@ -97,13 +98,20 @@ int hc_find_contours(const uint8_t* bin, int w, int h, int mode, int32_t* pts, i
     return a.key > b.key;
   });
   if ((int)bs.size() > max_c) return -1;
-  auto nz = [&](int idx) { return img[idx] != 0; };
+  // the device tracer: packed 8-neighbourhood per step
+  auto nb = [&](int x, int y) {
+    auto row = [&](int yy) {
+      const uint8_t* r = img.data() + (size_t)yy * Wp;
+      return (uint32_t)(r[x - 1] != 0) | ((uint32_t)(r[x] != 0) << 1) | ((uint32_t)(r[x + 1] != 0) << 2);
+    };
+    return mk::nb8_from_rows(row(y - 1), row(y), row(y + 1));
+  };
   int off = 0;
   for (size_t i = 0; i < bs.size(); i++) {
     int sx = bs[i].start % Wp, sy = bs[i].start / Wp;
-    int n = mk::trace_border(nz, Wp, sx, sy, bs[i].hole != 0, nullptr, 0);
+    int n = mk::trace_border_nb(nb, sx, sy, bs[i].hole != 0, nullptr, 0);
     if (off + n > max_pts) return -1;
-    mk::trace_border(nz, Wp, sx, sy, bs[i].hole != 0, pts + 2 * off, n);
+    mk::trace_border_nb(nb, sx, sy, bs[i].hole != 0, pts + 2 * off, n);
     meta[3 * i] = off;
     meta[3 * i + 1] = n;
     meta[3 * i + 2] = bs[i].hole;

@@ -270,6 +270,32 @@ __global__ __launch_bounds__(256) void k_bm0(const uint32_t* __restrict__ E, uin
   }
 }
 
+// Padded detector binary as a row-aligned bit plane: (W+2) x (H+2) with the
+// zero ring, WPW = ceil((W+2)/32) + 1 words per row (the spare word lets a
+// 64-bit window at any x be read without a bounds test).
+__device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
+__device__ inline uint32_t dbit(const uint32_t* B, int wpw, int x, int y) {
+  return (B[(size_t)y * wpw + (x >> 5)] >> (x & 31)) & 1u;
+}
+__global__ __launch_bounds__(256) void k_pack_det(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W,
+                                                  int H, size_t bstride, size_t dstride) {
+  const int f = blockIdx.y;
+  const int WW = bits::words(W), Wp = W + 2, Hp = H + 2, wpw = dbits_wpw(Wp);
+  const size_t n = (size_t)wpw * Hp;
+  const uint32_t* s = src + (size_t)f * bstride;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(k % wpw), py = (int)(k / wpw);
+    uint32_t v = 0;
+    if (py > 0 && py < Hp - 1) {
+      const uint32_t* row = s + (size_t)(py - 1) * WW;
+      const uint32_t cur = w < WW ? row[w] : 0u;
+      const uint32_t prv = (w > 0 && w - 1 < WW) ? row[w - 1] : 0u;
+      v = (cur << 1) | (prv >> 31);  // padded x = image x + 1
+    }
+    dst[(size_t)f * dstride + k] = v;
+  }
+}
+
 // ==================================================== contour components
 // On the zero-ringed detector binary (Wp x Hp): foreground 8-connected,
 // background 4-connected; the ring makes the outside background component 0.
@@ -320,18 +346,19 @@ __device__ inline void lds_union(int* L, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_cc_tile(const uint8_t* __restrict__ det, int32_t* __restrict__ lab, int Wp,
-                                                 int Hp, size_t plane) {
+__global__ __launch_bounds__(256) void k_cc_tile(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                 int32_t* __restrict__ lab, int Wp, int Hp, size_t plane) {
   __shared__ uint8_t C[CH * CW];  // 0 background, 1 foreground, 2 outside the image
   __shared__ int L[CH * CW];
   const int f = blockIdx.z;
   const int x0 = blockIdx.x * CW, y0 = blockIdx.y * CH;
-  const uint8_t* d = det + (size_t)f * plane;
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  const int wpw = dbits_wpw(Wp);
   int32_t* l = lab + (size_t)f * plane;
   const int t = threadIdx.x;
   for (int i = t; i < CH * CW; i += 256) {
     const int x = x0 + (i % CW), y = y0 + (i / CW);
-    C[i] = (x < Wp && y < Hp) ? (d[(size_t)y * Wp + x] ? 1 : 0) : 2;
+    C[i] = (x < Wp && y < Hp) ? (uint8_t)dbit(B, wpw, x, y) : 2;
   }
   __syncthreads();
   {  // row runs: 8 threads per row, 8 pixels each, sequential within the segment
@@ -375,10 +402,11 @@ __global__ __launch_bounds__(256) void k_cc_tile(const uint8_t* __restrict__ det
 }
 
 // one thread per seam pixel: vertical seams (x = k*CW) then horizontal (y = k*CH)
-__global__ __launch_bounds__(256) void k_cc_seam(const uint8_t* __restrict__ det, int32_t* lab, int Wp, int Hp,
-                                                 size_t plane) {
+__global__ __launch_bounds__(256) void k_cc_seam(const uint32_t* __restrict__ dbits, size_t dstride, int32_t* lab,
+                                                 int Wp, int Hp, size_t plane) {
   const int f = blockIdx.y;
-  const uint8_t* d = det + (size_t)f * plane;
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  const int wpw = dbits_wpw(Wp);
   int32_t* l = lab + (size_t)f * plane;
   const int nvs = (Wp - 1) / CW, nhs = (Hp - 1) / CH;
   const size_t nv = (size_t)nvs * Hp, n = nv + (size_t)nhs * Wp;
@@ -388,18 +416,18 @@ __global__ __launch_bounds__(256) void k_cc_seam(const uint8_t* __restrict__ det
     if (vert) { x = (int)(k / Hp + 1) * CW; y = (int)(k % Hp); }
     else { const size_t h = k - nv; y = (int)(h / Wp + 1) * CH; x = (int)(h % Wp); }
     const int p = y * Wp + x;
-    const int c = d[p] ? 1 : 0;
+    const uint32_t c = dbit(B, wpw, x, y);
     if (vert) {
-      if ((d[p - 1] ? 1 : 0) == c) uf_union_c(l, p, p - 1);
+      if (dbit(B, wpw, x - 1, y) == c) uf_union_c(l, p, p - 1);
       if (c) {
-        if (y > 0 && d[p - Wp - 1]) uf_union_c(l, p, p - Wp - 1);
-        if (y + 1 < Hp && d[p + Wp - 1]) uf_union_c(l, p, p + Wp - 1);
+        if (y > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
+        if (y + 1 < Hp && dbit(B, wpw, x - 1, y + 1)) uf_union_c(l, p, p + Wp - 1);
       }
     } else {
-      if ((d[p - Wp] ? 1 : 0) == c) uf_union_c(l, p, p - Wp);
+      if (dbit(B, wpw, x, y - 1) == c) uf_union_c(l, p, p - Wp);
       if (c) {
-        if (x > 0 && d[p - Wp - 1]) uf_union_c(l, p, p - Wp - 1);
-        if (x + 1 < Wp && d[p - Wp + 1]) uf_union_c(l, p, p - Wp + 1);
+        if (x > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
+        if (x + 1 < Wp && dbit(B, wpw, x + 1, y - 1)) uf_union_c(l, p, p - Wp + 1);
       }
     }
   }
@@ -412,17 +440,18 @@ __global__ __launch_bounds__(256) void k_cc_flatten(int32_t* lab, size_t n, size
 }
 // One border per fg component (outer, at its root) and per enclosed bg
 // component (hole, left of its root).
-__global__ __launch_bounds__(256) void k_border_emit(const uint8_t* __restrict__ det, const int32_t* __restrict__ lab,
-                                                     Border* __restrict__ borders, FrameState* st, int Wp, int Hp,
-                                                     size_t plane, int cap) {
+__global__ __launch_bounds__(256) void k_border_emit(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                     const int32_t* __restrict__ lab, Border* __restrict__ borders,
+                                                     FrameState* st, int Wp, int Hp, size_t plane, int cap) {
   const int f = blockIdx.y;
   const size_t n = (size_t)Wp * Hp;
-  const uint8_t* d = det + (size_t)f * plane;
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  const int wpw = dbits_wpw(Wp);
   const int32_t* l = lab + (size_t)f * plane;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
     if (l[p] != (int32_t)p) continue;
     Border b;
-    if (d[p]) {
+    if (dbit(B, wpw, (int)(p % Wp), (int)(p / Wp))) {
       b.key = (int32_t)p; b.start = (int32_t)p; b.hole = 0; b.parent = (int32_t)p;
     } else {
       if (p == 0) continue;
@@ -435,26 +464,29 @@ __global__ __launch_bounds__(256) void k_border_emit(const uint8_t* __restrict__
 }
 
 // ============================================ per-frame contour -> quads
-struct ByteNZ {
-  const uint8_t* d;
-  __device__ bool operator()(int i) const { return d[i] != 0; }
-};
-struct BitNZ {
+// 8-neighbourhood of padded pixel (x, y) from the row-aligned bit plane
+// (LDS copy or global): three 64-bit windows starting at x - 1.
+struct BitsNB {
   const uint32_t* b;
-  __device__ bool operator()(int i) const { return (b[i >> 5] >> (i & 31)) & 1u; }
+  int wpw;
+  __device__ uint32_t row3(int x, int y) const {
+    const uint32_t* r = b + (size_t)y * wpw + ((x - 1) >> 5);
+    const uint64_t v = ((uint64_t)r[1] << 32) | r[0];
+    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  }
+  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
 
-template <class NZ>
-__device__ void contour_pass(const NZ& nz, int Wp, const Border* bs, int nb, int32_t* counts, int32_t* offs,
+__device__ void contour_pass(const BitsNB& nb, int Wp, const Border* bs, int nb_count, int32_t* counts, int32_t* offs,
                              int32_t* pool, int pool_cap, int pass) {
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+  for (int i = threadIdx.x; i < nb_count; i += blockDim.x) {
     const Border b = bs[i];
-    int sx = b.start % Wp, sy = b.start / Wp;
+    const int sx = b.start % Wp, sy = b.start / Wp;
     if (pass == 0) {
-      counts[i] = trace_border(nz, Wp, sx, sy, b.hole != 0, nullptr, 0);
+      counts[i] = trace_border_nb(nb, sx, sy, b.hole != 0, nullptr, 0);
     } else {
-      int o = offs[i], c = counts[i];
-      if (o + c <= pool_cap) trace_border(nz, Wp, sx, sy, b.hole != 0, pool + 2 * (size_t)o, c);
+      const int o = offs[i], c = counts[i];
+      if (o + c <= pool_cap) trace_border_nb(nb, sx, sy, b.hole != 0, pool + 2 * (size_t)o, c);
     }
   }
 }
@@ -472,7 +504,8 @@ struct RawQuad {
   int32_t parent, hole, key;
 };
 
-__global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restrict__ det, const Border* __restrict__ borders,
+__global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                         const Border* __restrict__ borders,
                                                          FrameState* st, int32_t* __restrict__ counts,
                                                          int32_t* __restrict__ offs, int32_t* __restrict__ pool,
                                                          int32_t* __restrict__ scratch, int pool_cap,
@@ -492,7 +525,8 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
   __shared__ double qside[kMaxQuads];
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
-  const uint8_t* d = det + (size_t)f * plane;
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  const int wpw = dbits_wpw(Wp);
   const Border* bs = borders + (size_t)f * border_cap;
   int32_t* cnt = counts + (size_t)f * border_cap;
   int32_t* off = offs + (size_t)f * border_cap;
@@ -500,22 +534,20 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
   int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
-  const size_t npx = (size_t)Wp * Hp;
+  const uint64_t t0 = wall_clock64();
+#define MK_TICK(k) \
+  if (tid == 0) st[f].ticks[k] = (int32_t)(wall_clock64() - t0);
+  const size_t nwords = (size_t)wpw * Hp;
   if (use_lds) {
-    const size_t nw = (npx + 31) / 32;
-    for (size_t w = tid; w < nw; w += blockDim.x) {
-      uint32_t v = 0;
-      size_t base = w * 32;
-      for (int k = 0; k < 32; k++)
-        if (base + k < npx && d[base + k]) v |= 1u << k;
-      lds_bits[w] = v;
-    }
+    for (size_t w = tid; w < nwords; w += blockDim.x) lds_bits[w] = B[w];
   }
+  const BitsNB nbh{use_lds ? (const uint32_t*)lds_bits : B, wpw};
   if (tid == 0) { nraw = 0; total = 0; }
   __syncthreads();
-  if (use_lds) contour_pass(BitNZ{lds_bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
-  else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
+  MK_TICK(0);
+  contour_pass(nbh, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
   __syncthreads();
+  MK_TICK(1);
   // exclusive scan of the point counts, blockDim at a time
   for (int base = 0; base < nb; base += blockDim.x) {
     int i = base + tid;
@@ -542,15 +574,16 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
     }
     return;
   }
-  if (use_lds) contour_pass(BitNZ{lds_bits}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
-  else contour_pass(ByteNZ{d}, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
+  MK_TICK(2);
+  contour_pass(nbh, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
   __syncthreads();
+  MK_TICK(3);
   // approxPolyDP per border (eps = POLYGON_EPSILON, closed); keep 4-vertex results
   for (int i = tid; i < nb; i += blockDim.x) {
     int o = off[i], c = cnt[i];
     int32_t* dst = sc + 4 * (size_t)o;
     int32_t* stk = dst + 2 * (size_t)c;
-    int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk);
+    int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
     if (m == 4) {
       int q = atomicAdd(&nraw, 1);
       if (q < kMaxQuads) {
@@ -564,6 +597,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
     }
   }
   __syncthreads();
+  MK_TICK(4);
   const int nq = nraw < kMaxQuads ? nraw : kMaxQuads;
   // position in the CCOMP output order (keys are distinct)
   for (int i = tid; i < nq; i += blockDim.x) {
@@ -650,6 +684,9 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint8_t* __restri
     quads[(size_t)f * kMaxQuads + k] = q;
     for (int c = 0; c < 8; c++) { dbg[f].quads[k][c] = q.c[c]; dbg[f].test_pts[k][c] = q.tp[c]; }
   }
+  __syncthreads();
+  MK_TICK(5);
+#undef MK_TICK
 }
 
 // ================================================================ RPP

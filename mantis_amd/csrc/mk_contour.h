@@ -67,10 +67,73 @@ MK_HD int trace_border(const NZ& nz, int Wp, int sx, int sy, bool hole, int32_t*
   return n;
 }
 
+// Same border following driven by the packed 8-neighbourhood of the current
+// pixel: bit k of nb(x, y) = pixel in direction code k is nonzero (padded
+// coordinates). One neighbourhood fetch per step replaces up to 8 probes;
+// the next direction is a rotate + count-trailing-zeros. Equal to
+// trace_border point for point (tests/test_host_logic.py).
+MK_HD uint32_t nb8_from_rows(uint32_t up, uint32_t mid, uint32_t dn) {
+  // each argument: 3 bits (x-1, x, x+1) of one row
+  return ((mid >> 2) & 1u) | (((up >> 2) & 1u) << 1) | (((up >> 1) & 1u) << 2) | ((up & 1u) << 3) |
+         ((mid & 1u) << 4) | ((dn & 1u) << 5) | (((dn >> 1) & 1u) << 6) | (((dn >> 2) & 1u) << 7);
+}
+MK_HD int ctz32(uint32_t v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_ctz(v);
+#else
+  int k = 0;
+  while (!(v & 1u)) { v >>= 1; k++; }
+  return k;
+#endif
+}
+template <class NB>
+MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out, int cap) {
+  int x = sx, y = sy;
+  uint32_t m = nb(x, y);
+  const int s_end0 = hole ? 0 : 4;
+  int s = s_end0;
+  do {
+    s = (s - 1) & 7;
+  } while (!((m >> s) & 1u) && s != s_end0);
+  int px = sx - 1, py = sy - 1;
+  if (s == s_end0) {
+    if (out && cap > 0) { out[0] = px; out[1] = py; }
+    return 1;
+  }
+  const int x1 = sx + code_dx(s), y1 = sy + code_dy(s);  // i1
+  int n = 0;
+  int prev_s = s ^ 4;
+  // (x, y) = i3
+  for (;;) {
+    // first set direction after s, counter-clockwise: s+1, s+2, ...
+    const uint32_t r = ((m | (m << 8)) >> (s + 1)) & 0xffu;
+    s = (s + 1 + ctz32(r)) & 7;
+    if (s != prev_s) {
+      if (out && n < cap) { out[2 * n] = px; out[2 * n + 1] = py; }
+      n++;
+      prev_s = s;
+    }
+    const int dx = code_dx(s), dy = code_dy(s);
+    px += dx;
+    py += dy;
+    const int x4 = x + dx, y4 = y + dy;
+    if (x4 == sx && y4 == sy && x == x1 && y == y1) break;
+    x = x4;
+    y = y4;
+    m = nb(x, y);
+    s = (s + 4) & 7;
+  }
+  return n;
+}
+
 // cv::approxPolyDP (approxPolyDP_<int>, closed or open) on n points `src`
 // (x,y int pairs). dst needs n pairs, stack n slices (2 ints each).
 // Returns the output count.
-MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack) {
+// max_dp > 0: stop once the Douglas-Peucker stage has emitted max_dp points
+// and return max_dp + 1 (the quad detector passes 10: the clean-up removes at
+// most every other point, so 10 or more DP points can never end as 4).
+MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack,
+                      int max_dp = 0) {
   int count = count0;
   if (count == 0) return 0;
   int top = 0;
@@ -158,6 +221,7 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
     }
     if (le_eps) {
       dst[2 * new_count] = spx; dst[2 * new_count + 1] = spy; new_count++;
+      if (max_dp > 0 && new_count >= max_dp) return max_dp + 1;
     } else {
       rs_e = sl_e;
       sl_e = rs_s;

@@ -95,7 +95,7 @@ struct FrameState {
   int32_t reaches_pf;
   int32_t gauss_offset;  // index into the gaussian stream (floats)
   int32_t overflow;      // bit 0 borders, 1 points, 2 quads, 3 hyps
-  int32_t pad[7];
+  int32_t ticks[7];      // k_frame_contours phase ends, 10 ns wall-clock ticks from its start
 };
 
 }  // namespace mk

@@ -22,7 +22,7 @@ def lib():
         L.hc_rpp.restype = C.c_int
         L.hc_rpoly.restype = C.c_int
         L.hc_approx.restype = C.c_int
-        L.hc_approx.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_void_p]
+        L.hc_approx.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int]
         L.hc_find_contours.restype = C.c_int
         L.hc_find_contours.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                        C.c_int]
@@ -66,10 +66,13 @@ def sort_desc(err):
     return perm
 
 
-def approx_poly(pts, eps, closed=True):
+def approx_poly(pts, eps, closed=True, max_dp=0):
+    """max_dp > 0: the quad detector's early exit (returns None when it fires)."""
     pts = np.ascontiguousarray(pts, np.int32).reshape(-1, 2)
     out = np.zeros((len(pts) + 1, 2), np.int32)
-    m = lib().hc_approx(pts.ctypes.data, len(pts), float(eps), int(closed), out.ctypes.data)
+    m = lib().hc_approx(pts.ctypes.data, len(pts), float(eps), int(closed), out.ctypes.data, int(max_dp))
+    if m > len(pts):
+        return None
     return out[:m]
 
 

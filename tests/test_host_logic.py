@@ -110,6 +110,32 @@ def test_approx_poly_dp():
             assert np.array_equal(H.approx_poly(pts, eps, closed), O.approx_poly(pts, eps, closed))
 
 
+def test_approx_early_exit_keeps_every_quad():
+    """DP output >= 10 points can never clean up to 4 (the clean-up removes at
+    most every other point), so the detector stops DP there."""
+    rng = np.random.default_rng(12)
+    quads = 0
+    contours = []
+    for k in range(4):
+        R, pos = synth.random_pose(rng)
+        img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(9, 10 + k))
+        contours += H.find_contours(O.detector_binary(O.canny(img)), 2)[0]
+    for k in range(400):
+        n = int(rng.integers(3, 400))
+        t = np.sort(rng.uniform(0, 2 * np.pi, n))
+        r = rng.uniform(20, 200) * (1 + 0.3 * np.cos(rng.integers(3, 6) * t))
+        contours.append(np.column_stack([500 + r * np.cos(t), 500 + r * np.sin(t)]).astype(np.int32))
+    for c in contours:
+        full = O.approx_poly(c, 10.0, True)
+        fast = H.approx_poly(c, 10.0, True, max_dp=10)
+        if len(full) == 4:
+            quads += 1
+            assert fast is not None and np.array_equal(fast, full)
+        else:
+            assert fast is None or len(fast) != 4
+    assert quads > 100
+
+
 def test_bit_packed_morphology():
     rng = np.random.default_rng(31)
     for k in range(25):
