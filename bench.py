@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rigs", type=int, default=32, help="rigs per step per GPU")
+    p.add_argument("--rigs", type=int, default=128, help="rigs per step per GPU")
     p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
     p.add_argument("--latency-iters", type=int, default=15)
     p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
