@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--rigs", type=int, default=128, help="rigs per step per GPU")
     p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
+    p.add_argument("--contexts", type=int, default=2,
+                   help="library contexts per GPU, each driven by its own host thread (one ctx per thread, "
+                        "include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
     p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
     p.add_argument("--no-cpu", action="store_true")
@@ -76,8 +79,15 @@ def main():
     white, red, green = synth.load_map()
     K, D = synth.intrinsics(W, H)
     n_frames = a.rigs * CAMS
-    m = M.Mantis(M.default_config(device=local, max_cams=n_frames, max_width=W, max_height=H))
-    m.set_map(white, red, green)
+    nctx = max(1, min(a.contexts, a.rigs))
+    assert a.rigs % nctx == 0, "--rigs must be a multiple of --contexts"
+    rigs_ctx = a.rigs // nctx
+    ctxs = []
+    for _ in range(nctx):
+        mc = M.Mantis(M.default_config(device=local, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H))
+        mc.set_map(white, red, green)
+        ctxs.append(mc)
+    m = ctxs[0]
 
     # ---- synthetic rigs rendered into HBM once
     rng = np.random.default_rng(1000 + rank)
@@ -94,19 +104,33 @@ def main():
     dev = m.device_alloc(nd * fb)
     seeds = [synth.frame_seed(3, i + 100000 * rank) for i in range(nd)]
     m.synth_render(cams, seeds, dev)
+    m.synchronize()
     imgs = []
     for i in range(n_frames):
         j = i % nd
         imgs.append(M.make_image(None, K, D, T_base_cam=Tbc[j], device_ptr=dev + j * fb, width=W, height=H))
+    per_ctx = [imgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS] for k in range(nctx)]
+    from concurrent.futures import ThreadPoolExecutor
+
+    pool = ThreadPoolExecutor(max_workers=nctx)
+
+    def run_step():
+        """One step: every context processes its share of the rigs, concurrently."""
+        futs = [pool.submit(ctxs[k].process, per_ctx[k], rigs_ctx) for k in range(nctx)]
+        outs = [f.result() for f in futs]
+        rig = [r for o in outs for r in o[0]]
+        cam = [c for o in outs for c in o[1]]
+        return rig, cam
 
     def barrier_sync():
         if dist is not None:
             dist.barrier()
-        m.synchronize()
+        for mc in ctxs:
+            mc.synchronize()
 
     # ---- warmup
     for _ in range(a.warmup):
-        m.process(imgs, rigs=a.rigs)
+        run_step()
 
     # ---- timed region: stage events on the library stream
     m.set_profiling(True)
@@ -116,7 +140,7 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        rig, cam = m.process(imgs, rigs=a.rigs)
+        rig, cam = run_step()
         for name, ms in m.kernel_times():
             stage_ms[name] = stage_ms.get(name, 0.0) + ms
         scored += sum(c.n_scored for c in cam)
@@ -140,7 +164,7 @@ def main():
     # ---- dominant kernel roofline (per launch = per step)
     avg = {k: v / a.steps for k, v in stage_ms.items()}
     dom = max(avg, key=avg.get) if avg else None
-    frames_step = n_frames
+    frames_step = rigs_ctx * CAMS  # stage events are recorded on context 0's stream, over its frames
     scored_per_frame = scored / max(1, a.steps * n_frames)
     slow_per_frame = 80.0
     fast_per_frame = max(0.0, scored_per_frame - slow_per_frame)
@@ -177,7 +201,7 @@ def main():
                                                     FLOPS_PER_WINDOW * 37 * slow_per_frame) / dur_s / 1e12, 4)
                 if dom == "score_pf_yaw" else None,
                 "stages_ms": {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}}
-    path_bytes = frames_step * (6 * W * H + 3 * (s_fast + s_slow))
+    path_bytes = n_frames * (6 * W * H + 3 * (s_fast + s_slow))
 
     # ---- p50 latency of one rig (host submit -> result on host)
     lat = []
@@ -217,6 +241,7 @@ def main():
             "data": "synthetic fisheye grid frames rendered in HBM (SURVEY §8d scene), map.yaml landmarks",
             "config": {"workload": "config3: 4-cam 1280x720 rig, shared map, full mantis3 path per camera",
                        "rigs_per_step_per_gpu": a.rigs, "cams_per_rig": CAMS, "frames_per_step_per_gpu": n_frames,
+                       "contexts_per_gpu": nctx,
                        "resolution": [W, H], "landmarks": LANDMARKS, "parallelism": f"rig-data-parallel x{world}"},
             "p50_latency_ms": round(p50, 3),
             "camera_frames_per_s": round(value * CAMS, 2),
@@ -226,7 +251,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    m.close()
+    pool.shutdown()
+    for mc in ctxs:
+        mc.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -121,6 +121,7 @@ struct Ctx {
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
   size_t bstride = 0;                                           // words per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
+  CcCand* d_cand = nullptr;
   size_t dstride = 0;
   FrameDesc* d_frames = nullptr;
   Border* d_borders = nullptr;
@@ -164,6 +165,13 @@ void mark(Ctx* c, const char* name) {
   }
   (void)hipEventRecord(c->ev[c->ev_names.size()], c->s);
   c->ev_names.push_back(name);
+}
+
+// Entry points may be called from any host thread (one ctx per thread at a
+// time): make the ctx's GPU current on the calling thread.
+inline void bind_device(const Ctx* c) {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess || d != c->cfg.device) (void)hipSetDevice(c->cfg.device);
 }
 
 inline int blocks_for(size_t n, int per = 256, int cap = 4096) {
@@ -215,15 +223,17 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const size_t P = c->plane;
   const size_t npx = (size_t)W * H;
   const int Wp = W + 2, Hp = H + 2;
-  HIP_OK(hipMemsetAsync(c->d_strong, 0, P * n, c->s));
   if (det_bytes) HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
   mark(c, "start");
   dim3 gt((W + TX - 1) / TX, (H + TY - 1) / TY, n);
-  k_canny_cls<<<gt, 256, 0, c->s>>>(c->d_frames, c->d_cls, c->d_lab, P, c->cfg.canny_low, 3 * c->cfg.canny_low);
+  k_canny_cls<<<gt, 256, 0, c->s>>>(c->d_frames, c->d_cls, P, c->cfg.canny_low, 3 * c->cfg.canny_low);
   mark(c, "canny_nms");
   dim3 gp(blocks_for(npx), n);
-  k_uf_merge8<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, W, H, P);
-  k_hyst_flatten<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
+  dim3 ght((W + CW - 1) / CW, (H + CH - 1) / CH, n);
+  k_hyst_tile<<<ght, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
+  const size_t nhseam = (size_t)((W - 1) / CW) * H + (size_t)((H - 1) / CH) * W;
+  k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_cls, c->d_lab, W, H, P);
+  k_hyst_strong<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
   const size_t nw = (size_t)((W + 31) / 32) * H;
   dim3 gw(blocks_for(nw), n);
   const size_t B = c->bstride;
@@ -264,13 +274,12 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
   dim3 gp(blocks_for(np), n);
   dim3 gtile((Wp + CW - 1) / CW, (Hp + CH - 1) / CH, n);
-  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp, P);
+  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_st, Wp, Hp, P);
   const size_t nseam = (size_t)((Wp - 1) / CW) * Hp + (size_t)((Hp - 1) / CH) * Wp;
   k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp,
                                                                          P);
-  k_cc_flatten<<<gp, 256, 0, c->s>>>(c->d_lab, np, P);
-  k_border_emit<<<gp, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_borders, c->d_st, Wp, Hp, P,
-                                      kMaxBorders);
+  k_border_emit<<<dim3(64, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_borders, c->d_st, Wp,
+                                               P, kMaxBorders);
   mark(c, "components");
   const size_t bits_bytes = (size_t)dbits_wpw(Wp) * Hp * 4;
   const int use_lds = bits_bytes <= (size_t)c->lds_bytes ? 1 : 0;
@@ -541,6 +550,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
+  chk(dalloc(c, &c->d_cand, (size_t)F * kMaxCand));
   chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_frames, (size_t)F));
@@ -589,10 +599,11 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
 
 mantis_status mantis_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine,
                    c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
@@ -615,6 +626,7 @@ const char* mantis_last_error(void* ctx) {
 mantis_status mantis_set_map(void* ctx, const double* white, int32_t nw, const double* red, int32_t nr,
                              const double* green, int32_t ng) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || nw < 0 || nr < 0 || ng < 0 || nw + nr + ng > 768 || ng > 64 || (nw && !white) || (nr && !red) ||
       (ng && !green)) {
     if (c) c->err = "map: need nw+nr+ng <= 768 and ng <= 64";
@@ -673,6 +685,7 @@ mantis_status mantis_rng_set(void* ctx, uint64_t state) {
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
                                    mantis_result* out, mantis_cam_result* cam_out) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !cams || n_rigs <= 0 || cams_per_rig <= 0) return MANTIS_ERR_ARG;
   const int n = n_rigs * cams_per_rig;
   mantis_status st = process_frames(c, cams, n);
@@ -702,6 +715,7 @@ mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams
 
 mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !out || frame < 0 || frame >= c->F || bytes != sizeof(FrameDebug)) {
     if (c) c->err = "mantis_get_frame_debug: bad frame or size";
     return MANTIS_ERR_ARG;
@@ -714,6 +728,7 @@ size_t mantis_frame_debug_size(void) { return sizeof(FrameDebug); }
 
 int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t max) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !out || frame < 0 || frame >= c->F || !c->h_st) return -1;
   const int n = (int)(sizeof(FrameState) / sizeof(int32_t));
   const int k = max < n ? max : n;
@@ -723,6 +738,7 @@ int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t ma
 
 mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !img || !canny_out) return MANTIS_ERR_ARG;
   int W, H;
   mantis_status st = stage_frames(c, img, 1, W, H);
@@ -736,6 +752,7 @@ mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_ou
 
 mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out, uint8_t* mask_out) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !img) return MANTIS_ERR_ARG;
   int W, H;
   mantis_status st = stage_frames(c, img, 1, W, H);
@@ -754,6 +771,7 @@ mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out,
 mantis_status mantis_detect_quads(void* ctx, const mantis_image* img, int32_t* corners, int32_t max_quads,
                                   int32_t* n_quads) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !img || !n_quads) return MANTIS_ERR_ARG;
   int W, H;
   mantis_status st = stage_frames(c, img, 1, W, H);
@@ -777,6 +795,7 @@ mantis_status mantis_detect_quads(void* ctx, const mantis_image* img, int32_t* c
 mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
                                       int32_t n, int32_t fast, double* err, int32_t* nproj) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !img || !c2w || n <= 0 || !err || !nproj) return MANTIS_ERR_ARG;
   if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
   int W, H;
@@ -812,6 +831,7 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
 mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
                                double* t, double* errs, int32_t* rpp_status) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !img_pts || !obj_pts || n <= 0 || !R || !t || !errs || !rpp_status) return MANTIS_ERR_ARG;
   double *d_ip, *d_op;
   RppItem* d_it;
@@ -845,6 +865,7 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
 mantis_status mantis_synth_render(void* ctx, const mantis_synth_cam* cams, int32_t n, const uint64_t* seeds,
                                   uint8_t* out_dev) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !cams || n <= 0 || !seeds || !out_dev) return MANTIS_ERR_ARG;
   static_assert(sizeof(mantis_synth_cam) == sizeof(mantis_synth::Cam), "synth cam layout");
   mantis_synth::Cam* d_c;
@@ -864,6 +885,7 @@ mantis_status mantis_synth_render(void* ctx, const mantis_synth_cam* cams, int32
 
 mantis_status mantis_device_alloc(void* ctx, size_t bytes, void** dev_ptr) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !dev_ptr) return MANTIS_ERR_ARG;
   if (hipMalloc(dev_ptr, bytes) != hipSuccess) { c->err = "hipMalloc failed"; return MANTIS_ERR_OOM; }
   c->user_allocs.push_back(*dev_ptr);
@@ -871,6 +893,7 @@ mantis_status mantis_device_alloc(void* ctx, size_t bytes, void** dev_ptr) {
 }
 mantis_status mantis_device_free(void* ctx, void* dev_ptr) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   auto it = std::find(c->user_allocs.begin(), c->user_allocs.end(), dev_ptr);
   if (it == c->user_allocs.end()) return MANTIS_ERR_ARG;
@@ -880,6 +903,7 @@ mantis_status mantis_device_free(void* ctx, void* dev_ptr) {
 }
 mantis_status mantis_memcpy_h2d(void* ctx, void* dst, const void* src, size_t bytes) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
@@ -887,6 +911,7 @@ mantis_status mantis_memcpy_h2d(void* ctx, void* dst, const void* src, size_t by
 }
 mantis_status mantis_memcpy_d2h(void* ctx, void* dst, const void* src, size_t bytes) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
@@ -894,12 +919,14 @@ mantis_status mantis_memcpy_d2h(void* ctx, void* dst, const void* src, size_t by
 }
 mantis_status mantis_synchronize(void* ctx) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   HIP_OK(hipStreamSynchronize(c->s));
   return MANTIS_OK;
 }
 int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t max) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return 0;
   int n = (int)c->last_ms.size();
   for (int i = 0; i < n && i < max; i++) {
@@ -910,6 +937,7 @@ int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t ma
 }
 mantis_status mantis_set_profiling(void* ctx, int32_t on) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
   c->prof = on != 0;
   return MANTIS_OK;

@@ -109,6 +109,7 @@ extern "C" {
 mantis_status mantis_gn_accumulate(void* ctx, const double* T_w_b, const double* T_base_cam, int32_t n_cams,
                                    const double* obs, int32_t n_obs, double* acc28) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !T_w_b || !T_base_cam || n_cams <= 0 || (n_obs > 0 && !obs) || !acc28) return MANTIS_ERR_ARG;
   std::vector<GnCam> cams(n_cams);
   for (int i = 0; i < n_cams; i++) {
@@ -190,6 +191,7 @@ mantis_status mantis_comm_unique_id(void* id128) {
 
 mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int32_t rank) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !id128 || nranks <= 0 || rank < 0 || rank >= nranks) return MANTIS_ERR_ARG;
   ncclUniqueId id;
   std::memcpy(&id, id128, sizeof(id));
@@ -203,6 +205,7 @@ mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int
 
 mantis_status mantis_gn_allreduce(void* ctx, double* acc28) {
   Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
   if (!c || !acc28) return MANTIS_ERR_ARG;
   if (!c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
   if (!c->d_gn28 && dalloc(c, &c->d_gn28, 28) != MANTIS_OK) return MANTIS_ERR_OOM;

@@ -2,13 +2,14 @@
 //
 // Stage map (reference -> kernel):
 //   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_cls
-//   Canny hysteresis                 (OpenCV, [3P])                  k_uf_merge8 / k_hyst_flatten / k_hyst_edge
-//   dilate x2 / erode x1             QuadDetection.h:213-214         k_morph_h / k_morph_v
-//   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_grad_border + k_morph_*
-//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_cc_merge + k_border_emit + k_frame_contours
+//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_tile / _seam / _strong / _edge
+//   dilate x2 / erode x1             QuadDetection.h:213-214         k_bh / k_bv / k_pack_det (bit planes)
+//   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_bm0 + k_bh / k_bv
+//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_cc_tile / _seam / _flatten + k_border_emit
+//                                                                    + k_frame_contours
 //   approxPolyDP / Quadrilateral /
 //   removeDuplicateQuads / undistort QuadDetection.h:13-171, 219-228, 289-298   k_frame_contours
-//   CoPlanarPoseEstimator -> RPP     CoPlanarPoseEstimator.cpp:16-58 k_rpp
+//   CoPlanarPoseEstimator -> RPP     CoPlanarPoseEstimator.cpp:16-58 k_rpp_s1 / _s1b / _refine / _merge
 //   generateCentralHypotheses +
 //   PoseClusterer                    HypothesisGeneration.h:57-109, PoseClusterer.cpp:33-116  k_frame_hyps
 //   evaluate / PF / shifts / yaw /
@@ -40,9 +41,9 @@ __device__ inline int refl101(int i, int n) {
 
 // gray -> 3x3 Gaussian (x256 kernel [84,89,84], OpenCV <= 3.3) -> Sobel 3x3
 // (REPLICATE) -> L1 magnitude -> non-maximum suppression. cls: 0 none,
-// 1 weak candidate, 2 strong. lab: union-find init (p or -1).
+// 1 weak candidate, 2 strong.
 __global__ __launch_bounds__(256) void k_canny_cls(const FrameDesc* __restrict__ frames, uint8_t* __restrict__ cls,
-                                                   int32_t* __restrict__ lab, size_t plane, int low, int high) {
+                                                   size_t plane, int low, int high) {
   const int f = blockIdx.z;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
@@ -112,7 +113,6 @@ __global__ __launch_bounds__(256) void k_canny_cls(const FrameDesc* __restrict__
   const int SHIFT = 15;
   const int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
   uint8_t* cf = cls + (size_t)f * plane;
-  int32_t* lf = lab + (size_t)f * plane;
   for (int i = tid; i < TY * TX; i += 256) {
     int ly = i / TX, lx = i % TX;
     int x = x0 + lx, y = y0 + ly;
@@ -139,24 +139,29 @@ __global__ __launch_bounds__(256) void k_canny_cls(const FrameDesc* __restrict__
       }
       if (push) c = (m > high) ? 2 : 1;
     }
-    size_t p = (size_t)y * W + x;
-    cf[p] = c;
-    lf[p] = c ? (int32_t)p : -1;
+    cf[(size_t)y * W + x] = c;
   }
 }
 
 // ======================================================== union-find (CCL)
 // Concurrent union by index: roots are component minima, links point to
 // smaller indices only, so finds terminate and stale reads only cost retries.
-__device__ inline int uf_find(const int32_t* lab, int x) {
-  int p;
-  while ((p = lab[x]) != x) x = p;
-  return x;
-}
-__device__ inline void uf_union(int32_t* lab, int a, int b) {
+// Finds use path halving: only non-roots are rewritten (with an ancestor) and
+// roots change only through the CAS in uf_union_c, so this is race-safe.
+__device__ inline int uf_find_c(int32_t* lab, int x) {
   while (true) {
-    a = uf_find(lab, a);
-    b = uf_find(lab, b);
+    int p = lab[x];
+    if (p == x) return x;
+    int g = lab[p];
+    if (g == p) return p;
+    lab[x] = g;
+    x = g;
+  }
+}
+__device__ inline void uf_union_c(int32_t* lab, int a, int b) {
+  while (true) {
+    a = uf_find_c(lab, a);
+    b = uf_find_c(lab, b);
     if (a == b) return;
     if (a < b) { int t = a; a = b; b = t; }
     int old = atomicCAS(&lab[a], a, b);
@@ -164,42 +169,135 @@ __device__ inline void uf_union(int32_t* lab, int a, int b) {
     a = old;
   }
 }
+__device__ inline int lds_find(const int* L, int x) {
+  int p;
+  while ((p = L[x]) != x) x = p;
+  return x;
+}
+__device__ inline void lds_union(int* L, int a, int b) {
+  while (true) {
+    a = lds_find(L, a);
+    b = lds_find(L, b);
+    if (a == b) return;
+    if (a < b) { int t = a; a = b; b = t; }
+    int old = atomicCAS(&L[a], a, b);
+    if (old == a) return;
+    a = old;
+  }
+}
+constexpr int CW = 64, CH = 32;  // union-find tile
 
-// Canny hysteresis: 8-connected components of candidates (cls > 0)
-__global__ __launch_bounds__(256) void k_uf_merge8(const uint8_t* __restrict__ cls, int32_t* lab, int W, int H,
-                                                   size_t plane) {
-  const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
+// Canny hysteresis (cv::Canny's stack walk = 8-connected components of the
+// candidates that contain a strong pixel), two-level:
+//   k_hyst_tile  LDS union-find of candidates per 64x32 tile; each candidate
+//                gets its tile root's global index, each tile root its strong flag
+//   k_hyst_seam  unions across tile seams (global, path halving)
+//   k_hyst_strong  strong pixels mark their global root
+//   k_hyst_edge  edge = candidate whose global root is marked (bit plane)
+__global__ __launch_bounds__(256) void k_hyst_tile(const uint8_t* __restrict__ cls, int32_t* __restrict__ lab,
+                                                   uint8_t* __restrict__ strong, int W, int H, size_t plane) {
+  __shared__ uint8_t C[CH * CW];
+  __shared__ int L[CH * CW];
+  __shared__ uint8_t S[CH * CW];
+  const int f = blockIdx.z;
+  const int x0 = blockIdx.x * CW, y0 = blockIdx.y * CH;
   const uint8_t* c = cls + (size_t)f * plane;
   int32_t* l = lab + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
+  uint8_t* sg = strong + (size_t)f * plane;
+  const int t = threadIdx.x;
+  for (int i = t; i < CH * CW; i += 256) {
+    const int x = x0 + (i % CW), y = y0 + (i / CW);
+    C[i] = (x < W && y < H) ? c[(size_t)y * W + x] : 0;
+    S[i] = 0;
+  }
+  __syncthreads();
+  {
+    const int base = (t >> 3) * CW + (t & 7) * 8;
+    int run = base;
+    L[base] = base;
+    for (int k = 1; k < 8; k++) {
+      const int i = base + k;
+      if (!(C[i] && C[i - 1])) run = i;
+      L[i] = run;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < CH * CW; i += 256) {
+    if (!C[i]) continue;
+    const int lx = i % CW, ly = i / CW;
+    const bool left = lx > 0 && C[i - 1];
+    if ((lx & 7) == 0 && left) lds_union(L, i, i - 1);
+    if (ly == 0) continue;
+    const bool up = C[i - CW] != 0;
+    const bool upl = lx > 0 && C[i - CW - 1];
+    if (up) {
+      if (!(left && upl)) lds_union(L, i, i - CW);
+    } else {
+      if (upl && !left) lds_union(L, i, i - CW - 1);
+      if (lx + 1 < CW && C[i - CW + 1]) lds_union(L, i, i - CW + 1);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < CH * CW; i += 256) {
+    if (!C[i]) continue;
+    const int r = lds_find(L, i);
+    L[i] = r;
+    if (C[i] == 2) S[r] = 1;
+  }
+  __syncthreads();
+  for (int i = t; i < CH * CW; i += 256) {
+    if (!C[i]) continue;
+    const int r = L[i];
+    const int x = x0 + (i % CW), y = y0 + (i / CW);
+    const size_t p = (size_t)y * W + x;
+    l[p] = (y0 + r / CW) * W + x0 + (r % CW);
+    if (r == i) sg[p] = S[i];
+  }
+}
+// one thread per seam pixel: vertical seams (x = k*CW) then horizontal (y = k*CH)
+__global__ __launch_bounds__(256) void k_hyst_seam(const uint8_t* __restrict__ cls, int32_t* lab, int W, int H,
+                                                   size_t plane) {
+  const int f = blockIdx.y;
+  const uint8_t* c = cls + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  const int nvs = (W - 1) / CW, nhs = (H - 1) / CH;
+  const size_t nv = (size_t)nvs * H, n = nv + (size_t)nhs * W;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
+    int x, y;
+    const bool vert = k < nv;
+    if (vert) { x = (int)(k / H + 1) * CW; y = (int)(k % H); }
+    else { const size_t h = k - nv; y = (int)(h / W + 1) * CH; x = (int)(h % W); }
+    const int p = y * W + x;
     if (!c[p]) continue;
-    int x = (int)(p % W), y = (int)(p / W);
-    if (x > 0 && c[p - 1]) uf_union(l, (int)p, (int)p - 1);
-    if (y > 0) {
-      if (x > 0 && c[p - W - 1]) uf_union(l, (int)p, (int)(p - W - 1));
-      if (c[p - W]) uf_union(l, (int)p, (int)(p - W));
-      if (x + 1 < W && c[p - W + 1]) uf_union(l, (int)p, (int)(p - W + 1));
+    if (vert) {
+      if (c[p - 1]) uf_union_c(l, p, p - 1);
+      if (y > 0 && c[p - W - 1]) uf_union_c(l, p, p - W - 1);
+      if (y + 1 < H && c[p + W - 1]) uf_union_c(l, p, p + W - 1);
+    } else {
+      if (c[p - W]) uf_union_c(l, p, p - W);
+      if (x > 0 && c[p - W - 1]) uf_union_c(l, p, p - W - 1);
+      if (x + 1 < W && c[p - W + 1]) uf_union_c(l, p, p - W + 1);
     }
   }
 }
-__global__ __launch_bounds__(256) void k_hyst_flatten(const uint8_t* __restrict__ cls, int32_t* lab,
-                                                      uint8_t* __restrict__ strong, int W, int H, size_t plane) {
+__global__ __launch_bounds__(256) void k_hyst_strong(const uint8_t* __restrict__ cls, int32_t* lab,
+                                                     uint8_t* strong, int W, int H, size_t plane) {
   const int f = blockIdx.y;
   const size_t n = (size_t)W * H;
   const uint8_t* c = cls + (size_t)f * plane;
   int32_t* l = lab + (size_t)f * plane;
-  uint8_t* s = strong + (size_t)f * plane;
+  uint8_t* sg = strong + (size_t)f * plane;
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    if (!c[p]) continue;
-    int r = uf_find(l, (int)p);
-    l[p] = r;
-    if (c[p] == 2) s[r] = 1;
+    if (c[p] != 2) continue;
+    const int a = l[p];  // an ancestor (the tile root, or above it after halving)
+    const int r = uf_find_c(l, a);
+    if (r != (int)p) sg[r] = 1;  // tile roots already carry their own strong flag
   }
 }
+
 // edge = candidate whose component holds a strong pixel, written as a
 // bit plane (one 32-pixel word per work-item) and optionally as bytes
-__global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ cls, const int32_t* __restrict__ lab,
+__global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ cls, int32_t* lab,
                                                    const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
                                                    uint8_t* __restrict__ edge, int W, int H, size_t plane,
                                                    size_t bstride) {
@@ -213,7 +311,7 @@ __global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ c
     const size_t p0 = o + (size_t)y * W + 32 * w;
     uint32_t word = 0;
     for (int b = 0; b < xe; b++) {
-      const uint32_t e = (cls[p0 + b] && strong[o + lab[p0 + b]]) ? 1u : 0u;
+      const uint32_t e = (cls[p0 + b] && strong[o + uf_find_c(lab + o, lab[p0 + b])]) ? 1u : 0u;
       word |= e << b;
       if (edge) edge[p0 + b] = (uint8_t)e;
     }
@@ -304,50 +402,9 @@ __global__ __launch_bounds__(256) void k_pack_det(const uint32_t* __restrict__ s
 //              unions skipped), each pixel labelled with its tile-local root
 //   k_cc_seam  unions across tile seams only, global union-find
 //   k_cc_flatten  every pixel -> its global root
-constexpr int CW = 64, CH = 32;
-
-// find with path halving: only non-roots are rewritten (with an ancestor),
-// roots change only through the CAS in uf_union, so this is race-safe
-__device__ inline int uf_find_c(int32_t* lab, int x) {
-  while (true) {
-    int p = lab[x];
-    if (p == x) return x;
-    int g = lab[p];
-    if (g == p) return p;
-    lab[x] = g;
-    x = g;
-  }
-}
-__device__ inline void uf_union_c(int32_t* lab, int a, int b) {
-  while (true) {
-    a = uf_find_c(lab, a);
-    b = uf_find_c(lab, b);
-    if (a == b) return;
-    if (a < b) { int t = a; a = b; b = t; }
-    int old = atomicCAS(&lab[a], a, b);
-    if (old == a) return;
-    a = old;
-  }
-}
-__device__ inline int lds_find(const int* L, int x) {
-  int p;
-  while ((p = L[x]) != x) x = p;
-  return x;
-}
-__device__ inline void lds_union(int* L, int a, int b) {
-  while (true) {
-    a = lds_find(L, a);
-    b = lds_find(L, b);
-    if (a == b) return;
-    if (a < b) { int t = a; a = b; b = t; }
-    int old = atomicCAS(&L[a], a, b);
-    if (old == a) return;
-    a = old;
-  }
-}
-
 __global__ __launch_bounds__(256) void k_cc_tile(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                 int32_t* __restrict__ lab, int Wp, int Hp, size_t plane) {
+                                                 int32_t* __restrict__ lab, CcCand* __restrict__ cand,
+                                                 FrameState* st, int Wp, int Hp, size_t plane) {
   __shared__ uint8_t C[CH * CW];  // 0 background, 1 foreground, 2 outside the image
   __shared__ int L[CH * CW];
   const int f = blockIdx.z;
@@ -393,11 +450,31 @@ __global__ __launch_bounds__(256) void k_cc_tile(const uint32_t* __restrict__ db
     }
   }
   __syncthreads();
+  // labels only where later kernels look: tile-boundary pixels (seam unions,
+  // hole parents left of a tile) and the tile roots themselves
   for (int i = t; i < CH * CW; i += 256) {
     if (C[i] == 2) continue;
+    const int lx = i % CW, ly = i / CW;
     const int r = lds_find(L, i);
-    const int x = x0 + (i % CW), y = y0 + (i / CW);
-    l[(size_t)y * Wp + x] = (y0 + r / CW) * Wp + x0 + (r % CW);
+    const int x = x0 + lx, y = y0 + ly;
+    const int gp = y * Wp + x;
+    const int gr = (y0 + r / CW) * Wp + x0 + (r % CW);
+    const bool edge = lx == 0 || ly == 0 || lx == CW - 1 || ly == CH - 1 || x == Wp - 1 || y == Hp - 1;
+    if (edge || r == i) l[gp] = gr;
+    if (r == i) {
+      int hint = -1;
+      if (C[i] == 0 && x > 0) {
+        if (lx > 0) {
+          const int rl = lds_find(L, i - 1);
+          hint = (y0 + rl / CW) * Wp + x0 + (rl % CW);
+        } else {
+          hint = gp - 1;  // right column of the left tile: labelled
+        }
+      }
+      const int k = atomicAdd(&st[f].n_cand, 1);
+      if (k < kMaxCand) cand[(size_t)f * kMaxCand + k] = CcCand{gp, hint};
+      else atomicOr(&st[f].overflow, 1);
+    }
   }
 }
 
@@ -432,30 +509,28 @@ __global__ __launch_bounds__(256) void k_cc_seam(const uint32_t* __restrict__ db
     }
   }
 }
-__global__ __launch_bounds__(256) void k_cc_flatten(int32_t* lab, size_t n, size_t plane) {
-  const int f = blockIdx.y;
-  int32_t* l = lab + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x)
-    l[p] = uf_find_c(l, l[p]);
-}
 // One border per fg component (outer, at its root) and per enclosed bg
-// component (hole, left of its root).
+// component (hole, left of its root); the root of a component is the tile
+// root that stayed a root through the seam unions.
 __global__ __launch_bounds__(256) void k_border_emit(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                     const int32_t* __restrict__ lab, Border* __restrict__ borders,
-                                                     FrameState* st, int Wp, int Hp, size_t plane, int cap) {
+                                                     int32_t* lab, const CcCand* __restrict__ cand,
+                                                     Border* __restrict__ borders, FrameState* st, int Wp,
+                                                     size_t plane, int cap) {
   const int f = blockIdx.y;
-  const size_t n = (size_t)Wp * Hp;
+  const int nc = min(st[f].n_cand, kMaxCand);
   const uint32_t* B = dbits + (size_t)f * dstride;
   const int wpw = dbits_wpw(Wp);
-  const int32_t* l = lab + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    if (l[p] != (int32_t)p) continue;
+  int32_t* l = lab + (size_t)f * plane;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
+    const CcCand cd = cand[(size_t)f * kMaxCand + k];
+    const int p = cd.root;
+    if (l[p] != p) continue;
     Border b;
-    if (dbit(B, wpw, (int)(p % Wp), (int)(p / Wp))) {
-      b.key = (int32_t)p; b.start = (int32_t)p; b.hole = 0; b.parent = (int32_t)p;
+    if (dbit(B, wpw, p % Wp, p / Wp)) {
+      b.key = p; b.start = p; b.hole = 0; b.parent = p;
     } else {
       if (p == 0) continue;
-      b.key = (int32_t)p; b.start = (int32_t)p - 1; b.hole = 1; b.parent = l[p - 1];
+      b.key = p; b.start = p - 1; b.hole = 1; b.parent = uf_find_c(l, cd.hint);
     }
     int idx = atomicAdd(&st[f].n_borders, 1);
     if (idx < cap) borders[(size_t)f * cap + idx] = b;

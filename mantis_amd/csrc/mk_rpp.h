@@ -461,14 +461,31 @@ MK_HD void jacobi_svd(double (&At)[N * M], double (&Wout)[N], double* Vt) {
         for (int k = 0; k < M; k++) p += At[i * M + k] * At[j * M + k];
         if (fabs(p) <= eps * sqrt(a * b)) continue;
         p *= 2;
-        double beta = a - b, gamma = hypot(p, beta), c, s;
-        if (beta < 0) {
-          double delta = (gamma - beta) * 0.5;
-          s = sqrt(delta / gamma);
-          c = p / (gamma * s * 2);
+        double beta = a - b, gamma, c, s;
+        if (fabs(p) <= fabs(beta) * 0x1p-60) {
+          // hypot(p, beta) == |beta| exactly here (|p| is below half an ulp of
+          // |beta|), so the reference's sqrt of (2|beta| / 2|beta|) is exactly 1
+          // and one division is left. This is the common case once a row has
+          // decayed to rounding noise: a planar model makes M rank 2, and the
+          // reference keeps rotating that row until it underflows (~20 sweeps).
+          gamma = fabs(beta);
+          if (beta < 0) {
+            s = 1.0;
+            c = p / (gamma * s * 2);
+          } else {
+            c = 1.0;
+            s = p / (gamma * c * 2);
+          }
         } else {
-          c = sqrt((gamma + beta) / (gamma * 2));
-          s = p / (gamma * c * 2);
+          gamma = hypot(p, beta);
+          if (beta < 0) {
+            double delta = (gamma - beta) * 0.5;
+            s = sqrt(delta / gamma);
+            c = p / (gamma * s * 2);
+          } else {
+            c = sqrt((gamma + beta) / (gamma * 2));
+            s = p / (gamma * c * 2);
+          }
         }
         a = b = 0;
 #pragma unroll

@@ -85,6 +85,11 @@ struct FrameDebug {
 };
 
 // Per-frame counters / status written by the kernels.
+struct CcCand {  // a tile-local component root and, for background, where its parent is found
+  int32_t root, hint;
+};
+constexpr int kMaxCand = 65536;
+
 struct FrameState {
   int32_t n_borders;
   int32_t n_points;
@@ -95,7 +100,8 @@ struct FrameState {
   int32_t reaches_pf;
   int32_t gauss_offset;  // index into the gaussian stream (floats)
   int32_t overflow;      // bit 0 borders, 1 points, 2 quads, 3 hyps
-  int32_t ticks[7];      // k_frame_contours phase ends, 10 ns wall-clock ticks from its start
+  int32_t n_cand;        // component-root candidates (tile roots) of the contour CCL
+  int32_t ticks[6];      // k_frame_contours phase ends, 10 ns wall-clock ticks from its start
 };
 
 }  // namespace mk
