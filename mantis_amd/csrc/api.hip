@@ -584,10 +584,15 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   // the contour kernel keeps the padded frame as a bitmap in LDS when it fits
   int max_lds = 0;
   (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device);
-  const int static_lds = 28 * 1024;
+  hipFuncAttributes fa{};
+  int static_lds = 32 * 1024;
+  if (hipFuncGetAttributes(&fa, (const void*)k_frame_contours) == hipSuccess) static_lds = (int)fa.sharedSizeBytes;
   c->lds_bytes = std::max(0, std::min(max_lds, 160 * 1024) - static_lds);
-  if (c->lds_bytes > 0)
-    (void)hipFuncSetAttribute((const void*)k_frame_contours, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes);
+  if (c->lds_bytes > 0 &&
+      hipFuncSetAttribute((const void*)k_frame_contours, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) !=
+          hipSuccess)
+    c->lds_bytes = 0;  // contour tracing then reads the bit plane from global memory
+  (void)hipGetLastError();
   if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess) {
     g_create_err = "hipMemset failed";
     mantis_destroy(c);

@@ -552,18 +552,125 @@ struct BitsNB {
   __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
 
-__device__ void contour_pass(const BitsNB& nb, int Wp, const Border* bs, int nb_count, int32_t* counts, int32_t* offs,
-                             int32_t* pool, int pool_cap, int pass) {
-  for (int i = threadIdx.x; i < nb_count; i += blockDim.x) {
-    const Border b = bs[i];
-    const int sx = b.start % Wp, sy = b.start / Wp;
-    if (pass == 0) {
-      counts[i] = trace_border_nb(nb, sx, sy, b.hole != 0, nullptr, 0);
+// Single-pass border tracing: points go to 64-point chunks handed out by an
+// LDS bump allocator; a wave per chunk then compacts them by border.
+constexpr int kChunk = 64;
+struct ChunkEmit {
+  int32_t* chunks;  // [chunk][64][2]
+  int32_t* owner;   // border of each chunk
+  int32_t* ordv;    // ordinal of the chunk within its border
+  int32_t* counter; // LDS
+  int max_chunks, border, cur, k, nch;
+  bool ovf;
+  __device__ void operator()(int px, int py) {
+    if (cur < 0 || k == kChunk) {
+      if (ovf) return;
+      const int c = atomicAdd(counter, 1);
+      if (c >= max_chunks) { ovf = true; return; }
+      cur = c;
+      k = 0;
+      owner[c] = border;
+      ordv[c] = nch++;
+    }
+    int32_t* d = chunks + 2 * ((size_t)cur * kChunk + k);
+    d[0] = px;
+    d[1] = py;
+    k++;
+  }
+};
+
+// max over the wave of (d, idx) with ties to the smaller idx (the first
+// strict maximum of a sequential scan in idx order)
+__device__ inline void wave_argmax(double& d, int& idx) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double d2 = __shfl_xor(d, o);
+    const int i2 = __shfl_xor(idx, o);
+    if (d2 > d || (d2 == d && i2 < idx)) { d = d2; idx = i2; }
+  }
+}
+
+// approx_poly (mk_contour.h, closed, quad early exit) executed by one wave:
+// the farthest-point scans are lane-parallel reductions; lane 0 owns the DP
+// stack and the output (single-lane memory order), control is wave-uniform.
+__device__ int approx_poly_wave(const int32_t* __restrict__ src, int count, double eps, int32_t* dst, int32_t* stk,
+                                int max_dp) {
+  const int lane = threadIdx.x & 63;
+  if (count == 0) return 0;
+  eps *= eps;
+  int top = 0, nc = 0, rs_s = 0, pos = 0;
+  bool le_eps = false;
+  int spx = 0, spy = 0;
+  for (int it = 0; it < 3; it++) {
+    pos = (pos + rs_s) % count;
+    spx = src[2 * pos];
+    spy = src[2 * pos + 1];
+    double best = 0;
+    int bj = 0x7fffffff;
+    for (int j = 1 + lane; j < count; j += 64) {
+      int q = pos + j;
+      if (q >= count) q -= count;
+      const double dx = src[2 * q] - spx, dy = src[2 * q + 1] - spy;
+      const double d = dx * dx + dy * dy;
+      if (d > best) { best = d; bj = j; }
+    }
+    wave_argmax(best, bj);
+    if (best > 0) rs_s = bj;
+    le_eps = best <= eps;
+  }
+  if (!le_eps) {
+    const int sl_s = pos % count, sl_e = (rs_s + sl_s) % count;
+    if (lane == 0) {
+      stk[0] = sl_e; stk[1] = sl_s;  // PUSH(rs_s, rs_e)
+      stk[2] = sl_s; stk[3] = sl_e;  // PUSH(sl_s, sl_e)
+    }
+    top = 2;
+  } else {
+    if (lane == 0) { dst[0] = spx; dst[1] = spy; }
+    nc = 1;
+  }
+  while (top > 0) {
+    top--;
+    int a0 = 0, a1 = 0;
+    if (lane == 0) { a0 = stk[2 * top]; a1 = stk[2 * top + 1]; }
+    const int sl_s = __shfl(a0, 0), sl_e = __shfl(a1, 0);
+    const int epx = src[2 * sl_e], epy = src[2 * sl_e + 1];
+    int p0 = sl_s + 1;
+    if (p0 >= count) p0 = 0;
+    spx = src[2 * sl_s];
+    spy = src[2 * sl_s + 1];
+    if (p0 != sl_e) {
+      const double dx = epx - spx, dy = epy - spy;
+      int L = sl_e - p0;
+      if (L < 0) L += count;
+      double best = 0;
+      int bt = 0x7fffffff;
+      for (int t = lane; t < L; t += 64) {
+        int q = p0 + t;
+        if (q >= count) q -= count;
+        const double dist = fabs((src[2 * q + 1] - spy) * dx - (src[2 * q] - spx) * dy);
+        if (dist > best) { best = dist; bt = t; }
+      }
+      wave_argmax(best, bt);
+      if (best > 0) rs_s = (p0 + bt) % count;
+      le_eps = best * best <= eps * (dx * dx + dy * dy);
     } else {
-      const int o = offs[i], c = counts[i];
-      if (o + c <= pool_cap) trace_border_nb(nb, sx, sy, b.hole != 0, pool + 2 * (size_t)o, c);
+      le_eps = true;
+    }
+    if (le_eps) {
+      if (lane == 0) { dst[2 * nc] = spx; dst[2 * nc + 1] = spy; }
+      nc++;
+      if (max_dp > 0 && nc >= max_dp) return max_dp + 1;
+    } else {
+      if (lane == 0) {
+        stk[2 * top] = rs_s; stk[2 * top + 1] = sl_e;      // PUSH(rs_s, rs_e = sl_e)
+        stk[2 * top + 2] = sl_s; stk[2 * top + 3] = rs_s;  // PUSH(sl_s, sl_e = rs_s)
+      }
+      top += 2;
     }
   }
+  int r = 0;
+  if (lane == 0) r = approx_cleanup(dst, nc, eps, true);
+  return __shfl(r, 0);
 }
 
 // CCOMP output order (OpenCV tree pre-order): outers by key descending, each
@@ -573,6 +680,9 @@ __device__ inline bool ccomp_before(int pa, int ha, int ka, int pb, int hb, int 
   if (ha != hb) return ha < hb;
   return ka > kb;
 }
+
+constexpr int kLongBorder = 128;  // points; longer borders get a whole wave for approxPolyDP
+constexpr int kMaxLong = 512;
 
 struct RawQuad {
   int32_t c[8];
@@ -598,6 +708,8 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   __shared__ int32_t ord[kMaxQuads];
   __shared__ float qcx[kMaxQuads], qcy[kMaxQuads];
   __shared__ double qside[kMaxQuads];
+  __shared__ int32_t nchunk, nlong;
+  __shared__ int32_t longs[kMaxLong];
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
   const uint32_t* B = dbits + (size_t)f * dstride;
@@ -609,6 +721,17 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
+  auto emit_raw = [&](int i, const int32_t* q4) {
+    const int q = atomicAdd(&nraw, 1);
+    if (q < kMaxQuads) {
+      for (int k = 0; k < 8; k++) raw[q].c[k] = q4[k];
+      raw[q].parent = bs[i].parent;
+      raw[q].hole = bs[i].hole;
+      raw[q].key = bs[i].key;
+    } else {
+      atomicOr(&st[f].overflow, 4);
+    }
+  };
   const uint64_t t0 = wall_clock64();
 #define MK_TICK(k) \
   if (tid == 0) st[f].ticks[k] = (int32_t)(wall_clock64() - t0);
@@ -617,13 +740,23 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
     for (size_t w = tid; w < nwords; w += blockDim.x) lds_bits[w] = B[w];
   }
   const BitsNB nbh{use_lds ? (const uint32_t*)lds_bits : B, wpw};
-  if (tid == 0) { nraw = 0; total = 0; }
+  if (tid == 0) { nraw = 0; total = 0; nchunk = 0; nlong = 0; }
   __syncthreads();
   MK_TICK(0);
-  contour_pass(nbh, Wp, bs, nb, cnt, off, pl, pool_cap, 0);
+  // 1. follow every border once, points into chunks
+  const int max_chunks = pool_cap / kChunk;
+  int32_t* chunks = sc;                              // [0, 2 pool_cap)
+  int32_t* owner = sc + 2 * (size_t)pool_cap;        // [2 pool_cap, + max_chunks)
+  int32_t* ordv = owner + max_chunks;
+  for (int i = tid; i < nb; i += blockDim.x) {
+    const Border b = bs[i];
+    ChunkEmit em{chunks, owner, ordv, &nchunk, max_chunks, i, -1, 0, 0, false};
+    cnt[i] = trace_border_nb_em(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em);
+    if (em.ovf) atomicOr(&st[f].overflow, 2);
+  }
   __syncthreads();
   MK_TICK(1);
-  // exclusive scan of the point counts, blockDim at a time
+  // 2. exclusive scan of the point counts, blockDim at a time
   for (int base = 0; base < nb; base += blockDim.x) {
     int i = base + tid;
     int v = i < nb ? cnt[i] : 0;
@@ -640,7 +773,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
     if (tid == blockDim.x - 1) total += scan[tid];
     __syncthreads();
   }
-  if (total > pool_cap) {
+  if (total > pool_cap || nchunk > max_chunks) {
     if (tid == 0) {
       atomicOr(&st[f].overflow, 2);
       st[f].n_points = total;
@@ -650,25 +783,44 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
     return;
   }
   MK_TICK(2);
-  contour_pass(nbh, Wp, bs, nb, cnt, off, pl, pool_cap, 1);
+  // 3. compact: one wave per chunk, one lane per point
+  {
+    const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
+    for (int c = wave; c < nchunk; c += nwaves) {
+      const int b = owner[c], k = ordv[c] * kChunk + lane;
+      if (k < cnt[b]) {
+        const int32_t* sp = chunks + 2 * ((size_t)c * kChunk + lane);
+        int32_t* dp = pl + 2 * ((size_t)off[b] + k);
+        dp[0] = sp[0];
+        dp[1] = sp[1];
+      }
+    }
+  }
   __syncthreads();
   MK_TICK(3);
-  // approxPolyDP per border (eps = POLYGON_EPSILON, closed); keep 4-vertex results
+  // 4. approxPolyDP per border (eps = POLYGON_EPSILON, closed, quad early
+  // exit); long borders are deferred to whole waves
   for (int i = tid; i < nb; i += blockDim.x) {
-    int o = off[i], c = cnt[i];
+    const int o = off[i], c = cnt[i];
+    if (c > kLongBorder) {
+      const int k = atomicAdd(&nlong, 1);
+      if (k < kMaxLong) { longs[k] = i; continue; }
+    }
     int32_t* dst = sc + 4 * (size_t)o;
     int32_t* stk = dst + 2 * (size_t)c;
     int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
-    if (m == 4) {
-      int q = atomicAdd(&nraw, 1);
-      if (q < kMaxQuads) {
-        for (int k = 0; k < 8; k++) raw[q].c[k] = dst[k];
-        raw[q].parent = bs[i].parent;
-        raw[q].hole = bs[i].hole;
-        raw[q].key = bs[i].key;
-      } else {
-        atomicOr(&st[f].overflow, 4);
-      }
+    if (m == 4) emit_raw(i, dst);
+  }
+  __syncthreads();
+  {
+    const int wave = tid >> 6, nwaves = blockDim.x >> 6;
+    const int nl = nlong < kMaxLong ? nlong : kMaxLong;
+    for (int k = wave; k < nl; k += nwaves) {
+      const int i = longs[k], o = off[i], c = cnt[i];
+      int32_t* dst = sc + 4 * (size_t)o;
+      int32_t* stk = dst + 2 * (size_t)c;
+      const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
+      if (m == 4 && (tid & 63) == 0) emit_raw(i, dst);
     }
   }
   __syncthreads();

@@ -86,8 +86,10 @@ MK_HD int ctz32(uint32_t v) {
   return k;
 #endif
 }
-template <class NB>
-MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out, int cap) {
+// em(px, py) receives each CHAIN_APPROX_SIMPLE point in order (image
+// coordinates); returns the point count.
+template <class NB, class EM>
+MK_HD int trace_border_nb_em(const NB& nb, int sx, int sy, bool hole, EM& em) {
   int x = sx, y = sy;
   uint32_t m = nb(x, y);
   const int s_end0 = hole ? 0 : 4;
@@ -97,7 +99,7 @@ MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out,
   } while (!((m >> s) & 1u) && s != s_end0);
   int px = sx - 1, py = sy - 1;
   if (s == s_end0) {
-    if (out && cap > 0) { out[0] = px; out[1] = py; }
+    em(px, py);
     return 1;
   }
   const int x1 = sx + code_dx(s), y1 = sy + code_dy(s);  // i1
@@ -109,7 +111,7 @@ MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out,
     const uint32_t r = ((m | (m << 8)) >> (s + 1)) & 0xffu;
     s = (s + 1 + ctz32(r)) & 7;
     if (s != prev_s) {
-      if (out && n < cap) { out[2 * n] = px; out[2 * n + 1] = py; }
+      em(px, py);
       n++;
       prev_s = s;
     }
@@ -124,6 +126,62 @@ MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out,
     s = (s + 4) & 7;
   }
   return n;
+}
+struct ArrayEmit {
+  int32_t* out;
+  int cap, n;
+  MK_HD void operator()(int px, int py) {
+    if (out && n < cap) { out[2 * n] = px; out[2 * n + 1] = py; }
+    n++;
+  }
+};
+template <class NB>
+MK_HD int trace_border_nb(const NB& nb, int sx, int sy, bool hole, int32_t* out, int cap) {
+  ArrayEmit em{out, cap, 0};
+  return trace_border_nb_em(nb, sx, sy, hole, em);
+}
+
+// approxPolyDP's final clean-up of [almost] straight runs on the n_dp
+// Douglas–Peucker points in dst (eps = squared epsilon); returns the count.
+MK_HD int approx_cleanup(int32_t* dst, int new_count, double eps, bool closed0) {
+  bool is_closed = closed0;
+  int count = new_count;
+  int pos, wpos, spx, spy, ptx, pty, epx, epy;
+#define MK_READD(X, Y, P)           \
+  do {                              \
+    X = dst[2 * (P)];               \
+    Y = dst[2 * (P) + 1];           \
+    if (++(P) >= count) (P) = 0;    \
+  } while (0)
+  pos = is_closed ? count - 1 : 0;
+  MK_READD(spx, spy, pos);
+  wpos = pos;
+  MK_READD(ptx, pty, pos);
+  for (int i = !is_closed; i < count - !is_closed && new_count > 2; i++) {
+    double dx, dy, dist, succ;
+    MK_READD(epx, epy, pos);
+    dx = epx - spx;
+    dy = epy - spy;
+    dist = fabs((ptx - spx) * dy - (pty - spy) * dx);
+    succ = (ptx - spx) * (epx - ptx) + (pty - spy) * (epy - pty);
+    if (dist * dist <= 0.5 * eps * (dx * dx + dy * dy) && dx != 0 && dy != 0 && succ >= 0) {
+      new_count--;
+      dst[2 * wpos] = spx = epx;
+      dst[2 * wpos + 1] = spy = epy;
+      if (++wpos >= count) wpos = 0;
+      MK_READD(ptx, pty, pos);
+      i++;
+      continue;
+    }
+    dst[2 * wpos] = spx = ptx;
+    dst[2 * wpos + 1] = spy = pty;
+    if (++wpos >= count) wpos = 0;
+    ptx = epx;
+    pty = epy;
+  }
+  if (!is_closed) { dst[2 * wpos] = ptx; dst[2 * wpos + 1] = pty; }
+#undef MK_READD
+  return new_count;
 }
 
 // cv::approxPolyDP (approxPolyDP_<int>, closed or open) on n points `src`
@@ -232,44 +290,7 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
   if (!is_closed) { dst[2 * new_count] = src[2 * (count - 1)]; dst[2 * new_count + 1] = src[2 * (count - 1) + 1]; new_count++; }
 #undef MK_READ
 #undef MK_PUSH
-  // final clean-up of [almost] straight runs
-  is_closed = closed0;
-  count = new_count;
-#define MK_READD(X, Y, P)           \
-  do {                              \
-    X = dst[2 * (P)];               \
-    Y = dst[2 * (P) + 1];           \
-    if (++(P) >= count) (P) = 0;    \
-  } while (0)
-  pos = is_closed ? count - 1 : 0;
-  MK_READD(spx, spy, pos);
-  wpos = pos;
-  MK_READD(ptx, pty, pos);
-  for (i = !is_closed; i < count - !is_closed && new_count > 2; i++) {
-    double dx, dy, dist, succ;
-    MK_READD(epx, epy, pos);
-    dx = epx - spx;
-    dy = epy - spy;
-    dist = fabs((ptx - spx) * dy - (pty - spy) * dx);
-    succ = (ptx - spx) * (epx - ptx) + (pty - spy) * (epy - pty);
-    if (dist * dist <= 0.5 * eps * (dx * dx + dy * dy) && dx != 0 && dy != 0 && succ >= 0) {
-      new_count--;
-      dst[2 * wpos] = spx = epx;
-      dst[2 * wpos + 1] = spy = epy;
-      if (++wpos >= count) wpos = 0;
-      MK_READD(ptx, pty, pos);
-      i++;
-      continue;
-    }
-    dst[2 * wpos] = spx = ptx;
-    dst[2 * wpos + 1] = spy = pty;
-    if (++wpos >= count) wpos = 0;
-    ptx = epx;
-    pty = epy;
-  }
-  if (!is_closed) { dst[2 * wpos] = ptx; dst[2 * wpos + 1] = pty; }
-#undef MK_READD
-  return new_count;
+  return approx_cleanup(dst, new_count, eps, closed0);
 }
 
 }  // namespace mk
