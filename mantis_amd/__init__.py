@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmantis_amd.so")
+LIB_PATH = os.environ.get("MANTIS_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                             "libmantis_amd.so")
 
 MANTIS_OK = 0
 REASONS = {0: "published", 1: "no_quads", 2: "no_hyps", 3: "yaw_ambiguous", 4: "no_yaw"}

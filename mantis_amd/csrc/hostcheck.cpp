@@ -27,6 +27,21 @@ int hc_rpp(const double* model, const double* iprts, double* R, double* t, doubl
   return r.status;
 }
 
+// iteration counts of the phases: it[0] first ObjPose, it[1..5] candidate ObjPoses (-1 if absent)
+void hc_rpp_iters(const double* model, const double* iprts, int32_t* it) {
+  mk::rpp::Stage1 s;
+  mk::rpp::stage1(model, iprts, s);
+  it[0] = s.iterations;
+  for (int j = 0; j < mk::rpp::kCand; j++) {
+    it[1 + j] = -1;
+    if (s.error != 1 && ((s.keep_mask >> j) & 1)) {
+      mk::rpp::Refine r;
+      mk::rpp::refine(model, s.Q, s.sR[j], r);
+      it[1 + j] = r.iterations;
+    }
+  }
+}
+
 int hc_rpoly(const double* op, int deg, double* zr, double* zi) { return mk::rpp::rpoly(op, deg, zr, zi); }
 
 void hc_sort_desc(const double* err, int n, int* perm) {

@@ -494,15 +494,27 @@ __global__ __launch_bounds__(256) void k_cc_seam(const uint32_t* __restrict__ db
     else { const size_t h = k - nv; y = (int)(h / Wp + 1) * CH; x = (int)(h % Wp); }
     const int p = y * Wp + x;
     const uint32_t c = dbit(B, wpw, x, y);
+    // A 4-neighbour pair across the seam whose predecessor along the seam
+    // was the same kind of pair between the same two sets is implied: skip.
+    // Foreground diagonals are only needed when the 4-neighbour across the
+    // seam is background (otherwise they join through it).
     if (vert) {
-      if (dbit(B, wpw, x - 1, y) == c) uf_union_c(l, p, p - 1);
-      if (c) {
+      const uint32_t cl = dbit(B, wpw, x - 1, y);
+      if (cl == c) {
+        const bool implied = y > 0 && dbit(B, wpw, x, y - 1) == c && dbit(B, wpw, x - 1, y - 1) == c &&
+                             l[p] == l[p - Wp] && l[p - 1] == l[p - 1 - Wp];
+        if (!implied) uf_union_c(l, p, p - 1);
+      } else if (c) {
         if (y > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
         if (y + 1 < Hp && dbit(B, wpw, x - 1, y + 1)) uf_union_c(l, p, p + Wp - 1);
       }
     } else {
-      if (dbit(B, wpw, x, y - 1) == c) uf_union_c(l, p, p - Wp);
-      if (c) {
+      const uint32_t cu = dbit(B, wpw, x, y - 1);
+      if (cu == c) {
+        const bool implied = x > 0 && dbit(B, wpw, x - 1, y) == c && dbit(B, wpw, x - 1, y - 1) == c &&
+                             l[p] == l[p - 1] && l[p - Wp] == l[p - Wp - 1];
+        if (!implied) uf_union_c(l, p, p - Wp);
+      } else if (c) {
         if (x > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
         if (x + 1 < Wp && dbit(B, wpw, x + 1, y - 1)) uf_union_c(l, p, p - Wp + 1);
       }

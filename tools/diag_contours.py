@@ -34,10 +34,10 @@ m.set_profiling(True)
 m.process(imgs, rigs=rigs)
 print("stages", [(k, round(v, 3)) for k, v in m.kernel_times()], flush=True)
 C = np.array([m.frame_counters(i) for i in range(n)])
-names = ["borders", "points", "raw_q", "quads", "gen", "hyps", "pf", "goff", "ovf"]
+names = ["borders", "points", "raw_q", "quads", "gen", "hyps", "pf", "goff", "ovf", "cand"]
 for j, nm in enumerate(names):
     print(f"{nm:8s} mean {C[:, j].mean():10.1f} max {C[:, j].max()}")
-T = C[:, 9:16].astype(float) * 0.01  # us
+T = C[:, 10:16].astype(float) * 0.01  # us
 ph = ["bitmap", "trace0", "scan", "trace1", "approx", "rest"]
 prev = np.zeros(n)
 for j, nm in enumerate(ph):
