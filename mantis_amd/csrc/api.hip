@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <sstream>
@@ -130,6 +131,9 @@ struct Ctx {
   RppOut* d_rpp = nullptr;
   RppItem* d_items = nullptr;
   rpp::Refine* d_refine = nullptr;
+  int32_t *d_jobs0 = nullptr, *d_jobs1 = nullptr;  // RPP ObjPose job queues
+  RppQueue* d_rq = nullptr;
+  int rpp_blocks = 0;  // persistent-lane grid cap for k_objpose_q (0 = auto)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   FrameDebug* d_dbg = nullptr;
@@ -292,13 +296,28 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   return MANTIS_OK;
 }
 
+// Grid of a persistent ObjPose launch: enough lanes for ~2 jobs each at the
+// typical ~150 items per frame, at most rpp_blocks (MANTIS_RPP_BLOCKS) blocks.
+unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
+  size_t b = (expected_jobs + 511) / 512;
+  const size_t cap = c->rpp_blocks > 0 ? (size_t)c->rpp_blocks : 1024;
+  return (unsigned)std::max<size_t>(1, std::min(b, cap));
+}
+
+void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
+                       RppOut* out, size_t ni, size_t expected_items) {
+  k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q);
+  k_rpp_s1b<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, jobs1, q);
+  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q);
+  k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out);
+}
+
 mantis_status run_pose(Ctx* c, int n) {
+  HIP_OK(hipMemsetAsync(c->d_rq, 0, sizeof(RppQueue), c->s));
   dim3 gr((kMaxQuads * 2 + 255) / 256, n);
-  k_rpp_s1<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_items, c->cfg.grid_spacing / 2);
+  k_rpp_prep<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_items, c->d_jobs0, c->d_rq, c->cfg.grid_spacing / 2);
   const size_t ni = (size_t)n * kMaxQuads * 2;
-  k_rpp_s1b<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(c->d_items, ni);
-  k_rpp_refine<<<(unsigned)((ni * rpp::kCand + 255) / 256), 256, 0, c->s>>>(c->d_items, ni, c->d_refine);
-  k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(c->d_items, ni, c->d_refine, c->d_rpp);
+  launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, ni, (size_t)n * 160);
   mark(c, "rpp");
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
@@ -563,6 +582,9 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_rpp, (size_t)F * kMaxQuads * 2));
   chk(dalloc(c, &c->d_items, (size_t)F * kMaxQuads * 2));
   chk(dalloc(c, &c->d_refine, (size_t)F * kMaxQuads * 2 * rpp::kCand));
+  chk(dalloc(c, &c->d_jobs0, (size_t)F * kMaxQuads * 2));
+  chk(dalloc(c, &c->d_jobs1, (size_t)F * kMaxQuads * 2 * rpp::kCand));
+  chk(dalloc(c, &c->d_rq, 1));
   chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_st, (size_t)F));
@@ -588,6 +610,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   int static_lds = 32 * 1024;
   if (hipFuncGetAttributes(&fa, (const void*)k_frame_contours) == hipSuccess) static_lds = (int)fa.sharedSizeBytes;
   c->lds_bytes = std::max(0, std::min(max_lds, 160 * 1024) - static_lds);
+  if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
   if (c->lds_bytes > 0 &&
       hipFuncSetAttribute((const void*)k_frame_contours, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) !=
           hipSuccess)
@@ -609,7 +632,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
-                   c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine,
+                   c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
@@ -842,15 +865,17 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
   RppItem* d_it;
   rpp::Refine* d_rf;
   RppOut* d_out;
+  int32_t *d_j0, *d_j1;
+  RppQueue* d_q;
   if (dalloc(c, &d_ip, (size_t)8 * n) || dalloc(c, &d_op, (size_t)12 * n) || dalloc(c, &d_it, (size_t)n) ||
-      dalloc(c, &d_rf, (size_t)n * rpp::kCand) || dalloc(c, &d_out, (size_t)n))
+      dalloc(c, &d_rf, (size_t)n * rpp::kCand) || dalloc(c, &d_out, (size_t)n) || dalloc(c, &d_j0, (size_t)n) ||
+      dalloc(c, &d_j1, (size_t)n * rpp::kCand) || dalloc(c, &d_q, 1))
     return MANTIS_ERR_OOM;
   HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 8 * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
-  k_rpp_s1_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it);
-  k_rpp_s1b<<<(n + 255) / 256, 256, 0, c->s>>>(d_it, n);
-  k_rpp_refine<<<(unsigned)(((size_t)n * rpp::kCand + 255) / 256), 256, 0, c->s>>>(d_it, n, d_rf);
-  k_rpp_merge<<<(n + 255) / 256, 256, 0, c->s>>>(d_it, n, d_rf, d_out);
+  HIP_OK(hipMemsetAsync(d_q, 0, sizeof(RppQueue), c->s));
+  k_rpp_prep_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it, d_j0, d_q);
+  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, (size_t)n, (size_t)n);
   HIP_OK(hipGetLastError());
   std::vector<RppOut> h(n);
   HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));
@@ -862,7 +887,7 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
     errs[2 * i + 1] = h[i].img_err;
     rpp_status[i] = h[i].error == 1 ? -1 : h[i].status;
   }
-  void* ps[] = {d_ip, d_op, d_it, d_rf, d_out};
+  void* ps[] = {d_ip, d_op, d_it, d_rf, d_out, d_j0, d_j1, d_q};
   for (void* p : ps) (void)hipFree(p);
   return MANTIS_OK;
 }

@@ -929,91 +929,183 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
 }
 
 // ================================================================ RPP
-// Three phases (mk_rpp.h): stage1 per (frame, quad, orientation) — the first
-// ObjPose and the 2nd-pose candidates; refine per (item, candidate); merge per
-// item. Items are independent; the split keeps every phase's live state in
-// registers and runs the candidate ObjPoses in parallel.
+// Phases (mk_rpp.h): first ObjPose per (frame, quad, orientation); Get2ndPose
+// per item; one ObjPose per surviving 2nd-pose candidate; ordered merge.
+// The two ObjPose phases are job queues served by persistent lanes
+// (k_objpose_q): a lane whose ObjPose converged writes it out and takes the
+// next job, so a wave is not held by its slowest lane (first-ObjPose
+// iteration counts run from ~10 to ~600, candidate ones from 1 to ~800).
 // gridSquarePossibilities (Mantis3Params.h:102-123): #0 CCW, #1 mirrored.
 struct RppItem {
-  rpp::Stage1 s;
+  rpp::Stage1 s;   // s.Q holds the image points until the first ObjPose rewrites them
   double P[12];
   int32_t active, pad;
 };
+// queue control per phase: [0] job count, [1] next job
+struct RppQueue {
+  int32_t n0, next0, n1, next1;
+};
 
-__global__ __launch_bounds__(256, 2) void k_rpp_s1(const QuadRec* __restrict__ quads, const FrameState* __restrict__ st,
-                                               RppItem* __restrict__ items, double half) {
+__global__ __launch_bounds__(256) void k_rpp_prep(const QuadRec* __restrict__ quads, const FrameState* __restrict__ st,
+                                                  RppItem* __restrict__ items, int32_t* __restrict__ jobs,
+                                                  RppQueue* q, double half) {
   const int f = blockIdx.y;
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= kMaxQuads * 2) return;
-  const int q = item >> 1, o = item & 1;
-  RppItem& it = items[(size_t)f * kMaxQuads * 2 + item];
-  if (q >= st[f].n_quads) { it.active = 0; return; }
-  const QuadRec& Q = quads[(size_t)f * kMaxQuads + q];
-  double model[12], ip[12];
+  const int qd = item >> 1, o = item & 1;
+  const size_t slot = (size_t)f * kMaxQuads * 2 + item;
+  RppItem& it = items[slot];
+  if (qd >= st[f].n_quads) { it.active = 0; return; }
+  const QuadRec& Q = quads[(size_t)f * kMaxQuads + qd];
   const double sx0[4] = {half, -half, -half, half};
   const double sy0[4] = {half, half, -half, -half};
   const double sy1[4] = {-half, -half, half, half};
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    model[k] = sx0[k];
-    model[4 + k] = o == 0 ? sy0[k] : sy1[k];
-    model[8 + k] = 0.0;
-    ip[k] = Q.tp[2 * k];
-    ip[4 + k] = Q.tp[2 * k + 1];
-    ip[8 + k] = 1.0;
+    it.P[k] = sx0[k];
+    it.P[4 + k] = o == 0 ? sy0[k] : sy1[k];
+    it.P[8 + k] = 0.0;
+    it.s.Q[k] = Q.tp[2 * k];
+    it.s.Q[4 + k] = Q.tp[2 * k + 1];
+    it.s.Q[8 + k] = 1.0;
   }
-  rpp::stage1a(model, ip, it.s);
-#pragma unroll
-  for (int k = 0; k < 12; k++) it.P[k] = model[k];
   it.active = 1;
+  jobs[atomicAdd(&q->n0, 1)] = (int32_t)slot;
 }
 
-__global__ __launch_bounds__(256, 2) void k_rpp_s1_api(const double* __restrict__ img_pts,
-                                                   const double* __restrict__ obj_pts, int n,
-                                                   RppItem* __restrict__ items) {
+__global__ __launch_bounds__(256) void k_rpp_prep_api(const double* __restrict__ img_pts,
+                                                      const double* __restrict__ obj_pts, int n,
+                                                      RppItem* __restrict__ items, int32_t* __restrict__ jobs,
+                                                      RppQueue* q) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double model[12], ip[12];
+  RppItem& it = items[i];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    model[k] = obj_pts[12 * i + 3 * k];
-    model[4 + k] = obj_pts[12 * i + 3 * k + 1];
-    model[8 + k] = obj_pts[12 * i + 3 * k + 2];
-    ip[k] = img_pts[8 * i + 2 * k];
-    ip[4 + k] = img_pts[8 * i + 2 * k + 1];
-    ip[8 + k] = 1.0;
+    it.P[k] = obj_pts[12 * i + 3 * k];
+    it.P[4 + k] = obj_pts[12 * i + 3 * k + 1];
+    it.P[8 + k] = obj_pts[12 * i + 3 * k + 2];
+    it.s.Q[k] = img_pts[8 * i + 2 * k];
+    it.s.Q[4 + k] = img_pts[8 * i + 2 * k + 1];
+    it.s.Q[8 + k] = 1.0;
   }
-  rpp::stage1a(model, ip, items[i].s);
-#pragma unroll
-  for (int k = 0; k < 12; k++) items[i].P[k] = model[k];
-  items[i].active = 1;
+  it.active = 1;
+  jobs[i] = i;
+  if (i == 0) q->n0 = n;
 }
 
-// Get2ndPose setup (candidate rotations from the quartic) per active item
-__global__ __launch_bounds__(256, 2) void k_rpp_s1b(RppItem* __restrict__ items, size_t n_items) {
+// Persistent ObjPose lanes. MODE 0: job = item slot, first ObjPose (no initial
+// rotation) into items[].s. MODE 1: job = item * kCand + j, candidate ObjPose
+// from s.sR[j] into rf[job]. A wave refills its idle lanes with one atomic
+// when at least a quarter of them are idle (or all are), so the setup of new
+// jobs is shared by many lanes.
+template <int MODE>
+__device__ inline void op_begin(RppItem* items, int32_t job, rpp::OpState& s) {
+  const int32_t p = MODE == 0 ? job : job / rpp::kCand;
+  rpp::M34 P, Q;
+  const RppItem& it = items[p];
+#pragma unroll
+  for (int k = 0; k < 12; k++) { P.a[k] = it.P[k]; Q.a[k] = it.s.Q[k]; }
+  if (MODE == 0) {
+    rpp::op_setup(P, Q, nullptr, s);
+#pragma unroll
+    for (int k = 0; k < 12; k++) items[p].s.Q[k] = Q.a[k];
+  } else {
+    const int j = job - p * rpp::kCand;
+    rpp::M33 R0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) R0.a[k] = it.s.sR[j][k];
+    rpp::op_setup(P, Q, &R0, s);
+  }
+}
+
+template <int MODE>
+__device__ inline void op_end(RppItem* items, rpp::Refine* rf, int32_t job, const rpp::OpState& s, int code) {
+  rpp::M33 R;
+  rpp::M31 t;
+  double oe, ie;
+  rpp::op_finish(s, R, t, oe, ie);
+  if (MODE == 0) {
+    rpp::Stage1& o = items[job].s;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o.R[k] = R.a[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) o.t[k] = t.a[k];
+    o.obj_err = oe;
+    o.img_err = ie;
+    o.iterations = s.it;
+    o.error = code == 2 ? 2 : 0;
+    o.keep_mask = 0;
+  } else {
+    rpp::Refine& o = rf[job];
+#pragma unroll
+    for (int k = 0; k < 9; k++) o.R[k] = R.a[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) o.t[k] = t.a[k];
+    o.obj_err = oe;
+    o.img_err = ie;
+    o.iterations = s.it;
+    o.capped = code == 2 ? 1 : 0;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
+                                                   const int32_t* __restrict__ jobs, RppQueue* q) {
+  const int lane = threadIdx.x & 63;
+  const int32_t njobs = MODE == 0 ? q->n0 : q->n1;
+  int32_t* next = MODE == 0 ? &q->next0 : &q->next1;
+  rpp::OpState s;
+  int32_t job = -1;
+  bool exhausted = false;
+#pragma unroll 1
+  while (true) {
+    const uint64_t idle = __ballot(job < 0);
+    const int nidle = __popcll(idle);
+    if (!exhausted && nidle >= 16) {
+      const int leader = __ffsll((unsigned long long)idle) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(next, nidle);
+      base = __shfl(base, leader);
+      if (base + nidle >= njobs) exhausted = true;
+      if (job < 0) {
+        const int k = base + __popcll(idle & ((1ull << lane) - 1));
+        if (k < njobs) {
+          job = jobs[k];
+          op_begin<MODE>(items, job, s);
+        }
+      }
+    }
+    if (__ballot(job >= 0) == 0) {
+      if (exhausted) break;
+      continue;
+    }
+    if (job >= 0) {
+      const int code = rpp::op_step(s);
+      if (code) {
+        op_end<MODE>(items, rf, job, s, code);
+        job = -1;
+      }
+    }
+  }
+}
+
+// Get2ndPose setup (candidate rotations from the quartic) per active item;
+// every candidate that enters the search becomes a MODE-1 job
+__global__ __launch_bounds__(256) void k_rpp_s1b(RppItem* __restrict__ items, size_t n_items,
+                                                 int32_t* __restrict__ jobs1, RppQueue* q) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items || !items[i].active) return;
   double model[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) model[k] = items[i].P[k];
   rpp::stage1b(model, items[i].s);
-}
-
-// one work-item per (item, candidate slot)
-__global__ __launch_bounds__(256, 2) void k_rpp_refine(const RppItem* __restrict__ items, size_t n_items,
-                                                   rpp::Refine* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items * rpp::kCand) return;
-  const size_t p = i / rpp::kCand;
-  const int j = (int)(i - p * rpp::kCand);
-  const RppItem& it = items[p];
-  if (!it.active || it.s.error == 1 || !((it.s.keep_mask >> j) & 1)) return;
-  double model[12], Q[12], sR[9];
-#pragma unroll
-  for (int k = 0; k < 12; k++) { model[k] = it.P[k]; Q[k] = it.s.Q[k]; }
-#pragma unroll
-  for (int k = 0; k < 9; k++) sR[k] = it.s.sR[j][k];
-  rpp::refine(model, Q, sR, out[i]);
+  const int m = items[i].s.error == 1 ? 0 : items[i].s.keep_mask;
+  if (m) {
+    int b = atomicAdd(&q->n1, __popc(m));
+    for (int j = 0; j < rpp::kCand; j++)
+      if ((m >> j) & 1) jobs1[b++] = (int32_t)(i * rpp::kCand + j);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_rpp_merge(const RppItem* __restrict__ items, size_t n_items,

@@ -435,6 +435,9 @@ MK_HD int rpoly(const double* op, int degree, double* zeror, double* zeroi) {
 // At is N rows of length M (A^T), W the N singular values, Vt N x N.
 template <int M, int N>
 MK_HD void jacobi_svd(double (&At)[N * M], double (&Wout)[N], double* Vt) {
+#ifdef MK_SVD_TRACE
+  MK_SVD_TRACE(M, N, At, Vt);
+#endif
   const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
   double W[N];
 #pragma unroll
@@ -871,99 +874,139 @@ MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t
   }
 }
 
-// ObjPose (RPP.cpp:66-208); returns 1 when the (reference-unbounded) loop hit the cap
-MK_HD int obj_pose(const M34& P0, M34& Qp, const M33* initR, M33& R, M31& t, int& it, double& obj_err,
-                   double& img_err) {
-  const double TOL = 1E-5, EPS = 1E-8;
-  M34 P = P0;
-  it = 0;
-  M31 pbar = scl(rowsum(P), 1.0 / NP);
+// ObjPose (RPP.cpp:66-208) as a resumable state machine: op_setup (everything
+// before the loop), op_step (one trip of the reference's do-while: the stop
+// test, then one AbsKernel), op_finish (obj_err, img_err, t re-centring). A GPU
+// lane can then hold one job, retire it when op_step reports done and pick up
+// the next (k_objpose_q); obj_pose below runs the same three functions in a
+// plain loop, so host checks and device kernels share every operation.
+constexpr double kObjTol = 1E-5, kObjEps = 1E-8;  // RPP.cpp:7-8
+constexpr int kObjCap = 100000;                    // the reference loop is unbounded
+struct OpState {
+  M34 P;          // model points, re-centred (AbsKernel re-centres them again every call)
+  M34 Qi;         // current projections (AbsKernel input and output)
+  double F6[NP][6];  // F_i = v v^T / (v^T v), symmetric: xx xy xz yy yz zz
+  M33 G;          // tFactor
+  M33 R;
+  M31 t, pbar;
+  double old_err, new_err;
+  double qx0, qy0;  // Qp(0,0), Qp(1,0) for img_err (Q2: column 0 only)
+  int it;
+  int init_pass, first;
+};
+MK_HD M33 f_full(const double* f) {
+  M33 F;
+  F.a[0] = f[0]; F.a[1] = f[1]; F.a[2] = f[2];
+  F.a[3] = f[1]; F.a[4] = f[3]; F.a[5] = f[4];
+  F.a[6] = f[2]; F.a[7] = f[4]; F.a[8] = f[5];
+  return F;
+}
+// Qp is rewritten to F_i q_i when there is no initial rotation (the first
+// AbsKernel runs on Qp itself, RPP.cpp:105-110); the caller keeps that copy.
+MK_HD void op_setup(const M34& P0, M34& Qp, const M33* initR, OpState& s) {
+  s.P = P0;
+  s.it = 0;
+  s.pbar = scl(rowsum(s.P), 1.0 / NP);
 #pragma unroll
   for (int i = 0; i < NP; i++)
 #pragma unroll
-    for (int r = 0; r < 3; r++) P(r, i) -= pbar.a[r];
+    for (int r = 0; r < 3; r++) s.P(r, i) -= s.pbar.a[r];
   M33 F[NP];
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     M31 V = col(Qp, i);
     double ret = mm(tr(V), V).a[0];
-    F[i] = mm(V, tr(V), 1.0 / ret);
+    F[i] = mm(V, tr(V), 1.0 / ret);  // symmetric bit for bit (v_a v_b == v_b v_a)
+    s.F6[i][0] = F[i].a[0]; s.F6[i][1] = F[i].a[1]; s.F6[i][2] = F[i].a[2];
+    s.F6[i][3] = F[i].a[4]; s.F6[i][4] = F[i].a[5]; s.F6[i][5] = F[i].a[8];
   }
   M33 sumF = zeros<3, 3>();
 #pragma unroll
   for (int i = 0; i < NP; i++) sumF = add(sumF, F[i]);
   M33 I = eye3();
-  M33 tFactor = scl(inv3(sub(I, scl(sumF, 1.0 / NP))), 1.0 / NP);
-  double old_err = 0, new_err;
-  M34 Qi;
-  M33 Ri;
-  M31 ti;
-  // Without an initial rotation the reference's first AbsKernel runs on Qp
-  // itself (and rewrites it with F_i q_i, RPP.cpp:105-110); it is folded into
-  // the iteration below as pass -1 so AbsKernel has a single call site.
-  bool init_pass = initR == nullptr;
+  s.G = scl(inv3(sub(I, scl(sumF, 1.0 / NP))), 1.0 / NP);
+  s.old_err = 0;
+  s.init_pass = initR == nullptr;
   if (initR) {
-    Ri = *initR;
-    M31 s = zeros<3, 1>();
+    s.R = *initR;
+    M31 sm = zeros<3, 1>();
 #pragma unroll
-    for (int i = 0; i < NP; i++) s = mmc(mm(sub(F[i], I), Ri), col(P, i), s);
-    ti = mm(tFactor, s);
+    for (int i = 0; i < NP; i++) sm = mmc(mm(sub(F[i], I), s.R), col(s.P, i), sm);
+    s.t = mm(s.G, sm);
 #pragma unroll
     for (int i = 0; i < NP; i++) {
-      double x = P(0, i), y = P(1, i), z = P(2, i);
+      double x = s.P(0, i), y = s.P(1, i), z = s.P(2, i);
       M31 qo;
 #pragma unroll
       for (int r = 0; r < 3; r++) {
-        qo.a[r] = Ri(r, 0) * x + Ri(r, 1) * y + Ri(r, 2) * z + ti.a[r];
-        Qi(r, i) = qo.a[r];
+        qo.a[r] = s.R(r, 0) * x + s.R(r, 1) * y + s.R(r, 2) * z + s.t.a[r];
+        s.Qi(r, i) = qo.a[r];
       }
-      old_err += sqnorm3(mm(sub(I, F[i]), qo));
+      s.old_err += sqnorm3(mm(sub(I, F[i]), qo));
     }
   } else {
-    Qi = Qp;
+    s.Qi = Qp;
+    // what the first AbsKernel leaves in Qp: F_i q_i, computed as it does
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+      M31 q = mm(F[i], col(Qp, i));
+#pragma unroll
+      for (int r = 0; r < 3; r++) Qp(r, i) = q.a[r];
+    }
   }
-  int capped = 0;
+  s.qx0 = Qp(0, 0);
+  s.qy0 = Qp(1, 0);
   // the reference computes one AbsKernel before testing the stop rule
-  new_err = old_err;
-  bool first = true;
-#pragma unroll 1
-  while (true) {
-    if (!first) {
-      if (!(fabs((old_err - new_err) / old_err) > TOL && (new_err > EPS))) break;
-      if (it >= 100000) { capped = 1; break; }
-      old_err = new_err;
-    }
-    abs_kernel(P, Qi, F, tFactor, Ri, ti, Qi, new_err);
-    it = it + 1;
-    if (init_pass) {
-      // abs_kernel rewrote its input Q (= Qp) before forming Qi; recover Qp's
-      // new content: F_i q_i is recomputed exactly as abs_kernel did
-#pragma unroll
-      for (int i = 0; i < NP; i++) {
-        M31 q = mm(F[i], col(Qp, i));
-#pragma unroll
-        for (int r = 0; r < 3; r++) Qp(r, i) = q.a[r];
-      }
-      init_pass = false;
-      old_err = new_err;
-      continue;
-    }
-    first = false;
+  s.new_err = s.old_err;
+  s.first = 1;
+}
+// one loop trip; returns 0 while running, 1 converged, 2 iteration cap
+MK_HD int op_step(OpState& s) {
+  if (!s.first) {
+    if (!(fabs((s.old_err - s.new_err) / s.old_err) > kObjTol && (s.new_err > kObjEps))) return 1;
+    if (s.it >= kObjCap) return 2;
+    s.old_err = s.new_err;
   }
-  R = Ri;
-  t = ti;
-  obj_err = sqrt(new_err / NP);
+  M33 F[NP];
+#pragma unroll
+  for (int i = 0; i < NP; i++) F[i] = f_full(s.F6[i]);
+  abs_kernel(s.P, s.Qi, F, s.G, s.R, s.t, s.Qi, s.new_err);
+  s.it = s.it + 1;
+  if (s.init_pass) {
+    s.init_pass = 0;
+    s.old_err = s.new_err;
+  } else {
+    s.first = 0;
+  }
+  return 0;
+}
+MK_HD void op_finish(const OpState& s, M33& R, M31& t, double& obj_err, double& img_err) {
+  R = s.R;
+  obj_err = sqrt(s.new_err / NP);
   img_err = 0;
 #pragma unroll
   for (int i = 0; i < NP; i++) {
-    M31 Qproj = mmc(Ri, col(P, i), ti);
-    double xx = (Qproj.a[0] / Qproj.a[2]) - Qp(0, 0);
-    double yy = (Qproj.a[1] / Qproj.a[2]) - Qp(1, 0);
+    M31 Qproj = mmc(s.R, col(s.P, i), s.t);
+    double xx = (Qproj.a[0] / Qproj.a[2]) - s.qx0;
+    double yy = (Qproj.a[1] / Qproj.a[2]) - s.qy0;
     img_err += (xx * xx + yy * yy);
   }
   img_err = sqrt(img_err / NP);
-  t = sub(t, mm(Ri, pbar));
-  return capped;
+  t = sub(s.t, mm(s.R, s.pbar));
+}
+
+// ObjPose (RPP.cpp:66-208); returns 1 when the (reference-unbounded) loop hit the cap
+MK_HD int obj_pose(const M34& P0, M34& Qp, const M33* initR, M33& R, M31& t, int& it, double& obj_err,
+                   double& img_err) {
+  OpState s;
+  op_setup(P0, Qp, initR, s);
+  int r;
+#pragma unroll 1
+  while ((r = op_step(s)) == 0) {
+  }
+  op_finish(s, R, t, obj_err, img_err);
+  it = s.it;
+  return r == 2 ? 1 : 0;
 }
 
 MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
