@@ -12,7 +12,7 @@ all: product tools oracle
 
 product: mantis_amd/libmantis_amd.so
 mantis_amd/libmantis_amd.so: $(CSRC)/api.hip $(CSRC)/kernels.hip $(CSRC)/gn_impl.hip $(wildcard $(CSRC)/*.h) include/mantis.h
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/api.hip -lrccl
+	$(HIPCC) $(HIPFLAGS) -shared -pthread -o $@ $(CSRC)/api.hip -lrccl
 
 tools: build/libmantis_hostcheck.so tools/libmantis_synth.so
 build/libmantis_hostcheck.so: $(CSRC)/hostcheck.cpp $(wildcard $(CSRC)/mk_*.h)

@@ -34,6 +34,10 @@ import numpy as np
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
+# FP64 operations of one ObjPose iteration (one AbsKernel: the 3x3 accumulations,
+# OpenCV's one-sided Jacobi SVD, R, t and the error), counted by
+# tools/rpp_flops.cpp on the host build of mk_rpp.h (+,-,*,/,sqrt,hypot = 1 each)
+FLOPS_PER_OBJPOSE_ITER = 4282
 W, H = 1280, 720
 CAMS = 4
 LANDMARKS = 720
@@ -46,19 +50,22 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rigs", type=int, default=128, help="rigs per step per GPU")
+    p.add_argument("--rigs", type=int, default=1024, help="rigs per step per GPU")
     p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
-    p.add_argument("--contexts", type=int, default=2,
+    p.add_argument("--contexts", type=int, default=8,
                    help="library contexts per GPU, each driven by its own host thread (one ctx per thread, "
                         "include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
     p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
+    p.add_argument("--hw-queues", type=int, default=8,
+                   help="GPU_MAX_HW_QUEUES for this process, so the contexts' streams run on separate hardware queues")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
 
 
 def main():
     a = parse()
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, a.hw_queues))))  # before HIP initialises
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -161,46 +168,68 @@ def main():
     value = poses / elapsed
     ms_per_step = elapsed / a.steps * 1e3
 
-    # ---- dominant kernel roofline (per launch = per step)
-    avg = {k: v / a.steps for k, v in stage_ms.items()}
-    dom = max(avg, key=avg.get) if avg else None
+    # ---- per-step work counts (every step processes the same frames, so the
+    # counters of the last step describe each step): ObjPose iterations of the
+    # two RPP queues, scored hypotheses
     frames_step = rigs_ctx * CAMS  # stage events are recorded on context 0's stream, over its frames
+    iters = [0, 0]
+    for i in range(frames_step):
+        fc = m.frame_counters(i)
+        iters[0] += int(fc[16])
+        iters[1] += int(fc[17])
     scored_per_frame = scored / max(1, a.steps * n_frames)
     slow_per_frame = 80.0
     fast_per_frame = max(0.0, scored_per_frame - slow_per_frame)
     s_fast = LANDMARKS * fast_per_frame
     s_slow = 3700.0 * slow_per_frame
-    # algorithmic bytes per launch of each stage
-    alg_bytes = {
-        "canny_nms": frames_step * (3 * W * H + W * H),
-        "score_pf_yaw": frames_step * (3 * (s_fast + s_slow) + s_fast),
-        "contours_quads": frames_step * ((W + 2) * (H + 2)),
-        "mask_morph": frames_step * (2 * W * H),
-        "det_morph": frames_step * (2 * W * H),
-        "hysteresis": frames_step * (2 * W * H),
-        "components": frames_step * (5 * (W + 2) * (H + 2)),
+
+    # ---- roofline of the dominant stage (per launch = per step on context 0)
+    avg = {k: v / a.steps for k, v in stage_ms.items()}
+    # algorithmic bytes (HBM-bound stages) or FP64 flops (VALU-bound stages) per launch
+    work = {
+        "canny_nms": ("hbm", frames_step * (3 * W * H + W * H)),
+        "hysteresis": ("hbm", frames_step * (2 * W * H)),
+        "det_morph": ("hbm", frames_step * (2 * W * H // 8)),
+        "mask_morph": ("hbm", frames_step * (2 * W * H // 8 * 15 + W * H)),
+        "components": ("hbm", frames_step * (5 * (W + 2) * (H + 2))),
+        "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
+        "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
+        "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),
+        "score_pf_yaw": ("fp64", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
+                                                FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
-    roof = None
-    if dom:
-        dur_s = avg[dom] * 1e-3
-        b = alg_bytes.get(dom, 0.0)
-        achieved = b / dur_s / 1e9 if dur_s > 0 else 0.0
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                tj = json.load(open(pmc))
-                if tj.get("stage") == dom and tj.get("rigs") == a.rigs:
-                    traffic = tj.get("bytes_per_launch")
-            except Exception:
-                traffic = None
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "avg_launch_ms": round(avg[dom], 4),
-                "fp64_tflops": round(frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
-                                                    FLOPS_PER_WINDOW * 37 * slow_per_frame) / dur_s / 1e12, 4)
-                if dom == "score_pf_yaw" else None,
-                "stages_ms": {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}}
+
+    def roofline(stage):
+        if stage not in avg or stage not in work:
+            return None
+        kind, amount = work[stage]
+        dur_s = avg[stage] * 1e-3
+        if kind == "hbm":
+            achieved = amount / dur_s / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    tj = json.load(open(pmc))
+                    if tj.get("stage") == stage and tj.get("frames_per_launch") == frames_step:
+                        traffic = tj.get("bytes_per_launch")
+                except Exception:
+                    traffic = None
+            return {"bound": "hbm", "kernel": stage, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "alg_bytes_per_launch": int(amount), "avg_launch_ms": round(avg[stage], 4)}
+        achieved = amount / dur_s / 1e12
+        return {"bound": "fp64_valu", "kernel": stage, "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                "alg_flops_per_launch": int(amount), "avg_launch_ms": round(avg[stage], 4)}
+
+    kern = [k for k in avg if k in work]
+    dom = max(kern, key=avg.get) if kern else None  # dominant kernel stage by event time
+    roof = roofline(dom) if dom else None
+    if roof is not None:
+        roof["stages_ms"] = {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}
+        roof["objpose_iterations_per_launch"] = iters
+    roof_front = roofline("canny_nms")
     path_bytes = n_frames * (6 * W * H + 3 * (s_fast + s_slow))
 
     # ---- p50 latency of one rig (host submit -> result on host)
@@ -248,6 +277,7 @@ def main():
             "published_frac": round(published / max(1, a.rigs * a.steps), 4),
             "path_alg_GBps": round(path_bytes * a.steps / elapsed / 1e9, 3),
             "roofline": roof,
+            "roofline_frontend": roof_front,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -227,8 +227,8 @@ class Mantis:
         return list(out), list(cam_out)
 
     def frame_counters(self, i):
-        out = np.zeros(16, np.int32)
-        k = lib().mantis_frame_counters(self.h, i, out.ctypes.data, 16)
+        out = np.zeros(32, np.int32)
+        k = lib().mantis_frame_counters(self.h, i, out.ctypes.data, 32)
         if k < 0:
             raise MantisError("frame_counters: bad frame index")
         return out[:k]

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -305,11 +306,15 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
 }
 
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
-                       RppOut* out, size_t ni, size_t expected_items) {
-  k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q);
+                       RppOut* out, FrameState* st, size_t ni, size_t expected_items) {
+  k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q, st);
+  mark(c, "rpp_first");
   k_rpp_s1b<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, jobs1, q);
-  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q);
+  mark(c, "rpp_2nd");
+  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st);
+  mark(c, "rpp_cand");
   k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out);
+  mark(c, "rpp_merge");
 }
 
 mantis_status run_pose(Ctx* c, int n) {
@@ -317,8 +322,8 @@ mantis_status run_pose(Ctx* c, int n) {
   dim3 gr((kMaxQuads * 2 + 255) / 256, n);
   k_rpp_prep<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_items, c->d_jobs0, c->d_rq, c->cfg.grid_spacing / 2);
   const size_t ni = (size_t)n * kMaxQuads * 2;
-  launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, ni, (size_t)n * 160);
-  mark(c, "rpp");
+  mark(c, "rpp_prep");
+  launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160);
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
   const int per = c->cfg.particles * c->cfg.iterations * 6;
@@ -443,13 +448,22 @@ void fuse_rig(const mantis_image* cams, const mantis_cam_result* cr, int nc, man
 
 mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
   if (!c->d_lm) { c->err = "map not set (mantis_set_map)"; return MANTIS_ERR_STATE; }
+  if (n <= 0 || n > c->F) { c->err = "frame count exceeds max_cams"; return MANTIS_ERR_ARG; }
+  // The gaussian stream depends only on the RNG state, so a host thread draws
+  // it while the device runs the image stages and RPP (the pinned buffer is
+  // not in use: the previous call synchronised).
+  struct Joiner {
+    std::thread t;
+    ~Joiner() { if (t.joinable()) t.join(); }
+  } gauss;
+  gauss.t = std::thread([c, n] { gen_gauss(c, n); });
   int W, H;
   mantis_status st = stage_frames(c, cams, n, W, H);
   if (st != MANTIS_OK) return st;
   if ((st = run_image_stages(c, n, W, H)) != MANTIS_OK) return st;
   if ((st = run_contours(c, n, W, H)) != MANTIS_OK) return st;
   if ((st = run_pose(c, n)) != MANTIS_OK) return st;
-  gen_gauss(c, n);  // overlaps the device work queued above
+  gauss.t.join();
   if ((st = run_score(c, n)) != MANTIS_OK) return st;
   HIP_OK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(mantis_cam_result) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
@@ -874,12 +888,15 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
   HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 8 * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemsetAsync(d_q, 0, sizeof(RppQueue), c->s));
+  mark(c, "start");
   k_rpp_prep_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it, d_j0, d_q);
-  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, (size_t)n, (size_t)n);
+  mark(c, "rpp_prep");
+  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, nullptr, (size_t)n, (size_t)n);
   HIP_OK(hipGetLastError());
   std::vector<RppOut> h(n);
   HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
+  finish_profile(c);
   for (int i = 0; i < n; i++) {
     for (int k = 0; k < 9; k++) R[9 * i + k] = h[i].R[k];
     for (int k = 0; k < 3; k++) t[3 * i + k] = h[i].t[k];

@@ -1020,7 +1020,12 @@ __device__ inline void op_begin(RppItem* items, int32_t job, rpp::OpState& s) {
 }
 
 template <int MODE>
-__device__ inline void op_end(RppItem* items, rpp::Refine* rf, int32_t job, const rpp::OpState& s, int code) {
+__device__ inline void op_end(RppItem* items, rpp::Refine* rf, FrameState* st, int32_t job, const rpp::OpState& s,
+                              int code) {
+  if (st) {
+    const int32_t p = MODE == 0 ? job : job / rpp::kCand;
+    atomicAdd(&st[p / (kMaxQuads * 2)].rpp_iters[MODE], s.it);
+  }
   rpp::M33 R;
   rpp::M31 t;
   double oe, ie;
@@ -1051,7 +1056,7 @@ __device__ inline void op_end(RppItem* items, rpp::Refine* rf, int32_t job, cons
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
-                                                   const int32_t* __restrict__ jobs, RppQueue* q) {
+                                                   const int32_t* __restrict__ jobs, RppQueue* q, FrameState* st) {
   const int lane = threadIdx.x & 63;
   const int32_t njobs = MODE == 0 ? q->n0 : q->n1;
   int32_t* next = MODE == 0 ? &q->next0 : &q->next1;
@@ -1083,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
     if (job >= 0) {
       const int code = rpp::op_step(s);
       if (code) {
-        op_end<MODE>(items, rf, job, s, code);
+        op_end<MODE>(items, rf, st, job, s, code);
         job = -1;
       }
     }

@@ -15,6 +15,7 @@
 #pragma once
 #include <cfloat>
 #include <cmath>
+#include <cstring>
 
 #include "mk_math.h"
 
@@ -431,8 +432,80 @@ MK_HD int rpoly(const double* op, int degree, double* zeror, double* zeroi) {
 }
 
 // ---------------------------------------------------------------- JacobiSVD
-// Compile-time sizes throughout so every matrix stays in VGPRs (no scratch):
-// At is N rows of length M (A^T), W the N singular values, Vt N x N.
+// One-sided Jacobi as OpenCV's JacobiSVDImpl_ (what cv::SVD computes for
+// these shapes). Compile-time sizes throughout so every matrix stays in VGPRs
+// (no scratch): At is N rows of length M (A^T), W the N singular values, Vt
+// N x N.
+
+// One rotation of rows (i, j) with its skip test; returns whether it rotated.
+template <int M, int N>
+MK_HD bool jacobi_pair(double* At, double* W, double* Vt, int i, int j) {
+  const double eps = DBL_EPSILON * 10;
+  double a = W[i], p = 0, b = W[j];
+#pragma unroll
+  for (int k = 0; k < M; k++) p += At[i * M + k] * At[j * M + k];
+  if (fabs(p) <= eps * sqrt(a * b)) return false;
+  p *= 2;
+  double beta = a - b, gamma, c, s;
+  if (fabs(p) <= fabs(beta) * 0x1p-60) {
+    // hypot(p, beta) == |beta| exactly here (|p| is below half an ulp of
+    // |beta|), so the reference's sqrt of (2|beta| / 2|beta|) is exactly 1
+    // and one division is left. This is the common case once a row has
+    // decayed to rounding noise: a planar model makes M rank 2, and the
+    // reference keeps rotating that row until it underflows (~20 sweeps).
+    gamma = fabs(beta);
+    if (beta < 0) {
+      s = 1.0;
+      c = p / (gamma * s * 2);
+    } else {
+      c = 1.0;
+      s = p / (gamma * c * 2);
+    }
+  } else {
+    gamma = hypot(p, beta);
+    if (beta < 0) {
+      double delta = (gamma - beta) * 0.5;
+      s = sqrt(delta / gamma);
+      c = p / (gamma * s * 2);
+    } else {
+      c = sqrt((gamma + beta) / (gamma * 2));
+      s = p / (gamma * c * 2);
+    }
+  }
+  a = b = 0;
+#pragma unroll
+  for (int k = 0; k < M; k++) {
+    double t0 = c * At[i * M + k] + s * At[j * M + k];
+    double t1 = -s * At[i * M + k] + c * At[j * M + k];
+    At[i * M + k] = t0; At[j * M + k] = t1;
+    a += t0 * t0; b += t1 * t1;
+  }
+  W[i] = a; W[j] = b;
+  if (Vt) {
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      double t0 = c * Vt[i * N + k] + s * Vt[j * N + k];
+      double t1 = -s * Vt[i * N + k] + c * Vt[j * N + k];
+      Vt[i * N + k] = t0; Vt[j * N + k] = t1;
+    }
+  }
+  return true;
+}
+
+template <int M, int N>
+MK_HD void jacobi_sweeps(double* At, double* W, double* Vt) {
+  const int max_iter = M > 30 ? M : 30;
+#pragma unroll 1
+  for (int iter = 0; iter < max_iter; iter++) {
+    bool changed = false;
+#pragma unroll
+    for (int i = 0; i < N - 1; i++)
+#pragma unroll
+      for (int j = i + 1; j < N; j++) changed |= jacobi_pair<M, N>(At, W, Vt, i, j);
+    if (!changed) break;
+  }
+}
+
 template <int M, int N>
 MK_HD void jacobi_svd(double (&At)[N * M], double (&Wout)[N], double* Vt) {
 #ifdef MK_SVD_TRACE
@@ -451,66 +524,7 @@ MK_HD void jacobi_svd(double (&At)[N * M], double (&Wout)[N], double* Vt) {
       for (int k = 0; k < N; k++) Vt[i * N + k] = (k == i) ? 1.0 : 0.0;
     }
   }
-  const int max_iter = M > 30 ? M : 30;
-#pragma unroll 1
-  for (int iter = 0; iter < max_iter; iter++) {
-    bool changed = false;
-#pragma unroll
-    for (int i = 0; i < N - 1; i++)
-#pragma unroll
-      for (int j = i + 1; j < N; j++) {
-        double a = W[i], p = 0, b = W[j];
-#pragma unroll
-        for (int k = 0; k < M; k++) p += At[i * M + k] * At[j * M + k];
-        if (fabs(p) <= eps * sqrt(a * b)) continue;
-        p *= 2;
-        double beta = a - b, gamma, c, s;
-        if (fabs(p) <= fabs(beta) * 0x1p-60) {
-          // hypot(p, beta) == |beta| exactly here (|p| is below half an ulp of
-          // |beta|), so the reference's sqrt of (2|beta| / 2|beta|) is exactly 1
-          // and one division is left. This is the common case once a row has
-          // decayed to rounding noise: a planar model makes M rank 2, and the
-          // reference keeps rotating that row until it underflows (~20 sweeps).
-          gamma = fabs(beta);
-          if (beta < 0) {
-            s = 1.0;
-            c = p / (gamma * s * 2);
-          } else {
-            c = 1.0;
-            s = p / (gamma * c * 2);
-          }
-        } else {
-          gamma = hypot(p, beta);
-          if (beta < 0) {
-            double delta = (gamma - beta) * 0.5;
-            s = sqrt(delta / gamma);
-            c = p / (gamma * s * 2);
-          } else {
-            c = sqrt((gamma + beta) / (gamma * 2));
-            s = p / (gamma * c * 2);
-          }
-        }
-        a = b = 0;
-#pragma unroll
-        for (int k = 0; k < M; k++) {
-          double t0 = c * At[i * M + k] + s * At[j * M + k];
-          double t1 = -s * At[i * M + k] + c * At[j * M + k];
-          At[i * M + k] = t0; At[j * M + k] = t1;
-          a += t0 * t0; b += t1 * t1;
-        }
-        W[i] = a; W[j] = b;
-        changed = true;
-        if (Vt) {
-#pragma unroll
-          for (int k = 0; k < N; k++) {
-            double t0 = c * Vt[i * N + k] + s * Vt[j * N + k];
-            double t1 = -s * Vt[i * N + k] + c * Vt[j * N + k];
-            Vt[i * N + k] = t0; Vt[j * N + k] = t1;
-          }
-        }
-      }
-    if (!changed) break;
-  }
+  jacobi_sweeps<M, N>(At, W, Vt);
 #pragma unroll
   for (int i = 0; i < N; i++) {
     double sd = 0;

@@ -12,5 +12,5 @@ import json
 for l in open('gpurun_out/sweep.log'):
     if l.startswith('=='): print(l.strip(), end=' ')
     elif l.startswith('{'):
-        d=json.loads(l); print(d['value'], d['ms_per_step'], d['roofline']['stages_ms'].get('rpp'))
+        d=json.loads(l); r=d.get('roofline') or {}; print(d['value'], d['ms_per_step'], d['p50_latency_ms'], r.get('kernel'), r.get('achieved'), r.get('unit'), json.dumps(r.get('stages_ms')))
 P
