@@ -117,7 +117,8 @@ struct Ctx {
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
-  uint8_t *d_bgr = nullptr, *d_cls = nullptr, *d_strong = nullptr, *d_edge = nullptr,
+  uint16_t* d_lroot = nullptr;  // per-pixel Canny tile root (k_canny_uf -> k_hyst_edge)
+  uint8_t *d_bgr = nullptr, *d_strong = nullptr, *d_edge = nullptr,
           *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
@@ -134,7 +135,8 @@ struct Ctx {
   rpp::Refine* d_refine = nullptr;
   int32_t *d_jobs0 = nullptr, *d_jobs1 = nullptr;  // RPP ObjPose job queues
   RppQueue* d_rq = nullptr;
-  int rpp_blocks = 0;  // persistent-lane grid cap for k_objpose_q (0 = auto)
+  int rpp_blocks = 0;
+  bool vec_ok = false;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   FrameDebug* d_dbg = nullptr;
@@ -219,6 +221,8 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
       fd.bgr = dst;
     }
   }
+  c->vec_ok = (W % 4) == 0;
+  for (int i = 0; i < n; i++) c->vec_ok = c->vec_ok && ((uintptr_t)c->h_frames[i].bgr & 3) == 0;
   HIP_OK(hipMemcpyAsync(c->d_frames, c->h_frames, sizeof(FrameDesc) * n, hipMemcpyHostToDevice, c->s));
   return MANTIS_OK;
 }
@@ -230,20 +234,18 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const int Wp = W + 2, Hp = H + 2;
   if (det_bytes) HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
   mark(c, "start");
-  dim3 gt((W + TX - 1) / TX, (H + TY - 1) / TY, n);
-  k_canny_cls<<<gt, 256, 0, c->s>>>(c->d_frames, c->d_cls, P, c->cfg.canny_low, 3 * c->cfg.canny_low);
+  const size_t B = c->bstride;
+  dim3 gf((W + FTW - 1) / FTW, (H + FTH - 1) / FTH, n);
+  k_canny_uf<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
+                                   c->d_b2, c->d_lroot, c->d_lab, c->d_strong, P, B);
   mark(c, "canny_nms");
-  dim3 gp(blocks_for(npx), n);
-  dim3 ght((W + CW - 1) / CW, (H + CH - 1) / CH, n);
-  k_hyst_tile<<<ght, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
-  const size_t nhseam = (size_t)((W - 1) / CW) * H + (size_t)((H - 1) / CH) * W;
-  k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_cls, c->d_lab, W, H, P);
-  k_hyst_strong<<<gp, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, W, H, P);
+  const size_t nhseam = (size_t)((W - 1) / FTW) * H + (size_t)((H - 1) / FTH) * W;
+  if (nhseam) k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_b1, c->d_lab, W, H, P, B);
   const size_t nw = (size_t)((W + 31) / 32) * H;
   dim3 gw(blocks_for(nw), n);
-  const size_t B = c->bstride;
-  k_hyst_edge<<<gw, 256, 0, c->s>>>(c->d_cls, c->d_lab, c->d_strong, c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H,
-                                    P, B);
+  k_hyst_mark<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_lab, c->d_strong, W, H, P, B);
+  k_hyst_edge<<<gf, 256, 0, c->s>>>(c->d_lroot, c->d_lab, c->d_strong, c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H, P,
+                                    B);
   mark(c, "hysteresis");
   // detector: dilate(iter 2) = 5x5 rect, erode(iter 1) = 3x3 rect -> zero-ringed det bytes
   k_bh<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B, 2, 1);
@@ -281,7 +283,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   dim3 gtile((Wp + CW - 1) / CW, (Hp + CH - 1) / CH, n);
   k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_st, Wp, Hp, P);
   const size_t nseam = (size_t)((Wp - 1) / CW) * Hp + (size_t)((Hp - 1) / CH) * Wp;
-  k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp,
+  if (nseam) k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp,
                                                                          P);
   k_border_emit<<<dim3(64, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_borders, c->d_st, Wp,
                                                P, kMaxBorders);
@@ -575,8 +577,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   mantis_status st = MANTIS_OK;
   auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
   chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
-  chk(dalloc(c, &c->d_cls, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_lroot, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_edge, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_det, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_eb, (size_t)F * c->bstride));
@@ -645,7 +647,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_cls, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)

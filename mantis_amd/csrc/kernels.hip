@@ -1,8 +1,8 @@
 // HIP kernels (gfx950) of the mantis3 per-frame hot path. Host side: api.hip.
 //
 // Stage map (reference -> kernel):
-//   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_cls
-//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_tile / _seam / _strong / _edge
+//   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_uf (+ tile union-find)
+//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_seam / _mark / _edge
 //   dilate x2 / erode x1             QuadDetection.h:213-214         k_bh / k_bv / k_pack_det (bit planes)
 //   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_bm0 + k_bh / k_bv
 //   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_cc_tile / _seam / _flatten + k_border_emit
@@ -28,120 +28,6 @@
 #include "synth.h"
 
 namespace mk {
-
-// ============================================================ image stage 1
-constexpr int TX = 64, TY = 16;
-
-__device__ inline int refl101(int i, int n) {
-  if (n == 1) return 0;
-  if (i < 0) return -i;
-  if (i >= n) return 2 * n - 2 - i;
-  return i;
-}
-
-// gray -> 3x3 Gaussian (x256 kernel [84,89,84], OpenCV <= 3.3) -> Sobel 3x3
-// (REPLICATE) -> L1 magnitude -> non-maximum suppression. cls: 0 none,
-// 1 weak candidate, 2 strong.
-__global__ __launch_bounds__(256) void k_canny_cls(const FrameDesc* __restrict__ frames, uint8_t* __restrict__ cls,
-                                                   size_t plane, int low, int high) {
-  const int f = blockIdx.z;
-  const FrameDesc fd = frames[f];
-  const int W = fd.w, H = fd.h;
-  const int x0 = blockIdx.x * TX, y0 = blockIdx.y * TY;
-  if (x0 >= W || y0 >= H) return;
-  __shared__ uint8_t g[TY + 6][TX + 6];
-  __shared__ int32_t rowb[TY + 6][TX + 4];
-  __shared__ uint8_t bl[TY + 4][TX + 4];
-  __shared__ int16_t sdx[TY + 2][TX + 2], sdy[TY + 2][TX + 2];
-  __shared__ int32_t mag[TY + 2][TX + 2];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < (TY + 6) * (TX + 6); i += 256) {
-    int ly = i / (TX + 6), lx = i % (TX + 6);
-    int x = x0 - 3 + lx, y = y0 - 3 + ly;
-    uint8_t v = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      const uint8_t* p = fd.bgr + ((size_t)y * W + x) * 3;
-      v = (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
-    }
-    g[ly][lx] = v;
-  }
-  __syncthreads();
-  // horizontal pass of the blur on rows y0-3 .. y0+TY+2, columns x0-2 .. x0+TX+1
-  for (int i = tid; i < (TY + 6) * (TX + 4); i += 256) {
-    int ly = i / (TX + 4), lx = i % (TX + 4);
-    int x = x0 - 2 + lx, y = y0 - 3 + ly;
-    int v = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      int xm = refl101(x - 1, W) - (x0 - 3), xc = x - (x0 - 3), xp = refl101(x + 1, W) - (x0 - 3);
-      v = 84 * g[ly][xm] + 89 * g[ly][xc] + 84 * g[ly][xp];
-    }
-    rowb[ly][lx] = v;
-  }
-  __syncthreads();
-  for (int i = tid; i < (TY + 4) * (TX + 4); i += 256) {
-    int ly = i / (TX + 4), lx = i % (TX + 4);
-    int x = x0 - 2 + lx, y = y0 - 2 + ly;
-    uint8_t v = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      int ym = refl101(y - 1, H) - (y0 - 3), yc = y - (y0 - 3), yp = refl101(y + 1, H) - (y0 - 3);
-      int acc = 84 * rowb[ym][lx] + 89 * rowb[yc][lx] + 84 * rowb[yp][lx];
-      int r = (acc + (1 << 15)) >> 16;
-      v = (uint8_t)(r > 255 ? 255 : (r < 0 ? 0 : r));
-    }
-    bl[ly][lx] = v;
-  }
-  __syncthreads();
-  for (int i = tid; i < (TY + 2) * (TX + 2); i += 256) {
-    int ly = i / (TX + 2), lx = i % (TX + 2);
-    int x = x0 - 1 + lx, y = y0 - 1 + ly;
-    int gx = 0, gy = 0, m = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      auto B = [&](int xx, int yy) -> int {
-        xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
-        yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
-        return bl[yy - (y0 - 2)][xx - (x0 - 2)];
-      };
-      gx = (B(x + 1, y - 1) - B(x - 1, y - 1)) + 2 * (B(x + 1, y) - B(x - 1, y)) + (B(x + 1, y + 1) - B(x - 1, y + 1));
-      gy = (B(x - 1, y + 1) - B(x - 1, y - 1)) + 2 * (B(x, y + 1) - B(x, y - 1)) + (B(x + 1, y + 1) - B(x + 1, y - 1));
-      m = abs(gx) + abs(gy);
-    }
-    sdx[ly][lx] = (int16_t)gx;
-    sdy[ly][lx] = (int16_t)gy;
-    mag[ly][lx] = m;
-  }
-  __syncthreads();
-  const int SHIFT = 15;
-  const int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
-  uint8_t* cf = cls + (size_t)f * plane;
-  for (int i = tid; i < TY * TX; i += 256) {
-    int ly = i / TX, lx = i % TX;
-    int x = x0 + lx, y = y0 + ly;
-    if (x >= W || y >= H) continue;
-    int cy = ly + 1, cx = lx + 1;
-    int m = mag[cy][cx];
-    uint8_t c = 0;
-    if (m > low) {
-      int xs = sdx[cy][cx], ys = sdy[cy][cx];
-      int ax = abs(xs);
-      int ay = abs(ys) << SHIFT;
-      int tg22x = ax * TG22;
-      bool push;
-      if (ay < tg22x) {
-        push = m > mag[cy][cx - 1] && m >= mag[cy][cx + 1];
-      } else {
-        int tg67x = tg22x + (ax << (SHIFT + 1));
-        if (ay > tg67x) {
-          push = m > mag[cy - 1][cx] && m >= mag[cy + 1][cx];
-        } else {
-          int s = (xs ^ ys) < 0 ? -1 : 1;
-          push = m > mag[cy - 1][cx - s] && m > mag[cy + 1][cx + s];
-        }
-      }
-      if (push) c = (m > high) ? 2 : 1;
-    }
-    cf[(size_t)y * W + x] = c;
-  }
-}
 
 // ======================================================== union-find (CCL)
 // Concurrent union by index: roots are component minima, links point to
@@ -187,135 +73,353 @@ __device__ inline void lds_union(int* L, int a, int b) {
 }
 constexpr int CW = 64, CH = 32;  // union-find tile
 
-// Canny hysteresis (cv::Canny's stack walk = 8-connected components of the
-// candidates that contain a strong pixel), two-level:
-//   k_hyst_tile  LDS union-find of candidates per 64x32 tile; each candidate
-//                gets its tile root's global index, each tile root its strong flag
+// ============================================== Canny: classes + hysteresis
+// cvtColor(BGR2GRAY) -> GaussianBlur 3x3 (x256 kernel [84,89,84], OpenCV <= 3.3,
+// BORDER_REFLECT_101) -> Sobel 3x3 (REPLICATE) -> L1 magnitude -> NMS
+// (QuadDetection.h:209-212, HypothesisEvaluation.h:323-327; one Canny serves
+// both) and cv::Canny's hysteresis stack walk, i.e. the 8-connected components
+// of the NMS candidates that hold a strong pixel. Two-level, with nothing
+// per-pixel written to HBM but bit planes:
+//   k_canny_uf   per 128x32 tile: BGR (vector loads) -> classes in LDS, LDS
+//                union-find of the candidates; writes the candidate bit plane,
+//                a bit plane of the tile roots whose component holds a strong
+//                pixel, and sparse labels (tile roots, tile-border candidates)
 //   k_hyst_seam  unions across tile seams (global, path halving)
-//   k_hyst_strong  strong pixels mark their global root
-//   k_hyst_edge  edge = candidate whose global root is marked (bit plane)
-__global__ __launch_bounds__(256) void k_hyst_tile(const uint8_t* __restrict__ cls, int32_t* __restrict__ lab,
-                                                   uint8_t* __restrict__ strong, int W, int H, size_t plane) {
-  __shared__ uint8_t C[CH * CW];
-  __shared__ int L[CH * CW];
-  __shared__ uint8_t S[CH * CW];
-  const int f = blockIdx.z;
-  const int x0 = blockIdx.x * CW, y0 = blockIdx.y * CH;
-  const uint8_t* c = cls + (size_t)f * plane;
-  int32_t* l = lab + (size_t)f * plane;
-  uint8_t* sg = strong + (size_t)f * plane;
-  const int t = threadIdx.x;
-  for (int i = t; i < CH * CW; i += 256) {
-    const int x = x0 + (i % CW), y = y0 + (i / CW);
-    C[i] = (x < W && y < H) ? c[(size_t)y * W + x] : 0;
-    S[i] = 0;
-  }
-  __syncthreads();
+//   k_hyst_mark  strong tile roots mark their global root
+//   k_hyst_edge  per tile: the same LDS union-find again; edge = candidate
+//                whose global root is marked (bit plane, bytes on request)
+constexpr int FTW = 128, FTH = 32;            // front-end tile
+constexpr int FSEG = FTW * FTH / 256;          // pixels per thread-run in the tile union-find
+constexpr int FGW = FTW + 8, FGH = FTH + 6;    // gray tile: x0-4 .. x0+FTW+3 (4-aligned), y0-3 .. y0+FTH+2
+constexpr int FRW = FTW + 4;                   // blurred columns x0-2 .. x0+FTW+1
+constexpr int FMW = FTW + 2, FMH = FTH + 2;    // magnitude: x0-1 .. x0+FTW, y0-1 .. y0+FTH
+
+__device__ inline int refl101(int i, int n) {  // BORDER_REFLECT_101
+  if (n == 1) return 0;
+  if (i < 0) return -i;
+  if (i >= n) return 2 * n - 2 - i;
+  return i;
+}
+
+__device__ inline uint8_t gray_px(const uint8_t* p) {
+  return (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
+}
+
+// 8-connected union-find of the candidates C (LDS bytes) of one FTW x FTH tile;
+// leaves every candidate's L at its component's minimum index (deterministic).
+__device__ inline void tile_uf(const uint8_t* C, int* L, int t) {
+  constexpr int SPR = FTW / FSEG;
   {
-    const int base = (t >> 3) * CW + (t & 7) * 8;
+    const int base = (t / SPR) * FTW + (t % SPR) * FSEG;
     int run = base;
     L[base] = base;
-    for (int k = 1; k < 8; k++) {
+#pragma unroll
+    for (int k = 1; k < FSEG; k++) {
       const int i = base + k;
       if (!(C[i] && C[i - 1])) run = i;
       L[i] = run;
     }
   }
   __syncthreads();
-  for (int i = t; i < CH * CW; i += 256) {
+  for (int i = t; i < FTW * FTH; i += 256) {
     if (!C[i]) continue;
-    const int lx = i % CW, ly = i / CW;
+    const int lx = i % FTW, ly = i / FTW;
     const bool left = lx > 0 && C[i - 1];
-    if ((lx & 7) == 0 && left) lds_union(L, i, i - 1);
+    if ((lx % FSEG) == 0 && left) lds_union(L, i, i - 1);
     if (ly == 0) continue;
-    const bool up = C[i - CW] != 0;
-    const bool upl = lx > 0 && C[i - CW - 1];
+    const bool up = C[i - FTW] != 0;
+    const bool upl = lx > 0 && C[i - FTW - 1];
     if (up) {
-      if (!(left && upl)) lds_union(L, i, i - CW);
+      if (!(left && upl)) lds_union(L, i, i - FTW);
     } else {
-      if (upl && !left) lds_union(L, i, i - CW - 1);
-      if (lx + 1 < CW && C[i - CW + 1]) lds_union(L, i, i - CW + 1);
+      if (upl && !left) lds_union(L, i, i - FTW - 1);
+      if (lx + 1 < FTW && C[i - FTW + 1]) lds_union(L, i, i - FTW + 1);
     }
   }
   __syncthreads();
-  for (int i = t; i < CH * CW; i += 256) {
-    if (!C[i]) continue;
-    const int r = lds_find(L, i);
-    L[i] = r;
-    if (C[i] == 2) S[r] = 1;
+  for (int i = t; i < FTW * FTH; i += 256)
+    if (C[i]) L[i] = lds_find(L, i);
+  __syncthreads();
+}
+
+// vec: every frame of the batch has W % 4 == 0 and a 4-byte aligned base, so a
+// 4-pixel group is three aligned dwords. Stencils run down columns with
+// rolling register windows (one LDS read per new row instead of a 3x3 gather).
+__global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ frames, int low, int high, int vec,
+                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ rbits,
+                                                  uint16_t* __restrict__ lroot, int32_t* __restrict__ lab,
+                                                  uint8_t* __restrict__ strong, size_t plane, size_t bstride) {
+  const int f = blockIdx.z;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
+  if (x0 >= W || y0 >= H) return;
+  constexpr int BLH = FTH + 4;                     // blurred rows y0-2 .. y0+FTH+1
+  __shared__ uint8_t g[FGH * FGW];                 // gray, x0-4 .., y0-3 ..
+  __shared__ uint8_t bl[BLH * FRW];                // blurred, x0-2 .., y0-2 ..
+  __shared__ int16_t mag[FMH * FMW];               // |gx|+|gy|, x0-1 .., y0-1 ..
+  __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];  // horizontal blur, then gx | gy of the tile, then labels
+  int16_t* gx_s = gxy;
+  int16_t* gy_s = gxy + FTW * FTH;
+  __shared__ uint8_t K[FTW * FTH], S[FTW * FTH];
+  int* L = (int*)gxy;
+  const int t = threadIdx.x;
+  // gray, 4-pixel groups
+  for (int u = t; u < FGH * (FGW / 4); u += 256) {
+    const int ly = u / (FGW / 4), lg = u % (FGW / 4);
+    const int y = y0 - 3 + ly, xs = x0 - 4 + 4 * lg;
+    uint8_t* o = g + ly * FGW + 4 * lg;
+    if (y < 0 || y >= H) {
+      o[0] = o[1] = o[2] = o[3] = 0;
+    } else if (vec && xs >= 0 && xs + 3 < W) {
+      const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
+      uint32_t d[3] = {q[0], q[1], q[2]};
+      const uint8_t* b = (const uint8_t*)d;
+#pragma unroll
+      for (int k = 0; k < 4; k++) o[k] = gray_px(b + 3 * k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int x = xs + k;
+        o[k] = (x >= 0 && x < W) ? gray_px(fd.bgr + ((size_t)y * W + x) * 3) : 0;
+      }
+    }
   }
   __syncthreads();
-  for (int i = t; i < CH * CW; i += 256) {
-    if (!C[i]) continue;
+  // horizontal blur on rows y0-3 .. y0+FTH+2, columns x0-2 .. x0+FTW+1
+  // (BORDER_REFLECT_101); staged in the magnitude/gradient buffers, which are
+  // not live yet
+  uint16_t* rowb = (uint16_t*)gxy;  // FGH * FRW <= 2 * FTW * FTH
+  for (int i = t; i < FGH * FRW; i += 256) {
+    const int ly = i / FRW, lx = i % FRW;
+    const int x = x0 - 2 + lx, y = y0 - 3 + ly;
+    int v = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      const int xm = refl101(x - 1, W) - (x0 - 4), xc = x - (x0 - 4), xp = refl101(x + 1, W) - (x0 - 4);
+      const uint8_t* gr = g + ly * FGW;
+      v = 84 * gr[xm] + 89 * gr[xc] + 84 * gr[xp];
+    }
+    rowb[i] = (uint16_t)v;
+  }
+  __syncthreads();
+  // vertical blur on rows y0-2 .. y0+FTH+1
+  for (int i = t; i < BLH * FRW; i += 256) {
+    const int ly = i / FRW, lx = i % FRW;
+    const int x = x0 - 2 + lx, y = y0 - 2 + ly;
+    uint8_t v = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      const int ym = refl101(y - 1, H) - (y0 - 3), yc = y - (y0 - 3), yp = refl101(y + 1, H) - (y0 - 3);
+      const int acc = 84 * rowb[ym * FRW + lx] + 89 * rowb[yc * FRW + lx] + 84 * rowb[yp * FRW + lx];
+      const int r = (acc + (1 << 15)) >> 16;
+      v = (uint8_t)(r > 255 ? 255 : r);
+    }
+    bl[i] = v;
+  }
+  __syncthreads();
+  // Sobel (replicated border) -> L1 magnitude on x0-1 .. x0+FTW, y0-1 .. y0+FTH;
+  // the tile's own pixels also keep gx, gy for the NMS
+  for (int i = t; i < FMH * FMW; i += 256) {
+    const int ly = i / FMW, lx = i % FMW;
+    const int x = x0 - 1 + lx, y = y0 - 1 + ly;
+    int m = 0;
+    if (x >= 0 && x < W && y >= 0 && y < H) {
+      const int cl = (x > 0 ? x - 1 : 0) - (x0 - 2), cm = x - (x0 - 2), cr = (x + 1 < W ? x + 1 : W - 1) - (x0 - 2);
+      const int ra = ((y > 0 ? y - 1 : 0) - (y0 - 2)) * FRW, rb = (y - (y0 - 2)) * FRW,
+                rc = ((y + 1 < H ? y + 1 : H - 1) - (y0 - 2)) * FRW;
+      const int l0 = bl[ra + cl], m0 = bl[ra + cm], q0 = bl[ra + cr];
+      const int l1 = bl[rb + cl], q1 = bl[rb + cr];
+      const int l2 = bl[rc + cl], m2 = bl[rc + cm], q2 = bl[rc + cr];
+      const int gx = (q0 - l0) + 2 * (q1 - l1) + (q2 - l2);
+      const int gy = (l2 - l0) + 2 * (m2 - m0) + (q2 - q0);
+      m = abs(gx) + abs(gy);
+      if (ly >= 1 && ly <= FTH && lx >= 1 && lx <= FTW) {
+        const int j = (ly - 1) * FTW + lx - 1;
+        gx_s[j] = (int16_t)gx;
+        gy_s[j] = (int16_t)gy;
+      }
+    }
+    mag[i] = (int16_t)m;
+  }
+  __syncthreads();
+  // NMS -> classes (0 none, 1 weak candidate, 2 strong)
+  const int SHIFT = 15;
+  const int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
+  for (int i = t; i < FTW * FTH; i += 256) {
+    const int ly = i / FTW, lx = i % FTW;
+    const int x = x0 + lx, y = y0 + ly;
+    uint8_t c = 0;
+    if (x < W && y < H) {
+      const int cy = ly + 1, cx = lx + 1;
+      const int m = mag[cy * FMW + cx];
+      if (m > low) {
+        const int xs = gx_s[i], ys = gy_s[i];
+        const int ax = abs(xs);
+        const int ay = abs(ys) << SHIFT;
+        const int tg22x = ax * TG22;
+        bool push;
+        if (ay < tg22x) {
+          push = m > mag[cy * FMW + cx - 1] && m >= mag[cy * FMW + cx + 1];
+        } else {
+          const int tg67x = tg22x + (ax << (SHIFT + 1));
+          if (ay > tg67x) {
+            push = m > mag[(cy - 1) * FMW + cx] && m >= mag[(cy + 1) * FMW + cx];
+          } else {
+            const int s = (xs ^ ys) < 0 ? -1 : 1;
+            push = m > mag[(cy - 1) * FMW + cx - s] && m > mag[(cy + 1) * FMW + cx + s];
+          }
+        }
+        if (push) c = (m > high) ? 2 : 1;
+      }
+    }
+    K[i] = c;
+    S[i] = 0;
+  }
+  __syncthreads();
+  tile_uf(K, L, t);
+  for (int i = t; i < FTW * FTH; i += 256)
+    if (K[i] == 2) S[L[i]] = 1;
+  __syncthreads();
+  // bit planes: candidates, strong tile roots (4 words per tile row)
+  const int WW = bits::words(W);
+  const size_t ob = (size_t)f * bstride;
+  if (t < FTH * (FTW / 32)) {
+    const int ly = t / (FTW / 32), wi = t % (FTW / 32);
+    const int y = y0 + ly, w = (x0 >> 5) + wi;
+    if (y < H && w < WW) {
+      uint32_t cw = 0, rw = 0;
+      const int i0 = ly * FTW + 32 * wi;
+#pragma unroll 8
+      for (int b = 0; b < 32; b++) {
+        cw |= (uint32_t)(K[i0 + b] != 0) << b;
+        rw |= (uint32_t)(S[i0 + b] != 0) << b;
+      }
+      cbits[ob + (size_t)y * WW + w] = cw;
+      rbits[ob + (size_t)y * WW + w] = rw;
+    }
+  }
+  // per-pixel tile root (0xffff: not a candidate); sparse labels: tile roots
+  // (own index, strong flag cleared) and the tile-border candidates the seam
+  // unions start from
+  int32_t* l = lab + (size_t)f * plane;
+  uint8_t* sg = strong + (size_t)f * plane;
+  uint16_t* lr = lroot + (size_t)f * plane;
+  for (int i = t; i < FTW * FTH; i += 256) {
+    const int lx = i % FTW, ly = i / FTW;
+    const int x = x0 + lx, y = y0 + ly;
+    if (x >= W || y >= H) continue;
+    const int p = y * W + x;
+    if (!K[i]) {
+      lr[p] = 0xffff;
+      continue;
+    }
     const int r = L[i];
-    const int x = x0 + (i % CW), y = y0 + (i / CW);
-    const size_t p = (size_t)y * W + x;
-    l[p] = (y0 + r / CW) * W + x0 + (r % CW);
-    if (r == i) sg[p] = S[i];
+    lr[p] = (uint16_t)r;
+    if (r == i) {
+      l[p] = p;
+      sg[p] = 0;
+    } else if (lx == 0 || ly == 0 || lx == FTW - 1 || ly == FTH - 1) {
+      l[p] = (y0 + r / FTW) * W + x0 + (r % FTW);
+    }
   }
 }
-// one thread per seam pixel: vertical seams (x = k*CW) then horizontal (y = k*CH)
-__global__ __launch_bounds__(256) void k_hyst_seam(const uint8_t* __restrict__ cls, int32_t* lab, int W, int H,
-                                                   size_t plane) {
+
+__device__ inline bool cbit(const uint32_t* cb, int WW, int x, int y) {
+  return (cb[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
+}
+
+// one thread per seam pixel: vertical seams (x = k*FTW) then horizontal (y = k*FTH)
+__global__ __launch_bounds__(256) void k_hyst_seam(const uint32_t* __restrict__ cbits, int32_t* lab, int W, int H,
+                                                   size_t plane, size_t bstride) {
   const int f = blockIdx.y;
-  const uint8_t* c = cls + (size_t)f * plane;
+  const uint32_t* cb = cbits + (size_t)f * bstride;
+  const int WW = bits::words(W);
   int32_t* l = lab + (size_t)f * plane;
-  const int nvs = (W - 1) / CW, nhs = (H - 1) / CH;
+  const int nvs = (W - 1) / FTW, nhs = (H - 1) / FTH;
   const size_t nv = (size_t)nvs * H, n = nv + (size_t)nhs * W;
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
     int x, y;
     const bool vert = k < nv;
-    if (vert) { x = (int)(k / H + 1) * CW; y = (int)(k % H); }
-    else { const size_t h = k - nv; y = (int)(h / W + 1) * CH; x = (int)(h % W); }
+    if (vert) { x = (int)(k / H + 1) * FTW; y = (int)(k % H); }
+    else { const size_t h = k - nv; y = (int)(h / W + 1) * FTH; x = (int)(h % W); }
+    if (!cbit(cb, WW, x, y)) continue;
     const int p = y * W + x;
-    if (!c[p]) continue;
     if (vert) {
-      if (c[p - 1]) uf_union_c(l, p, p - 1);
-      if (y > 0 && c[p - W - 1]) uf_union_c(l, p, p - W - 1);
-      if (y + 1 < H && c[p + W - 1]) uf_union_c(l, p, p + W - 1);
+      if (cbit(cb, WW, x - 1, y)) uf_union_c(l, p, p - 1);
+      if (y > 0 && cbit(cb, WW, x - 1, y - 1)) uf_union_c(l, p, p - W - 1);
+      if (y + 1 < H && cbit(cb, WW, x - 1, y + 1)) uf_union_c(l, p, p + W - 1);
     } else {
-      if (c[p - W]) uf_union_c(l, p, p - W);
-      if (x > 0 && c[p - W - 1]) uf_union_c(l, p, p - W - 1);
-      if (x + 1 < W && c[p - W + 1]) uf_union_c(l, p, p - W + 1);
+      if (cbit(cb, WW, x, y - 1)) uf_union_c(l, p, p - W);
+      if (x > 0 && cbit(cb, WW, x - 1, y - 1)) uf_union_c(l, p, p - W - 1);
+      if (x + 1 < W && cbit(cb, WW, x + 1, y - 1)) uf_union_c(l, p, p - W + 1);
     }
-  }
-}
-__global__ __launch_bounds__(256) void k_hyst_strong(const uint8_t* __restrict__ cls, int32_t* lab,
-                                                     uint8_t* strong, int W, int H, size_t plane) {
-  const int f = blockIdx.y;
-  const size_t n = (size_t)W * H;
-  const uint8_t* c = cls + (size_t)f * plane;
-  int32_t* l = lab + (size_t)f * plane;
-  uint8_t* sg = strong + (size_t)f * plane;
-  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (size_t)gridDim.x * blockDim.x) {
-    if (c[p] != 2) continue;
-    const int a = l[p];  // an ancestor (the tile root, or above it after halving)
-    const int r = uf_find_c(l, a);
-    if (r != (int)p) sg[r] = 1;  // tile roots already carry their own strong flag
   }
 }
 
-// edge = candidate whose component holds a strong pixel, written as a
-// bit plane (one 32-pixel word per work-item) and optionally as bytes
-__global__ __launch_bounds__(256) void k_hyst_edge(const uint8_t* __restrict__ cls, int32_t* lab,
-                                                   const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
-                                                   uint8_t* __restrict__ edge, int W, int H, size_t plane,
-                                                   size_t bstride) {
+// strong tile roots mark their global root; one 32-pixel word per work-item
+__global__ __launch_bounds__(256) void k_hyst_mark(const uint32_t* __restrict__ rbits, int32_t* lab, uint8_t* strong,
+                                                   int W, int H, size_t plane, size_t bstride) {
   const int f = blockIdx.y;
   const int WW = bits::words(W);
   const size_t n = (size_t)WW * H;
-  const size_t o = (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  uint8_t* sg = strong + (size_t)f * plane;
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const int w = (int)(k % WW), y = (int)(k / WW);
-    const int xe = min(32, W - 32 * w);
-    const size_t p0 = o + (size_t)y * W + 32 * w;
-    uint32_t word = 0;
-    for (int b = 0; b < xe; b++) {
-      const uint32_t e = (cls[p0 + b] && strong[o + uf_find_c(lab + o, lab[p0 + b])]) ? 1u : 0u;
-      word |= e << b;
-      if (edge) edge[p0 + b] = (uint8_t)e;
+    uint32_t w = rbits[(size_t)f * bstride + k];
+    if (!w) continue;
+    const int y = (int)(k / WW), xb = (int)(k % WW) * 32;
+    while (w) {
+      const int b = __ffs(w) - 1;
+      w &= w - 1;
+      sg[uf_find_c(l, y * W + xb + b)] = 1;
     }
-    ebits[(size_t)f * bstride + k] = word;
+  }
+}
+
+// edge = candidate whose global root is marked: per tile, each tile root
+// looks up its global root once, every candidate reads its tile root's flag
+__global__ __launch_bounds__(256) void k_hyst_edge(const uint16_t* __restrict__ lroot, int32_t* lab,
+                                                   const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
+                                                   uint8_t* __restrict__ edge, int W, int H, size_t plane,
+                                                   size_t bstride) {
+  __shared__ uint16_t R[FTW * FTH];
+  __shared__ uint8_t Fl[FTW * FTH];
+  const int f = blockIdx.z;
+  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
+  if (x0 >= W || y0 >= H) return;
+  const int t = threadIdx.x;
+  const int WW = bits::words(W);
+  const size_t ob = (size_t)f * bstride;
+  const uint16_t* lr = lroot + (size_t)f * plane;
+  int32_t* l = lab + (size_t)f * plane;
+  const uint8_t* sg = strong + (size_t)f * plane;
+  for (int i = t; i < FTW * FTH; i += 256) {
+    const int x = x0 + (i % FTW), y = y0 + (i / FTW);
+    const uint16_t r = (x < W && y < H) ? lr[(size_t)y * W + x] : (uint16_t)0xffff;
+    R[i] = r;
+    if (r == i) Fl[i] = sg[uf_find_c(l, y * W + x)];
+  }
+  __syncthreads();
+  if (t < FTH * (FTW / 32)) {
+    const int ly = t / (FTW / 32), wi = t % (FTW / 32);
+    const int y = y0 + ly, w = (x0 >> 5) + wi;
+    if (y < H && w < WW) {
+      uint32_t ew = 0;
+      const int i0 = ly * FTW + 32 * wi;
+#pragma unroll 8
+      for (int b = 0; b < 32; b++) {
+        const uint16_t r = R[i0 + b];
+        ew |= (uint32_t)(r != 0xffff && Fl[r]) << b;
+      }
+      ebits[ob + (size_t)y * WW + w] = ew;
+    }
+  }
+  if (edge) {
+    uint8_t* e = edge + (size_t)f * plane;
+    for (int i = t; i < FTW * FTH; i += 256) {
+      const int x = x0 + (i % FTW), y = y0 + (i / FTW);
+      const uint16_t r = R[i];
+      if (x < W && y < H) e[(size_t)y * W + x] = (r != 0xffff && Fl[r]) ? 1 : 0;
+    }
   }
 }
 

@@ -51,6 +51,22 @@ def test_canny_bit_exact(mantis, frames):
         assert np.array_equal(got, ref), f"canny differs at {np.argwhere(got != ref)[:10]}"
 
 
+def test_canny_bit_exact_odd_sizes_and_noise(mantis):
+    """Partial 128x32 tiles, W % 4 != 0 (byte-load path), seams crossed by
+    long noisy components: smoothed noise gives dense, tangled candidates."""
+    import mantis_amd as M
+
+    rng = np.random.default_rng(77)
+    K, D = synth.intrinsics()
+    for (w, h) in [(907, 505), (1280, 720), (130, 35), (33, 7)]:
+        base = rng.integers(0, 256, (h // 4 + 2, w // 4 + 2, 3)).astype(np.float64)
+        img = np.repeat(np.repeat(base, 4, 0), 4, 1)[:h, :w]
+        img = np.clip(img + rng.normal(0, 25, img.shape), 0, 255).astype(np.uint8)
+        got = mantis.canny(M.make_image(img, K, D))
+        ref = O.canny(img)
+        assert np.array_equal(got, ref), f"{w}x{h}: canny differs at {np.argwhere(got != ref)[:10]}"
+
+
 def test_detector_binary_and_mask_bit_exact(mantis, frames):
     for fr in frames[:3]:
         det, mask = mantis.masks(_img(fr))
