@@ -164,6 +164,20 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
 mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
                                double* t, double* errs, int32_t* rpp_status);
 
+/* Dense scoring with an argmin (BASELINE config 5: 81 shifts x 4 yaws x 50
+ * perturbations = 16,200 hypotheses, SURVEY §8 d/e): the fast evaluator
+ * (evaluateHypotheses, HypothesisEvaluation.h:31-41, 71-158) on n hypotheses,
+ * then the lowest error with the first index on ties (the strict "<" the
+ * reference's best-1 choice keeps). Hypothesis k of this call has global index
+ * index_base + k. With use_comm (after mantis_comm_init) every rank passes its
+ * shard and one ncclAllGather of (err, index) pairs gives all ranks the global
+ * winner. best_idx = -1 when no hypothesis was scored. */
+mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                  int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
+                                  int64_t* best_idx);
+/* The cross-shard rule on its own (host only): pairs = nranks x (err, global index). */
+mantis_status mantis_argmin_pick(const double* pairs, int32_t nranks, double* best_err, int64_t* best_idx);
+
 /* ----------------------------------------- Gauss–Newton rig refinement (new) */
 /* One GN step over m camera observations: for camera c, corr_c normalized image points u (2)
  * matched to world points X (3). Accumulates J^T J (21 upper-tri), J^T r (6), cost (1) into

@@ -116,6 +116,9 @@ _SIGS = {
     "mantis_comm_unique_id": (C.c_int, [C.c_void_p]),
     "mantis_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     "mantis_gn_allreduce": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mantis_score_argmin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
+                                      C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_argmin_pick": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
 }
 
 
@@ -270,6 +273,29 @@ class Mantis:
                                                 err.ctypes.data, npj.ctypes.data), "score_hypotheses")
         return err, npj
 
+    def comm_init(self, rank, world, dist=None):
+        """RCCL communicator for this context: rank 0 creates the unique id and
+        torch.distributed (any backend) broadcasts it."""
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            self._chk(lib().mantis_comm_unique_id(uid), "comm_unique_id")
+        if dist is not None and world > 1:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0)
+            C.memmove(uid, box[0], 128)
+        self._chk(lib().mantis_comm_init(self.h, uid, world, rank), "comm_init")
+
+    def score_argmin(self, img, c2w, index_base=0, use_comm=False, mask=None):
+        """Dense scoring + first-minimum argmin (config 5); returns (err, global index)."""
+        c2w = np.ascontiguousarray(c2w, np.float64).reshape(-1, 12)
+        e = C.c_double()
+        i = C.c_int64()
+        mk = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self._chk(lib().mantis_score_argmin(self.h, C.byref(img), None if mk is None else mk.ctypes.data,
+                                            c2w.ctypes.data, len(c2w), index_base, int(use_comm), C.byref(e),
+                                            C.byref(i)), "score_argmin")
+        return e.value, i.value
+
     def rpp(self, img_pts, obj_pts):
         img_pts = np.ascontiguousarray(img_pts, np.float64).reshape(-1, 4, 2)
         obj_pts = np.ascontiguousarray(obj_pts, np.float64).reshape(-1, 4, 3)
@@ -318,3 +344,15 @@ class Mantis:
         ms = (C.c_float * 64)()
         n = lib().mantis_kernel_times(self.h, names, ms, 64)
         return [(names[i].decode(), ms[i]) for i in range(n)]
+
+
+def argmin_pick(pairs):
+    """The cross-shard first-minimum rule of mantis_score_argmin (host only):
+    pairs = ranks x (err, global index), index -1 for an empty shard."""
+    pairs = np.ascontiguousarray(pairs, np.float64).reshape(-1, 2)
+    e = C.c_double()
+    i = C.c_int64()
+    st = lib().mantis_argmin_pick(pairs.ctypes.data, len(pairs), C.byref(e), C.byref(i))
+    if st != MANTIS_OK:
+        raise MantisError(f"argmin_pick failed ({st})")
+    return e.value, i.value

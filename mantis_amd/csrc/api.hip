@@ -136,7 +136,11 @@ struct Ctx {
   int32_t *d_jobs0 = nullptr, *d_jobs1 = nullptr;  // RPP ObjPose job queues
   RppQueue* d_rq = nullptr;
   int rpp_blocks = 0;
-  bool vec_ok = false;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
+  bool vec_ok = false;
+  // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
+  double *d_dense_c2w = nullptr, *d_dense_err = nullptr, *d_pairs = nullptr;
+  int32_t* d_dense_np = nullptr;
+  size_t dense_cap = 0;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   FrameDebug* d_dbg = nullptr;
@@ -649,7 +653,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
-                   c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
+                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   for (void* p : c->user_allocs) (void)hipFree(p);
@@ -995,3 +999,4 @@ mantis_status mantis_set_profiling(void* ctx, int32_t on) {
 }  // extern "C"
 
 #include "gn_impl.hip"
+#include "dense_impl.hip"

@@ -1,0 +1,123 @@
+// Dense hypothesis scoring with an argmin (BASELINE config 5, SURVEY §8 d/e):
+// n hypotheses (e.g. 81 shifts x 4 yaws x 50 perturbations = 16,200) scored
+// against the 720 map.yaml landmarks with the fast evaluator
+// (evaluateHypotheses, HypothesisEvaluation.h:31-41, 71-158; one wave per
+// hypothesis, k_score_api), reduced on the device to the lowest error with
+// the first index on ties (the strict "<" of the reference's best-1 choice).
+// Sharded over ranks: every rank scores a contiguous block of the global
+// hypothesis list; one ncclAllGather of (err, global index) per rank (16 B)
+// and the same first-minimum rule give every rank the global winner. Included
+// by api.hip (shares its Ctx).
+
+namespace mk {
+
+// one block: lowest err, then lowest index
+__global__ __launch_bounds__(1024) void k_argmin(const double* __restrict__ err, int n, int64_t base,
+                                                 double* __restrict__ out2) {
+  __shared__ double se[1024];
+  __shared__ int si[1024];
+  const int t = threadIdx.x;
+  double be = DBL_MAX;
+  int bi = 0x7fffffff;
+  for (int i = t; i < n; i += 1024) {
+    const double e = err[i];
+    if (e < be) { be = e; bi = i; }  // strided scan: ascending i within a thread
+  }
+  se[t] = be;
+  si[t] = bi;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if (t < s) {
+      const double e2 = se[t + s];
+      const int i2 = si[t + s];
+      if (e2 < se[t] || (e2 == se[t] && i2 < si[t])) { se[t] = e2; si[t] = i2; }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out2[0] = se[0];
+    out2[1] = si[0] == 0x7fffffff ? -1.0 : (double)(base + si[0]);
+  }
+}
+
+}  // namespace mk
+
+extern "C" {
+
+// (err, global index) pairs of nranks shards -> the first minimum; an index
+// of -1 marks an empty shard. Host function (also used by the CPU tests).
+mantis_status mantis_argmin_pick(const double* pairs, int32_t nranks, double* best_err, int64_t* best_idx) {
+  if (!pairs || nranks <= 0 || !best_err || !best_idx) return MANTIS_ERR_ARG;
+  double be = DBL_MAX;
+  int64_t bi = -1;
+  for (int r = 0; r < nranks; r++) {
+    const double e = pairs[2 * r];
+    const int64_t i = (int64_t)pairs[2 * r + 1];
+    if (i < 0) continue;
+    if (bi < 0 || e < be || (e == be && i < bi)) { be = e; bi = i; }
+  }
+  *best_err = be;
+  *best_idx = bi;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                  int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
+                                  int64_t* best_idx) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !img || !c2w || n < 0 || !best_err || !best_idx) return MANTIS_ERR_ARG;
+  if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
+  if (use_comm && !c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
+  int W, H;
+  mantis_status st = stage_frames(c, img, 1, W, H);
+  if (st != MANTIS_OK) return st;
+  const size_t cap = (size_t)(n > 0 ? n : 1);
+  if (cap > c->dense_cap) {
+    (void)hipFree(c->d_dense_c2w);
+    (void)hipFree(c->d_dense_err);
+    (void)hipFree(c->d_dense_np);
+    c->d_dense_c2w = nullptr;
+    c->d_dense_err = nullptr;
+    c->d_dense_np = nullptr;
+    c->dense_cap = 0;
+    if (dalloc(c, &c->d_dense_c2w, 12 * cap) != MANTIS_OK || dalloc(c, &c->d_dense_err, cap) != MANTIS_OK ||
+        dalloc(c, &c->d_dense_np, cap) != MANTIS_OK)
+      return MANTIS_ERR_OOM;
+    c->dense_cap = cap;
+  }
+  if (!c->d_pairs && dalloc(c, &c->d_pairs, (size_t)2 * 64) != MANTIS_OK) return MANTIS_ERR_OOM;
+  const uint8_t* d_mask = nullptr;
+  if (mask) {
+    HIP_OK(hipMemcpyAsync(c->d_mask, mask, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+    d_mask = c->d_mask;
+  }
+  if (n > 0) HIP_OK(hipMemcpyAsync(c->d_dense_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
+  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  mark(c, "start");
+  if (n > 0) {
+    k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, c->d_dense_c2w, n, 1, c->d_dense_err,
+                                               c->d_dense_np);
+    mark(c, "score_dense");
+  }
+  k_argmin<<<1, 1024, 0, c->s>>>(c->d_dense_err, n, index_base, c->d_pairs);
+  mark(c, "argmin");
+  HIP_OK(hipGetLastError());
+  int nr = 1;
+  if (use_comm) {
+    int cnt = 0;
+    ncclCommCount((ncclComm_t)c->comm, &cnt);
+    if (cnt > 63) { c->err = "argmin exchange supports up to 63 ranks"; return MANTIS_ERR_ARG; }
+    nr = cnt;
+    ncclResult_t r = ncclAllGather(c->d_pairs, c->d_pairs + 2, 2, ncclFloat64, (ncclComm_t)c->comm, c->s);
+    if (r != ncclSuccess) { c->err = std::string("ncclAllGather: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+    mark(c, "allgather");
+  }
+  double h[2 * 64];
+  HIP_OK(hipMemcpyAsync(h, c->d_pairs + (use_comm ? 2 : 0), sizeof(double) * 2 * nr, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  finish_profile(c);
+  return mantis_argmin_pick(h, nr, best_err, best_idx);
+}
+
+}  // extern "C"

@@ -82,3 +82,58 @@ def test_camera_sharded_gn_world2():
     np.testing.assert_allclose(ca, costs1, rtol=1e-9)
     assert costs1[-1] < 1e-3 * costs1[0]
     np.testing.assert_allclose(Ta[:3, 3], T_true[:3, 3], atol=2e-3)
+
+
+def _argmin_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import mantis_amd as M
+    from mantis_amd import dense
+
+    err = _dense_errors()
+    lo, hi = dense.shard_range(len(err), rank, world)
+    local = err[lo:hi]
+    # device-side rule per shard (k_argmin): first minimum of the block
+    pair = torch.tensor([local.min(), lo + int(np.argmin(local))] if len(local) else [np.finfo(np.float64).max, -1.0],
+                        dtype=torch.float64)
+    pairs = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(pairs, pair)  # the ncclAllGather of mantis_score_argmin, 16 B per rank
+    out[rank] = M.argmin_pick(torch.stack(pairs).numpy())
+    dist.destroy_process_group()
+
+
+def _dense_errors():
+    rng = np.random.default_rng(5)
+    err = rng.integers(1000, 5000, 16200).astype(np.float64) / 7.0
+    m = err.min()
+    err[[9000, 8100, 12000]] = m - 1.0  # ties on both sides of the 2-rank boundary (8100)
+    return err
+
+
+def test_hypothesis_sharded_argmin_world2():
+    """Config 5: 16,200 hypotheses split over ranks; the exchanged (err, index)
+    pairs give every rank the global first minimum."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_argmin_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    err = _dense_errors()
+    want = (float(err.min()), int(np.argmin(err)))
+    assert want[1] == 8100
+    assert out[0] == want and out[1] == want
+
+
+def test_argmin_pick_rules():
+    import mantis_amd as M
+    from mantis_amd import dense
+
+    big = np.finfo(np.float64).max
+    assert M.argmin_pick([[3.0, 7], [3.0, 2], [4.0, 0]]) == (3.0, 2)
+    assert M.argmin_pick([[big, -1], [5.0, 11]]) == (5.0, 11)
+    assert M.argmin_pick([[big, -1], [big, -1]])[1] == -1
+    assert M.argmin_pick([[big, 4], [big, 9]]) == (big, 4)  # every hypothesis unprojectable: first index
+    spans = [dense.shard_range(16200, r, 8) for r in range(8)]
+    assert spans[0] == (0, 2025) and spans[-1] == (14175, 16200)
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(7))
+    assert dense.shard_range(5, 3, 4) == (4, 5) and dense.shard_range(2, 3, 4) == (2, 2)

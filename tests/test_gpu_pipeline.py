@@ -141,3 +141,31 @@ def test_gn_accumulate_mfma_vs_numpy(m720):
                                           acc.ctypes.data)
         assert st == 0
         np.testing.assert_allclose(acc, want, rtol=1e-12, atol=1e-14 * np.abs(want).max())
+
+
+def test_dense_config5_argmin(m720, landmark_map):
+    """Config 5 structure (shifts x yaws x perturbations) on the cleaned frame:
+    device argmin == first minimum of the per-hypothesis errors, errors
+    bit-identical to the oracle, and two shards + the exchange rule agree."""
+    import mantis_amd as M
+    from mantis_amd import dense
+
+    rng = np.random.default_rng(31)
+    R, pos = synth.random_pose(rng)
+    K, D = synth.intrinsics()
+    img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(5, 1))
+    im = M.make_image(img, K, D)
+    _, mask = m720.masks(im)
+    hyps = dense.config5_hypotheses(R, pos, np.random.default_rng(3), n_particles=3)
+    assert len(hyps) == 972
+    err, npj = m720.score(im, hyps, fast=True, mask=mask)
+    e, i = m720.score_argmin(im, hyps, 0, False, mask)
+    assert i == int(np.argmin(err)) and e == err.min()
+    cut = 500
+    a = m720.score_argmin(im, hyps[:cut], 0, False, mask)
+    b = m720.score_argmin(im, hyps[cut:], cut, False, mask)
+    assert M.argmin_pick([a, b]) == (e, i)
+    orc = O.Oracle(*landmark_map, seed=1)
+    cleaned = img * (mask[..., None] != 0)
+    oe, on = orc.score(cleaned, K, D, hyps[:200], fast=True)
+    assert np.array_equal(err[:200], oe) and np.array_equal(npj[:200], on)
