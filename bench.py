@@ -50,14 +50,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rigs", type=int, default=1024, help="rigs per step per GPU")
+    p.add_argument("--rigs", type=int, default=2048, help="rigs per step per GPU")
     p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
-    p.add_argument("--contexts", type=int, default=8,
+    p.add_argument("--contexts", type=int, default=2,
                    help="library contexts per GPU, each driven by its own host thread (one ctx per thread, "
                         "include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
     p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
-    p.add_argument("--hw-queues", type=int, default=8,
+    p.add_argument("--hw-queues", type=int, default=4,
                    help="GPU_MAX_HW_QUEUES for this process, so the contexts' streams run on separate hardware queues")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()

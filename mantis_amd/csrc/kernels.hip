@@ -80,7 +80,7 @@ constexpr int CW = 64, CH = 32;  // union-find tile
 // both) and cv::Canny's hysteresis stack walk, i.e. the 8-connected components
 // of the NMS candidates that hold a strong pixel. Two-level, with nothing
 // per-pixel written to HBM but bit planes:
-//   k_canny_uf   per 128x32 tile: BGR (vector loads) -> classes in LDS, LDS
+//   k_canny_uf   per 128x16 tile: BGR (vector loads) -> classes in LDS, LDS
 //                union-find of the candidates; writes the candidate bit plane,
 //                a bit plane of the tile roots whose component holds a strong
 //                pixel, and sparse labels (tile roots, tile-border candidates)
@@ -88,7 +88,7 @@ constexpr int CW = 64, CH = 32;  // union-find tile
 //   k_hyst_mark  strong tile roots mark their global root
 //   k_hyst_edge  per tile: the same LDS union-find again; edge = candidate
 //                whose global root is marked (bit plane, bytes on request)
-constexpr int FTW = 128, FTH = 32;            // front-end tile
+constexpr int FTW = 128, FTH = 16;            // front-end tile
 constexpr int FSEG = FTW * FTH / 256;          // pixels per thread-run in the tile union-find
 constexpr int FGW = FTW + 8, FGH = FTH + 6;    // gray tile: x0-4 .. x0+FTW+3 (4-aligned), y0-3 .. y0+FTH+2
 constexpr int FRW = FTW + 4;                   // blurred columns x0-2 .. x0+FTW+1
@@ -107,8 +107,12 @@ __device__ inline uint8_t gray_px(const uint8_t* p) {
 
 // 8-connected union-find of the candidates C (LDS bytes) of one FTW x FTH tile;
 // leaves every candidate's L at its component's minimum index (deterministic).
-__device__ inline void tile_uf(const uint8_t* C, int* L, int t) {
+// Candidates are sparse (thin NMS curves), so after the per-run init the
+// union and flatten passes walk a compacted candidate list (built with one
+// ballot and one LDS atomic per wave and step) instead of every pixel.
+__device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* count, int t) {
   constexpr int SPR = FTW / FSEG;
+  if (t == 0) *count = 0;
   {
     const int base = (t / SPR) * FTW + (t % SPR) * FSEG;
     int run = base;
@@ -121,8 +125,19 @@ __device__ inline void tile_uf(const uint8_t* C, int* L, int t) {
     }
   }
   __syncthreads();
+  const int lane = t & 63;
   for (int i = t; i < FTW * FTH; i += 256) {
-    if (!C[i]) continue;
+    const bool c = C[i] != 0;
+    const uint64_t m = __ballot(c);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, 0);
+    if (c) list[base + __popcll(m & ((1ull << lane) - 1))] = (int16_t)i;
+  }
+  __syncthreads();
+  const int n = *count;
+  for (int k = t; k < n; k += 256) {
+    const int i = list[k];
     const int lx = i % FTW, ly = i / FTW;
     const bool left = lx > 0 && C[i - 1];
     if ((lx % FSEG) == 0 && left) lds_union(L, i, i - 1);
@@ -137,39 +152,38 @@ __device__ inline void tile_uf(const uint8_t* C, int* L, int t) {
     }
   }
   __syncthreads();
-  for (int i = t; i < FTW * FTH; i += 256)
-    if (C[i]) L[i] = lds_find(L, i);
+  for (int k = t; k < n; k += 256) {
+    const int i = list[k];
+    L[i] = lds_find(L, i);
+  }
   __syncthreads();
+  return n;
 }
 
-// vec: every frame of the batch has W % 4 == 0 and a 4-byte aligned base, so a
-// 4-pixel group is three aligned dwords. Stencils run down columns with
-// rolling register windows (one LDS read per new row instead of a 3x3 gather).
-__global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ frames, int low, int high, int vec,
-                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ rbits,
-                                                  uint16_t* __restrict__ lroot, int32_t* __restrict__ lab,
-                                                  uint8_t* __restrict__ strong, size_t plane, size_t bstride) {
-  const int f = blockIdx.z;
-  const FrameDesc fd = frames[f];
-  const int W = fd.w, H = fd.h;
-  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
-  if (x0 >= W || y0 >= H) return;
-  constexpr int BLH = FTH + 4;                     // blurred rows y0-2 .. y0+FTH+1
-  __shared__ uint8_t g[FGH * FGW];                 // gray, x0-4 .., y0-3 ..
-  __shared__ uint8_t bl[BLH * FRW];                // blurred, x0-2 .., y0-2 ..
-  __shared__ int16_t mag[FMH * FMW];               // |gx|+|gy|, x0-1 .., y0-1 ..
-  __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];  // horizontal blur, then gx | gy of the tile, then labels
+// The Canny stages of one tile into K (classes). IN: the tile and its halo
+// (x0-4 .. x0+FTW+3, y0-3 .. y0+FTH+2) lie inside the image and the rows
+// allow dword loads, so the border rules (reflect/replicate/zero) drop out.
+template <bool IN>
+__device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, int y0, int low, int high, int vec,
+                                     uint8_t* g, uint8_t* bl, int16_t* mag, int16_t* gxy, uint8_t* K, uint8_t* S,
+                                     int t) {
+  constexpr int BLH = FTH + 4;
   int16_t* gx_s = gxy;
   int16_t* gy_s = gxy + FTW * FTH;
-  __shared__ uint8_t K[FTW * FTH], S[FTW * FTH];
-  int* L = (int*)gxy;
-  const int t = threadIdx.x;
   // gray, 4-pixel groups
   for (int u = t; u < FGH * (FGW / 4); u += 256) {
     const int ly = u / (FGW / 4), lg = u % (FGW / 4);
     const int y = y0 - 3 + ly, xs = x0 - 4 + 4 * lg;
     uint8_t* o = g + ly * FGW + 4 * lg;
-    if (y < 0 || y >= H) {
+    if (IN) {
+      const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
+      uint32_t d[3] = {q[0], q[1], q[2]};
+      const uint8_t* b = (const uint8_t*)d;
+      uint32_t w4 = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) w4 |= (uint32_t)gray_px(b + 3 * k) << (8 * k);
+      *(uint32_t*)o = w4;
+    } else if (y < 0 || y >= H) {
       o[0] = o[1] = o[2] = o[3] = 0;
     } else if (vec && xs >= 0 && xs + 3 < W) {
       const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
@@ -187,15 +201,15 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   }
   __syncthreads();
   // horizontal blur on rows y0-3 .. y0+FTH+2, columns x0-2 .. x0+FTW+1
-  // (BORDER_REFLECT_101); staged in the magnitude/gradient buffers, which are
-  // not live yet
+  // (BORDER_REFLECT_101); staged in the gradient buffer, not live yet
   uint16_t* rowb = (uint16_t*)gxy;  // FGH * FRW <= 2 * FTW * FTH
   for (int i = t; i < FGH * FRW; i += 256) {
     const int ly = i / FRW, lx = i % FRW;
     const int x = x0 - 2 + lx, y = y0 - 3 + ly;
     int v = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      const int xm = refl101(x - 1, W) - (x0 - 4), xc = x - (x0 - 4), xp = refl101(x + 1, W) - (x0 - 4);
+    if (IN || (x >= 0 && x < W && y >= 0 && y < H)) {
+      const int xm = (IN ? x - 1 : refl101(x - 1, W)) - (x0 - 4), xc = x - (x0 - 4),
+                xp = (IN ? x + 1 : refl101(x + 1, W)) - (x0 - 4);
       const uint8_t* gr = g + ly * FGW;
       v = 84 * gr[xm] + 89 * gr[xc] + 84 * gr[xp];
     }
@@ -207,8 +221,9 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
     const int ly = i / FRW, lx = i % FRW;
     const int x = x0 - 2 + lx, y = y0 - 2 + ly;
     uint8_t v = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      const int ym = refl101(y - 1, H) - (y0 - 3), yc = y - (y0 - 3), yp = refl101(y + 1, H) - (y0 - 3);
+    if (IN || (x >= 0 && x < W && y >= 0 && y < H)) {
+      const int ym = (IN ? y - 1 : refl101(y - 1, H)) - (y0 - 3), yc = y - (y0 - 3),
+                yp = (IN ? y + 1 : refl101(y + 1, H)) - (y0 - 3);
       const int acc = 84 * rowb[ym * FRW + lx] + 89 * rowb[yc * FRW + lx] + 84 * rowb[yp * FRW + lx];
       const int r = (acc + (1 << 15)) >> 16;
       v = (uint8_t)(r > 255 ? 255 : r);
@@ -222,10 +237,11 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
     const int ly = i / FMW, lx = i % FMW;
     const int x = x0 - 1 + lx, y = y0 - 1 + ly;
     int m = 0;
-    if (x >= 0 && x < W && y >= 0 && y < H) {
-      const int cl = (x > 0 ? x - 1 : 0) - (x0 - 2), cm = x - (x0 - 2), cr = (x + 1 < W ? x + 1 : W - 1) - (x0 - 2);
-      const int ra = ((y > 0 ? y - 1 : 0) - (y0 - 2)) * FRW, rb = (y - (y0 - 2)) * FRW,
-                rc = ((y + 1 < H ? y + 1 : H - 1) - (y0 - 2)) * FRW;
+    if (IN || (x >= 0 && x < W && y >= 0 && y < H)) {
+      const int cl = (IN || x > 0 ? x - 1 : 0) - (x0 - 2), cm = x - (x0 - 2),
+                cr = (IN || x + 1 < W ? x + 1 : W - 1) - (x0 - 2);
+      const int ra = ((IN || y > 0 ? y - 1 : 0) - (y0 - 2)) * FRW, rb = (y - (y0 - 2)) * FRW,
+                rc = ((IN || y + 1 < H ? y + 1 : H - 1) - (y0 - 2)) * FRW;
       const int l0 = bl[ra + cl], m0 = bl[ra + cm], q0 = bl[ra + cr];
       const int l1 = bl[rb + cl], q1 = bl[rb + cr];
       const int l2 = bl[rc + cl], m2 = bl[rc + cm], q2 = bl[rc + cr];
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
     const int ly = i / FTW, lx = i % FTW;
     const int x = x0 + lx, y = y0 + ly;
     uint8_t c = 0;
-    if (x < W && y < H) {
+    if (IN || (x < W && y < H)) {
       const int cy = ly + 1, cx = lx + 1;
       const int m = mag[cy * FMW + cx];
       if (m > low) {
@@ -264,8 +280,8 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
           if (ay > tg67x) {
             push = m > mag[(cy - 1) * FMW + cx] && m >= mag[(cy + 1) * FMW + cx];
           } else {
-            const int s = (xs ^ ys) < 0 ? -1 : 1;
-            push = m > mag[(cy - 1) * FMW + cx - s] && m > mag[(cy + 1) * FMW + cx + s];
+            const int sg = (xs ^ ys) < 0 ? -1 : 1;
+            push = m > mag[(cy - 1) * FMW + cx - sg] && m > mag[(cy + 1) * FMW + cx + sg];
           }
         }
         if (push) c = (m > high) ? 2 : 1;
@@ -275,9 +291,44 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
     S[i] = 0;
   }
   __syncthreads();
-  tile_uf(K, L, t);
-  for (int i = t; i < FTW * FTH; i += 256)
+}
+
+// vec: every frame of the batch has W % 4 == 0 and a 4-byte aligned base, so a
+// 4-pixel group is three aligned dwords. Stencils run down columns with
+// rolling register windows (one LDS read per new row instead of a 3x3 gather).
+__global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ frames, int low, int high, int vec,
+                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ rbits,
+                                                  uint16_t* __restrict__ lroot, int32_t* __restrict__ lab,
+                                                  uint8_t* __restrict__ strong, size_t plane, size_t bstride) {
+  const int f = blockIdx.z;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
+  if (x0 >= W || y0 >= H) return;
+  // LDS regions reused across phases (38 KB: four blocks per CU):
+  //   R1: gray (x0-4 .., y0-3 ..) -> magnitude (x0-1 .., y0-1 ..) -> candidate list
+  //   R2: blurred (x0-2 .., y0-2 ..)
+  //   R3: horizontal blur -> gx | gy of the tile -> union-find labels
+  constexpr int BLH = FTH + 4;                     // blurred rows y0-2 .. y0+FTH+1
+  constexpr int R1 = FMH * FMW * 2 > FGH * FGW ? FMH * FMW * 2 : FGH * FGW;
+  __shared__ __align__(16) uint8_t r1[R1 > FTW * FTH * 2 ? R1 : FTW * FTH * 2];
+  __shared__ uint8_t bl[BLH * FRW];
+  __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];
+  __shared__ uint8_t K[FTW * FTH], S[FTW * FTH];
+  __shared__ int ncount;
+  uint8_t* g = r1;
+  int16_t* mag = (int16_t*)r1;
+  int16_t* list = (int16_t*)r1;
+  int* L = (int*)gxy;
+  const int t = threadIdx.x;
+  const bool interior = vec && x0 >= 4 && x0 + FTW + 4 <= W && y0 >= 3 && y0 + FTH + 3 <= H;
+  if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, S, t);
+  else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, S, t);
+  const int ncand = tile_uf(K, L, list, &ncount, t);
+  for (int k = t; k < ncand; k += 256) {
+    const int i = list[k];
     if (K[i] == 2) S[L[i]] = 1;
+  }
   __syncthreads();
   // bit planes: candidates, strong tile roots (4 words per tile row)
   const int WW = bits::words(W);
@@ -304,16 +355,14 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   uint8_t* sg = strong + (size_t)f * plane;
   uint16_t* lr = lroot + (size_t)f * plane;
   for (int i = t; i < FTW * FTH; i += 256) {
+    const int x = x0 + (i % FTW), y = y0 + (i / FTW);
+    if (x < W && y < H) lr[(size_t)y * W + x] = K[i] ? (uint16_t)L[i] : (uint16_t)0xffff;
+  }
+  for (int k = t; k < ncand; k += 256) {
+    const int i = list[k];
     const int lx = i % FTW, ly = i / FTW;
-    const int x = x0 + lx, y = y0 + ly;
-    if (x >= W || y >= H) continue;
-    const int p = y * W + x;
-    if (!K[i]) {
-      lr[p] = 0xffff;
-      continue;
-    }
+    const int p = (y0 + ly) * W + x0 + lx;
     const int r = L[i];
-    lr[p] = (uint16_t)r;
     if (r == i) {
       l[p] = p;
       sg[p] = 0;
