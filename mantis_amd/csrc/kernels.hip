@@ -707,7 +707,7 @@ __global__ __launch_bounds__(256) void k_border_emit(const uint32_t* __restrict_
 // 8-neighbourhood of padded pixel (x, y) from the row-aligned bit plane
 // (LDS copy or global): three 64-bit windows starting at x - 1.
 struct BitsNB {
-  const uint32_t* b;
+  const uint32_t* __restrict__ b;
   int wpw;
   __device__ uint32_t row3(int x, int y) const {
     const uint32_t* r = b + (size_t)y * wpw + ((x - 1) >> 5);
@@ -716,6 +716,82 @@ struct BitsNB {
   }
   __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
+// The LDS copy of the plane, addressed through the dynamic shared symbol so
+// the loads are ds_read (a generic pointer compiles to flat loads, which also
+// wait on every outstanding global store of the point emitter).
+extern __shared__ uint32_t g_dyn_lds[];
+struct LdsNB {
+  int wpw;
+  __device__ uint32_t row3(int x, int y) const {
+    const int w = y * wpw + ((x - 1) >> 5);
+    const uint64_t v = ((uint64_t)g_dyn_lds[w + 1] << 32) | g_dyn_lds[w];
+    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  }
+  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
+};
+
+// direction code -> (dx + 1), (dy + 1), two bits per code (branch-free code_dx/code_dy)
+__device__ inline int fdx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }
+__device__ inline int fdy(int s) { return (int)((0xA901u >> (2 * s)) & 3u) - 1; }
+
+// Next-direction table of the border follower: for the 3x3 pattern
+// p9 = up | mid << 3 | dn << 6 (each 3 bits = columns x-1, x, x+1) and the
+// search start s (the code pointing back to the previous pixel), the first
+// set neighbour counter-clockwise after s (8: none). One LDS byte per step
+// replaces building the packed 8-neighbourhood and the rotate + ctz search.
+__device__ inline void build_next_lut(uint8_t* lut, int tid, int nthreads) {
+  for (int e = tid; e < 512 * 8; e += nthreads) {
+    const uint32_t p9 = (uint32_t)e >> 3;
+    const int s = e & 7;
+    const uint32_t m = nb8_from_rows(p9 & 7u, (p9 >> 3) & 7u, (p9 >> 6) & 7u);
+    const uint32_t r = ((m | (m << 8)) >> (s + 1)) & 0xffu;
+    lut[e] = r ? (uint8_t)((s + 1 + __builtin_ctz(r)) & 7) : (uint8_t)8;
+  }
+}
+
+// trace_border_nb_em (mk_contour.h, host-checked against the oracle) driven
+// by the table: the same point sequence.
+template <class NB, class EM>
+__device__ int trace_border_lut(const NB& nb, const uint8_t* lut, int sx, int sy, bool hole, EM& em,
+                                int* steps_max = nullptr) {
+  int steps = 0;
+  int x = sx, y = sy;
+  uint32_t m = nb(x, y);
+  const int s_end0 = hole ? 0 : 4;
+  int s = s_end0;
+  do {
+    s = (s - 1) & 7;
+  } while (!((m >> s) & 1u) && s != s_end0);
+  int px = sx - 1, py = sy - 1;
+  if (s == s_end0) {
+    em(px, py);
+    return 1;
+  }
+  const int x1 = sx + fdx(s), y1 = sy + fdy(s);
+  int n = 0;
+  int prev_s = s ^ 4;
+  uint32_t p9 = nb.row3(x, y - 1) | (nb.row3(x, y) << 3) | (nb.row3(x, y + 1) << 6);
+  for (;;) {
+    s = lut[(p9 << 3) | s];
+    if (s != prev_s) {
+      em(px, py);
+      n++;
+      prev_s = s;
+    }
+    const int dx = fdx(s), dy = fdy(s);
+    px += dx;
+    py += dy;
+    const int x4 = x + dx, y4 = y + dy;
+    if (x4 == sx && y4 == sy && x == x1 && y == y1) break;
+    x = x4;
+    y = y4;
+    p9 = nb.row3(x, y - 1) | (nb.row3(x, y) << 3) | (nb.row3(x, y + 1) << 6);
+    s = (s + 4) & 7;
+    steps++;
+  }
+  if (steps_max) atomicMax(steps_max, steps);
+  return n;
+}
 
 // Single-pass border tracing: points go to 64-point chunks handed out by an
 // LDS bump allocator; a wave per chunk then compacts them by border.
@@ -737,9 +813,7 @@ struct ChunkEmit {
       owner[c] = border;
       ordv[c] = nch++;
     }
-    int32_t* d = chunks + 2 * ((size_t)cur * kChunk + k);
-    d[0] = px;
-    d[1] = py;
+    *(int2*)(chunks + 2 * ((size_t)cur * kChunk + k)) = make_int2(px, py);  // one 8-byte store
     k++;
   }
 };
@@ -863,7 +937,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
                                                          const FrameDesc* __restrict__ frames, int Wp, int Hp,
                                                          size_t plane, int border_cap, double eps, double search_mult,
                                                          int use_lds) {
-  extern __shared__ uint32_t lds_bits[];
+  uint32_t* lds_bits = g_dyn_lds;
   __shared__ int32_t scan[1024];
   __shared__ RawQuad raw[kMaxQuads];
   __shared__ int32_t nraw, total, nkeep;
@@ -875,6 +949,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   __shared__ double qside[kMaxQuads];
   __shared__ int32_t nchunk, nlong;
   __shared__ int32_t longs[kMaxLong];
+  __shared__ uint8_t next_lut[512 * 8];
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
   const uint32_t* B = dbits + (size_t)f * dstride;
@@ -904,7 +979,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   if (use_lds) {
     for (size_t w = tid; w < nwords; w += blockDim.x) lds_bits[w] = B[w];
   }
-  const BitsNB nbh{use_lds ? (const uint32_t*)lds_bits : B, wpw};
+  build_next_lut(next_lut, tid, blockDim.x);
   if (tid == 0) { nraw = 0; total = 0; nchunk = 0; nlong = 0; }
   __syncthreads();
   MK_TICK(0);
@@ -916,7 +991,10 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   for (int i = tid; i < nb; i += blockDim.x) {
     const Border b = bs[i];
     ChunkEmit em{chunks, owner, ordv, &nchunk, max_chunks, i, -1, 0, 0, false};
-    cnt[i] = trace_border_nb_em(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em);
+    cnt[i] = use_lds ? trace_border_lut(LdsNB{wpw}, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em,
+                                        &st[f].trace_steps_max)
+                     : trace_border_lut(BitsNB{B, wpw}, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em,
+                                        &st[f].trace_steps_max);
     if (em.ovf) atomicOr(&st[f].overflow, 2);
   }
   __syncthreads();

@@ -35,6 +35,7 @@ m.process(imgs, rigs=rigs)
 print("stages", [(k, round(v, 3)) for k, v in m.kernel_times()], flush=True)
 C = np.array([m.frame_counters(i) for i in range(n)])
 names = ["borders", "points", "raw_q", "quads", "gen", "hyps", "pf", "goff", "ovf", "cand"]
+print("longest walk steps mean", C[:, 18].mean(), "max", C[:, 18].max())
 for j, nm in enumerate(names):
     print(f"{nm:8s} mean {C[:, j].mean():10.1f} max {C[:, j].max()}")
 T = C[:, 10:16].astype(float) * 0.01  # us
