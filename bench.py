@@ -187,8 +187,10 @@ def main():
     avg = {k: v / a.steps for k, v in stage_ms.items()}
     # algorithmic bytes (HBM-bound stages) or FP64 flops (VALU-bound stages) per launch
     work = {
-        "canny_nms": ("hbm", frames_step * (3 * W * H + W * H)),
-        "hysteresis": ("hbm", frames_step * (2 * W * H)),
+        # BGR read once; candidate and strong-root bit planes written
+        "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
+        # candidate bits read, edge bits written
+        "hysteresis": ("hbm", frames_step * (W * H // 4)),
         "det_morph": ("hbm", frames_step * (2 * W * H // 8)),
         "mask_morph": ("hbm", frames_step * (2 * W * H // 8 * 15 + W * H)),
         "components": ("hbm", frames_step * (5 * (W + 2) * (H + 2))),
@@ -211,8 +213,8 @@ def main():
             if os.path.exists(pmc):
                 try:
                     tj = json.load(open(pmc))
-                    if tj.get("stage") == stage and tj.get("frames_per_launch") == frames_step:
-                        traffic = tj.get("bytes_per_launch")
+                    if tj.get("stage") == stage and tj.get("hbm_bytes_per_frame"):
+                        traffic = int(tj["hbm_bytes_per_frame"] * frames_step)
                 except Exception:
                     traffic = None
             return {"bound": "hbm", "kernel": stage, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
