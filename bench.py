@@ -194,6 +194,7 @@ def main():
         "det_morph": ("hbm", frames_step * (2 * W * H // 8)),
         "mask_morph": ("hbm", frames_step * (2 * W * H // 8 * 15 + W * H)),
         "components": ("hbm", frames_step * (5 * (W + 2) * (H + 2))),
+        "border_trace": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
         "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),

@@ -161,7 +161,6 @@ struct Ctx {
   std::vector<float> last_ms;
   std::vector<std::string> last_names;
   std::vector<void*> user_allocs;
-  int lds_bytes = 0;
   // multi-GPU
   void* comm = nullptr;  // ncclComm_t
   double* d_gn28 = nullptr;
@@ -292,12 +291,13 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   k_border_emit<<<dim3(64, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_borders, c->d_st, Wp,
                                                P, kMaxBorders);
   mark(c, "components");
-  const size_t bits_bytes = (size_t)dbits_wpw(Wp) * Hp * 4;
-  const int use_lds = bits_bytes <= (size_t)c->lds_bytes ? 1 : 0;
-  k_frame_contours<<<n, 1024, use_lds ? bits_bytes : 0, c->s>>>(
-      c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->pool_cap, c->d_quads,
-      c->d_dbg, c->d_frames, Wp, Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon, c->cfg.search_radius_multiplier,
-      use_lds);
+  k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
+                                                c->d_scratch, c->pool_cap, Wp, kMaxBorders);
+  mark(c, "border_trace");
+  k_frame_contours<<<n, 1024, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
+                                         c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
+                                         Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon,
+                                         c->cfg.search_radius_multiplier);
   mark(c, "contours_quads");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
@@ -623,18 +623,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     mantis_destroy(c);
     return st;
   }
-  // the contour kernel keeps the padded frame as a bitmap in LDS when it fits
-  int max_lds = 0;
-  (void)hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, cfg.device);
-  hipFuncAttributes fa{};
-  int static_lds = 32 * 1024;
-  if (hipFuncGetAttributes(&fa, (const void*)k_frame_contours) == hipSuccess) static_lds = (int)fa.sharedSizeBytes;
-  c->lds_bytes = std::max(0, std::min(max_lds, 160 * 1024) - static_lds);
   if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
-  if (c->lds_bytes > 0 &&
-      hipFuncSetAttribute((const void*)k_frame_contours, hipFuncAttributeMaxDynamicSharedMemorySize, c->lds_bytes) !=
-          hipSuccess)
-    c->lds_bytes = 0;  // contour tracing then reads the bit plane from global memory
   (void)hipGetLastError();
   if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess) {
     g_create_err = "hipMemset failed";

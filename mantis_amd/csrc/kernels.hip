@@ -716,20 +716,6 @@ struct BitsNB {
   }
   __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
-// The LDS copy of the plane, addressed through the dynamic shared symbol so
-// the loads are ds_read (a generic pointer compiles to flat loads, which also
-// wait on every outstanding global store of the point emitter).
-extern __shared__ uint32_t g_dyn_lds[];
-struct LdsNB {
-  int wpw;
-  __device__ uint32_t row3(int x, int y) const {
-    const int w = y * wpw + ((x - 1) >> 5);
-    const uint64_t v = ((uint64_t)g_dyn_lds[w + 1] << 32) | g_dyn_lds[w];
-    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
-  }
-  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
-};
-
 // direction code -> (dx + 1), (dy + 1), two bits per code (branch-free code_dx/code_dy)
 __device__ inline int fdx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }
 __device__ inline int fdy(int s) { return (int)((0xA901u >> (2 * s)) & 3u) - 1; }
@@ -928,6 +914,40 @@ struct RawQuad {
   int32_t parent, hole, key;
 };
 
+// 1. follow every border once (one work-item per border, many frames in
+// flight): points into 64-point chunks handed out by a per-frame counter.
+// The walks are serial chains of dependent neighbourhood reads; running them
+// in small blocks with the bit plane in L2 (instead of one 1024-thread block
+// per frame holding the plane in LDS) lets every CU interleave the walks of
+// many frames.
+__global__ __launch_bounds__(256) void k_trace_borders(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                       const Border* __restrict__ borders, FrameState* st,
+                                                       int32_t* __restrict__ counts, int32_t* __restrict__ scratch,
+                                                       int pool_cap, int Wp, int border_cap) {
+  __shared__ uint8_t next_lut[512 * 8];
+  const int f = blockIdx.y;
+  build_next_lut(next_lut, threadIdx.x, blockDim.x);
+  __syncthreads();
+  int nb = st[f].n_borders;
+  if (nb > border_cap) nb = border_cap;
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  const int wpw = dbits_wpw(Wp);
+  const Border* bs = borders + (size_t)f * border_cap;
+  int32_t* cnt = counts + (size_t)f * border_cap;
+  int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
+  const int max_chunks = pool_cap / kChunk;
+  int32_t* chunks = sc;                        // [0, 2 pool_cap)
+  int32_t* owner = sc + 2 * (size_t)pool_cap;  // [2 pool_cap, + max_chunks)
+  int32_t* ordv = owner + max_chunks;
+  const BitsNB nbh{B, wpw};
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+    const Border b = bs[i];
+    ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, i, -1, 0, 0, false};
+    cnt[i] = trace_border_lut(nbh, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em, &st[f].trace_steps_max);
+    if (em.ovf) atomicOr(&st[f].overflow, 2);
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restrict__ dbits, size_t dstride,
                                                          const Border* __restrict__ borders,
                                                          FrameState* st, int32_t* __restrict__ counts,
@@ -935,9 +955,7 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
                                                          int32_t* __restrict__ scratch, int pool_cap,
                                                          QuadRec* __restrict__ quads, FrameDebug* dbg,
                                                          const FrameDesc* __restrict__ frames, int Wp, int Hp,
-                                                         size_t plane, int border_cap, double eps, double search_mult,
-                                                         int use_lds) {
-  uint32_t* lds_bits = g_dyn_lds;
+                                                         size_t plane, int border_cap, double eps, double search_mult) {
   __shared__ int32_t scan[1024];
   __shared__ RawQuad raw[kMaxQuads];
   __shared__ int32_t nraw, total, nkeep;
@@ -949,7 +967,6 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   __shared__ double qside[kMaxQuads];
   __shared__ int32_t nchunk, nlong;
   __shared__ int32_t longs[kMaxLong];
-  __shared__ uint8_t next_lut[512 * 8];
   const int f = blockIdx.x;
   const int tid = threadIdx.x;
   const uint32_t* B = dbits + (size_t)f * dstride;
@@ -975,29 +992,13 @@ __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restr
   const uint64_t t0 = wall_clock64();
 #define MK_TICK(k) \
   if (tid == 0) st[f].ticks[k] = (int32_t)(wall_clock64() - t0);
-  const size_t nwords = (size_t)wpw * Hp;
-  if (use_lds) {
-    for (size_t w = tid; w < nwords; w += blockDim.x) lds_bits[w] = B[w];
-  }
-  build_next_lut(next_lut, tid, blockDim.x);
-  if (tid == 0) { nraw = 0; total = 0; nchunk = 0; nlong = 0; }
+  if (tid == 0) { nraw = 0; total = 0; nlong = 0; nchunk = st[f].n_chunks; }
   __syncthreads();
   MK_TICK(0);
-  // 1. follow every border once, points into chunks
   const int max_chunks = pool_cap / kChunk;
-  int32_t* chunks = sc;                              // [0, 2 pool_cap)
+  int32_t* chunks = sc;                              // [0, 2 pool_cap), filled by k_trace_borders
   int32_t* owner = sc + 2 * (size_t)pool_cap;        // [2 pool_cap, + max_chunks)
   int32_t* ordv = owner + max_chunks;
-  for (int i = tid; i < nb; i += blockDim.x) {
-    const Border b = bs[i];
-    ChunkEmit em{chunks, owner, ordv, &nchunk, max_chunks, i, -1, 0, 0, false};
-    cnt[i] = use_lds ? trace_border_lut(LdsNB{wpw}, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em,
-                                        &st[f].trace_steps_max)
-                     : trace_border_lut(BitsNB{B, wpw}, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em,
-                                        &st[f].trace_steps_max);
-    if (em.ovf) atomicOr(&st[f].overflow, 2);
-  }
-  __syncthreads();
   MK_TICK(1);
   // 2. exclusive scan of the point counts, blockDim at a time
   for (int base = 0; base < nb; base += blockDim.x) {

@@ -103,7 +103,8 @@ struct FrameState {
   int32_t n_cand;        // component-root candidates (tile roots) of the contour CCL
   int32_t ticks[6];      // k_frame_contours phase ends, 10 ns wall-clock ticks from its start
   int32_t rpp_iters[2];  // AbsKernel calls of the first / candidate ObjPoses (k_objpose_q)
-  int32_t trace_steps_max;  // longest border walk (steps) of k_frame_contours
+  int32_t trace_steps_max;  // longest border walk (steps) of k_trace_borders
+  int32_t n_chunks;         // 64-point chunks handed out by k_trace_borders
 };
 
 }  // namespace mk
