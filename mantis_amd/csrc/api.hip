@@ -140,7 +140,12 @@ struct Ctx {
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
   double *d_dense_c2w = nullptr, *d_dense_err = nullptr, *d_pairs = nullptr;
   int32_t* d_dense_np = nullptr;
-  size_t dense_cap = 0;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
+  size_t dense_cap = 0;
+  // rig GN (cfg.gn_enable): per-camera inv(T_base_cam), per-rig poses, correspondences
+  GnCam* d_gncam = nullptr;
+  RigGnIO* d_rigio = nullptr;
+  double* d_gnobs = nullptr;
+  int gn_rigs = 0, gn_cpr = 0;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   FrameDebug* d_dbg = nullptr;
@@ -642,7 +647,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
-                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
+                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   for (void* p : c->user_allocs) (void)hipFree(p);
@@ -719,6 +724,10 @@ mantis_status mantis_rng_set(void* ctx, uint64_t state) {
   return MANTIS_OK;
 }
 
+namespace {
+mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, mantis_result* out);  // gn_impl.hip
+}
+
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
                                    mantis_result* out, mantis_cam_result* cam_out) {
   Ctx* c = (Ctx*)ctx;
@@ -737,6 +746,10 @@ mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t 
       for (int i = 0; i < cams_per_rig; i++) k += c->h_st[r * cams_per_rig + i].reaches_pf;
       out[r].rng_state_after = c->h_states[k];
     }
+  }
+  if (out && c->cfg.gn_enable) {
+    st = run_rig_gn(c, cams, n_rigs, cams_per_rig, out);
+    if (st != MANTIS_OK) return st;
   }
   if (cam_out) std::memcpy(cam_out, c->h_res, sizeof(mantis_cam_result) * n);
   for (int f = 0; f < n; f++)

@@ -16,10 +16,6 @@ namespace mk {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-struct GnCam {
-  double R_cb[9];  // inv(T_b_c) rotation
-  double t_cb[3];
-};
 
 // value of M[row][col] (col 0..5 = J, 6 = r, else 0) for one residual row
 __device__ inline double gn_entry(const double* Rwb_t, const double* twb, const GnCam* cams, const double* obs,
@@ -84,23 +80,280 @@ __global__ __launch_bounds__(256) void k_gn_accum(const double* __restrict__ Twb
   }
 }
 
-}  // namespace mk
-
-namespace {
-void rodrigues(const double* w, double* R) {
-  double th = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-  double a, b;
-  if (th < 1e-12) { a = 1.0; b = 0.5; }
-  else { a = std::sin(th) / th; b = (1 - std::cos(th)) / (th * th); }
-  double K2[9];
+// (J^T J + lambda I) delta = -J^T r from the 28 accumulators by Cholesky, then
+// T_w_b <- T_w_b Exp(delta) (right perturbation: translation delta[0..2],
+// rotation vector delta[3..5] through Rodrigues). Returns false when the
+// normal matrix is not positive definite (too few observations). Shared by
+// mantis_gn_solve (host) and the batched rig kernel.
+MK_HD bool gn_solve6(const double* acc28, double lambda, double* T_w_b, double* delta6) {
+  double A[6][6], b[6];
+  int n = 0;
+  for (int i = 0; i < 6; i++)
+    for (int j = i; j < 6; j++) { A[i][j] = A[j][i] = acc28[n++]; }
+  for (int i = 0; i < 6; i++) { A[i][i] += lambda; b[i] = -acc28[21 + i]; }
+  double L[6][6];
+  for (int i = 0; i < 6; i++)
+    for (int j = 0; j < 6; j++) L[i][j] = 0;
+  for (int i = 0; i < 6; i++)
+    for (int j = 0; j <= i; j++) {
+      double s = A[i][j];
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+      if (i == j) {
+        if (!(s > 0)) return false;
+        L[i][i] = sqrt(s);
+      } else {
+        L[i][j] = s / L[j][j];
+      }
+    }
+  double y[6], x[6];
+  for (int i = 0; i < 6; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s / L[i][i];
+  }
+  for (int i = 5; i >= 0; i--) {
+    double s = y[i];
+    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
+    x[i] = s / L[i][i];
+  }
+  if (delta6)
+    for (int i = 0; i < 6; i++) delta6[i] = x[i];
+  const double* w = x + 3;
+  const double th = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  const double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+  double a, bb;
+  if (th < 1e-12) { a = 1.0; bb = 0.5; }
+  else { a = sin(th) / th; bb = (1 - cos(th)) / (th * th); }
+  double dR[9];
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {
       double s = 0;
       for (int k = 0; k < 3; k++) s += K[i * 3 + k] * K[k * 3 + j];
-      K2[i * 3 + j] = s;
+      dR[i * 3 + j] = (i == j ? 1.0 : 0.0) + a * K[i * 3 + j] + bb * s;
     }
-  for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * K[i] + b * K2[i];
+  const double D[16] = {dR[0], dR[1], dR[2], x[0], dR[3], dR[4], dR[5], x[1], dR[6], dR[7], dR[8], x[2], 0, 0, 0, 1};
+  double r[16];
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 4; j++) {
+      double s = 0;
+      for (int k = 0; k < 4; k++) s += T_w_b[i * 4 + k] * D[k * 4 + j];
+      r[i * 4 + j] = s;
+    }
+  for (int i = 0; i < 16; i++) T_w_b[i] = r[i];
+  return true;
+}
+
+// ------------------------------------------------ batched rig GN (pipeline)
+// cfg.gn_enable: after the per-camera pipeline and the rig fusion, one block
+// per rig refines the base pose over all its cameras' quads. A detected quad
+// is the dark inside of one grid cell, so its centre is the cell centre; in
+// the undistorted normalized image (a perspective view) the centre of the
+// square is exactly where the quad's diagonals cross. Each quad gives that
+// point, back-projected with the fused pose onto the floor and snapped to the
+// nearest cell centre (-1.28 + 0.32 k of the map's grid; accepted within
+// 0.1 m). The list is compacted in item order (block scan), so the MFMA sums
+// are reproducible.
+
+__device__ inline bool gn_quad_obs(const FrameDesc& fd, const QuadRec& q, const double* Rwc, const double* Cw,
+                                   double half, double spacing, double* o) {
+  double u[4], v[4];
+  for (int k = 0; k < 4; k++) undistort(fd.cam, (double)q.c[2 * k], (double)q.c[2 * k + 1], &u[k], &v[k]);
+  // diagonals p0-p2 and p1-p3: p0 + a (p2 - p0) = p1 + b (p3 - p1)
+  const double d1x = u[2] - u[0], d1y = v[2] - v[0], d2x = u[3] - u[1], d2y = v[3] - v[1];
+  const double den = d1x * d2y - d1y * d2x;
+  if (fabs(den) < 1e-12) return false;
+  const double a = ((u[1] - u[0]) * d2y - (v[1] - v[0]) * d2x) / den;
+  if (!(a > 0 && a < 1)) return false;
+  const double uc = u[0] + a * d1x, vc = v[0] + a * d1y;
+  const double dw[3] = {Rwc[0] * uc + Rwc[1] * vc + Rwc[2], Rwc[3] * uc + Rwc[4] * vc + Rwc[5],
+                        Rwc[6] * uc + Rwc[7] * vc + Rwc[8]};
+  if (!(dw[2] < -1e-9)) return false;
+  const double tt = -Cw[2] / dw[2];
+  if (!(tt > 0)) return false;
+  const double X = Cw[0] + tt * dw[0], Y = Cw[1] + tt * dw[1];
+  const double c0 = -half + 0.5 * spacing;  // first cell centre
+  const double kx = rint((X - c0) / spacing), ky = rint((Y - c0) / spacing);
+  const double lim = rint(2 * half / spacing) - 1;
+  if (kx < 0 || ky < 0 || kx > lim || ky > lim) return false;
+  const double gx = c0 + spacing * kx, gy = c0 + spacing * ky;
+  if (fabs(X - gx) > 0.1 || fabs(Y - gy) > 0.1) return false;
+  o[1] = uc;
+  o[2] = vc;
+  o[3] = gx;
+  o[4] = gy;
+  o[5] = 0.0;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_rig_gn(const FrameDesc* __restrict__ frames, const FrameState* __restrict__ st,
+                                                const QuadRec* __restrict__ quads, const GnCam* __restrict__ gncam,
+                                                RigGnIO* io, int cams_per_rig, double* __restrict__ obs_all,
+                                                int obs_cap, int iterations, double half, double spacing) {
+  __shared__ double red[4][16][16];
+  __shared__ double T[16], acc28[28];
+  __shared__ int32_t scan[256];
+  __shared__ int32_t nobs_s, done;
+  const int rig = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  RigGnIO& R = io[rig];
+  if (!R.valid) return;
+  if (t < 16) T[t] = R.Twb[t];
+  __syncthreads();
+  const GnCam* cams = gncam + (size_t)rig * cams_per_rig;
+  double* obs = obs_all + (size_t)rig * obs_cap * 6;
+  const int n_items = cams_per_rig * kMaxQuads;
+  // pass 1: count accepted corners of this thread's item range; pass 2: write them in item order
+  for (int pass = 0; pass < 2; pass++) {
+    int cntv = 0, pos = 0;
+    if (pass == 1) pos = scan[t];
+    const int per = (n_items + 255) / 256;
+    for (int it = t * per; it < n_items && it < (t + 1) * per; it++) {
+      const int c = it / kMaxQuads, q = it % kMaxQuads;
+      const int f = rig * cams_per_rig + c;
+      if (q >= st[f].n_quads) continue;
+      // camera pose in the world from the base pose: T_wc = T_wb inv(T_cb)
+      double Rbc[9], tbc[3], Rwc[9], Cw[3];
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rbc[3 * a + b] = cams[c].R_cb[3 * b + a];
+      for (int a = 0; a < 3; a++) tbc[a] = -(Rbc[3 * a] * cams[c].t_cb[0] + Rbc[3 * a + 1] * cams[c].t_cb[1] +
+                                              Rbc[3 * a + 2] * cams[c].t_cb[2]);
+      for (int a = 0; a < 3; a++) {
+        for (int b = 0; b < 3; b++)
+          Rwc[3 * a + b] = T[4 * a] * Rbc[b] + T[4 * a + 1] * Rbc[3 + b] + T[4 * a + 2] * Rbc[6 + b];
+        Cw[a] = T[4 * a] * tbc[0] + T[4 * a + 1] * tbc[1] + T[4 * a + 2] * tbc[2] + T[4 * a + 3];
+      }
+      double o[6];
+      if (!gn_quad_obs(frames[f], quads[(size_t)f * kMaxQuads + q], Rwc, Cw, half, spacing, o)) continue;
+      if (pass == 1 && pos < obs_cap) {
+        o[0] = (double)c;
+        for (int e = 0; e < 6; e++) obs[(size_t)pos * 6 + e] = o[e];
+      }
+      pos++;
+      cntv++;
+    }
+    if (pass == 0) {
+      scan[t] = cntv;
+      __syncthreads();
+      if (t == 0) {
+        int run = 0;
+        for (int i = 0; i < 256; i++) { const int v = scan[i]; scan[i] = run; run += v; }
+        nobs_s = run < obs_cap ? run : obs_cap;
+        done = 0;
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const int n_obs = nobs_s;
+  if (n_obs < 6) {
+    if (t == 0) { R.n_obs = n_obs; R.iterations = 0; }
+    return;
+  }
+  int it_done = 0;
+  for (int it = 0; it < iterations; it++) {
+    double Rt[9], tw[3];
+    for (int a = 0; a < 3; a++) {
+      for (int b = 0; b < 3; b++) Rt[3 * a + b] = T[4 * b + a];
+      tw[a] = T[4 * a + 3];
+    }
+    v4d acc = {0, 0, 0, 0};
+    const int rows = 2 * n_obs;
+    const int kk = lane >> 4, m = lane & 15;
+    for (int base = wave * 4; base < rows; base += 16) {
+      const double v = gn_entry(Rt, tw, cams, obs, n_obs, base + kk, m);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+    }
+    for (int r = 0; r < 4; r++) red[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
+    __syncthreads();
+    if (t == 0) {
+      int n = 0;
+      for (int a = 0; a < 6; a++)
+        for (int b = a; b < 6; b++) acc28[n++] = red[0][a][b] + red[1][a][b] + red[2][a][b] + red[3][a][b];
+      for (int a = 0; a < 6; a++) acc28[21 + a] = red[0][a][6] + red[1][a][6] + red[2][a][6] + red[3][a][6];
+      acc28[27] = red[0][6][6] + red[1][6][6] + red[2][6][6] + red[3][6][6];
+      if (it == 0) R.cost0 = acc28[27];
+      R.cost = acc28[27];
+      double Tn[16], d6[6];
+      for (int e = 0; e < 16; e++) Tn[e] = T[e];
+      if (!gn_solve6(acc28, 1e-9, Tn, d6)) {
+        done = 1;
+      } else {
+        for (int e = 0; e < 16; e++) T[e] = Tn[e];
+        double dn = 0;
+        for (int e = 0; e < 6; e++) dn += d6[e] * d6[e];
+        if (dn < 1e-24) done = 1;
+      }
+    }
+    __syncthreads();
+    it_done = it + 1;
+    if (done) break;
+  }
+  if (t < 16) R.Twb[t] = T[t];
+  if (t == 0) { R.iterations = it_done; R.n_obs = n_obs; }
+}
+
+}  // namespace mk
+
+namespace {
+// cfg.gn_enable: refine every rig's fused base pose on the device (k_rig_gn);
+// per-camera inv(T_base_cam) and the fused poses go up, refined poses come back.
+mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, mantis_result* out) {
+  const int n = n_rigs * cpr;
+  const int obs_cap = cpr * kMaxQuads;
+  std::vector<GnCam> gc(n);
+  std::vector<RigGnIO> io(n_rigs);
+  for (int f = 0; f < n; f++) {
+    double inv[16];
+    mat4_inv_rigid(cams[f].T_base_cam, inv);
+    for (int a = 0; a < 3; a++) {
+      for (int b = 0; b < 3; b++) gc[f].R_cb[3 * a + b] = inv[4 * a + b];
+      gc[f].t_cb[a] = inv[4 * a + 3];
+    }
+  }
+  for (int r = 0; r < n_rigs; r++) {
+    std::memset(&io[r], 0, sizeof(RigGnIO));
+    const double* q = out[r].orientation_xyzw;
+    if (q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3] > 0.5) {
+      quat_to_mat4(q, out[r].position, io[r].Twb);
+      io[r].valid = 1;
+    }
+  }
+  if (c->gn_rigs < n_rigs || c->gn_cpr != cpr) {
+    (void)hipFree(c->d_gncam);
+    (void)hipFree(c->d_rigio);
+    (void)hipFree(c->d_gnobs);
+    c->d_gncam = nullptr;
+    c->d_rigio = nullptr;
+    c->d_gnobs = nullptr;
+    c->gn_rigs = 0;
+    if (dalloc(c, &c->d_gncam, (size_t)n) || dalloc(c, &c->d_rigio, (size_t)n_rigs) ||
+        dalloc(c, &c->d_gnobs, (size_t)n_rigs * obs_cap * 6))
+      return MANTIS_ERR_OOM;
+    c->gn_rigs = n_rigs;
+    c->gn_cpr = cpr;
+  }
+  HIP_OK(hipMemcpyAsync(c->d_gncam, gc.data(), sizeof(GnCam) * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(c->d_rigio, io.data(), sizeof(RigGnIO) * n_rigs, hipMemcpyHostToDevice, c->s));
+  const double spacing = c->cfg.grid_spacing, half = 4.5 * spacing;  // lines at -1.44 + 0.32 k, k = 0..9
+  k_rig_gn<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cpr, c->d_gnobs,
+                                      obs_cap, c->cfg.gn_iterations, half, spacing);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(io.data(), c->d_rigio, sizeof(RigGnIO) * n_rigs, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (int r = 0; r < n_rigs; r++) {
+    if (!io[r].valid || io[r].iterations <= 0) continue;
+    double R[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) R[i * 3 + j] = io[r].Twb[i * 4 + j];
+    mk::Quat q = basis_to_quat(R);
+    out[r].orientation_xyzw[0] = q.x;
+    out[r].orientation_xyzw[1] = q.y;
+    out[r].orientation_xyzw[2] = q.z;
+    out[r].orientation_xyzw[3] = q.w;
+    for (int i = 0; i < 3; i++) out[r].position[i] = io[r].Twb[i * 4 + 3];
+    out[r].gn_iterations = io[r].iterations;
+    out[r].gn_cost = io[r].cost;
+  }
+  return MANTIS_OK;
 }
 }  // namespace
 
@@ -143,42 +396,7 @@ mantis_status mantis_gn_accumulate(void* ctx, const double* T_w_b, const double*
 
 mantis_status mantis_gn_solve(const double* acc28, double lambda, double* T_w_b, double* delta6) {
   if (!acc28 || !T_w_b) return MANTIS_ERR_ARG;
-  double A[6][6], b[6];
-  int n = 0;
-  for (int i = 0; i < 6; i++)
-    for (int j = i; j < 6; j++) { A[i][j] = A[j][i] = acc28[n++]; }
-  for (int i = 0; i < 6; i++) { A[i][i] += lambda; b[i] = -acc28[21 + i]; }
-  // Cholesky A = L L^T
-  double L[6][6] = {{0}};
-  for (int i = 0; i < 6; i++)
-    for (int j = 0; j <= i; j++) {
-      double s = A[i][j];
-      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
-      if (i == j) {
-        if (!(s > 0)) return MANTIS_ERR_ARG;  // not positive definite (too few observations)
-        L[i][i] = std::sqrt(s);
-      } else {
-        L[i][j] = s / L[j][j];
-      }
-    }
-  double y[6], x[6];
-  for (int i = 0; i < 6; i++) {
-    double s = b[i];
-    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
-    y[i] = s / L[i][i];
-  }
-  for (int i = 5; i >= 0; i--) {
-    double s = y[i];
-    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
-    x[i] = s / L[i][i];
-  }
-  if (delta6)
-    for (int i = 0; i < 6; i++) delta6[i] = x[i];
-  double dR[9];
-  rodrigues(x + 3, dR);
-  double D[16] = {dR[0], dR[1], dR[2], x[0], dR[3], dR[4], dR[5], x[1], dR[6], dR[7], dR[8], x[2], 0, 0, 0, 1};
-  mat4_mul(T_w_b, D, T_w_b);
-  return MANTIS_OK;
+  return mk::gn_solve6(acc28, lambda, T_w_b, delta6) ? MANTIS_OK : MANTIS_ERR_ARG;
 }
 
 mantis_status mantis_comm_unique_id(void* id128) {

@@ -107,4 +107,16 @@ struct FrameState {
   int32_t n_chunks;         // 64-point chunks handed out by k_trace_borders
 };
 
+// Gauss–Newton rig refinement (gn_impl.hip): one camera's inv(T_base_cam)
+struct GnCam {
+  double R_cb[9];
+  double t_cb[3];
+};
+// per-rig input/output of k_rig_gn: base pose in, refined pose out
+struct RigGnIO {
+  double Twb[16];
+  double cost0, cost;
+  int32_t valid, iterations, n_obs, pad;
+};
+
 }  // namespace mk
