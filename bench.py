@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--hw-queues", type=int, default=4,
                    help="GPU_MAX_HW_QUEUES for this process, so the contexts' streams run on separate hardware queues")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--gn", type=int, default=1,
+                   help="joint rig Gauss-Newton after the per-camera pipeline (SURVEY §8 d config 3); 0 = reference-parity only")
+    p.add_argument("--gn-iterations", type=int, default=8)
     return p.parse_args()
 
 
@@ -91,7 +94,8 @@ def main():
     rigs_ctx = a.rigs // nctx
     ctxs = []
     for _ in range(nctx):
-        mc = M.Mantis(M.default_config(device=local, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H))
+        mc = M.Mantis(M.default_config(device=local, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H,
+                                       gn_enable=a.gn, gn_iterations=a.gn_iterations))
         mc.set_map(white, red, green)
         ctxs.append(mc)
     m = ctxs[0]
@@ -198,6 +202,8 @@ def main():
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
         "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),
+        # rig GN: per iteration and rig, MFMA over 2 * (~4 x 75) residual rows of [J | r] (7 x 7 outer products)
+
         "score_pf_yaw": ("fp64", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
@@ -271,7 +277,8 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic fisheye grid frames rendered in HBM (SURVEY §8d scene), map.yaml landmarks",
-            "config": {"workload": "config3: 4-cam 1280x720 rig, shared map, full mantis3 path per camera",
+            "config": {"workload": "config3: 4-cam 1280x720 rig, shared map, full mantis3 path per camera"
+                                    + (" + joint rig Gauss-Newton" if a.gn else ""),
                        "rigs_per_step_per_gpu": a.rigs, "cams_per_rig": CAMS, "frames_per_step_per_gpu": n_frames,
                        "contexts_per_gpu": nctx,
                        "resolution": [W, H], "landmarks": LANDMARKS, "parallelism": f"rig-data-parallel x{world}"},

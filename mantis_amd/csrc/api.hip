@@ -369,11 +369,13 @@ mantis_status run_score(Ctx* c, int n) {
   return MANTIS_OK;
 }
 
-void finish_profile(Ctx* c) {
+void finish_profile(Ctx* c, bool append = false) {
   if (!c->prof || c->ev_names.empty()) return;
   (void)hipEventSynchronize(c->ev[c->ev_names.size() - 1]);
-  c->last_names.clear();
-  c->last_ms.clear();
+  if (!append) {
+    c->last_names.clear();
+    c->last_ms.clear();
+  }
   for (size_t i = 1; i < c->ev_names.size(); i++) {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev[i - 1], c->ev[i]);

@@ -334,11 +334,14 @@ mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, 
   HIP_OK(hipMemcpyAsync(c->d_gncam, gc.data(), sizeof(GnCam) * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(c->d_rigio, io.data(), sizeof(RigGnIO) * n_rigs, hipMemcpyHostToDevice, c->s));
   const double spacing = c->cfg.grid_spacing, half = 4.5 * spacing;  // lines at -1.44 + 0.32 k, k = 0..9
+  mark(c, "start");
   k_rig_gn<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cpr, c->d_gnobs,
                                       obs_cap, c->cfg.gn_iterations, half, spacing);
+  mark(c, "rig_gn");
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(io.data(), c->d_rigio, sizeof(RigGnIO) * n_rigs, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
+  finish_profile(c, true);
   for (int r = 0; r < n_rigs; r++) {
     if (!io[r].valid || io[r].iterations <= 0) continue;
     double R[9];
