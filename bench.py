@@ -202,7 +202,6 @@ def main():
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
         "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),
-        # rig GN: per iteration and rig, MFMA over 2 * (~4 x 75) residual rows of [J | r] (7 x 7 outer products)
 
         "score_pf_yaw": ("fp64", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
