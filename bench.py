@@ -50,9 +50,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rigs", type=int, default=2048, help="rigs per step per GPU")
+    p.add_argument("--rigs", type=int, default=3072, help="rigs per step per GPU")
     p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
-    p.add_argument("--contexts", type=int, default=2,
+    p.add_argument("--contexts", type=int, default=3,
                    help="library contexts per GPU, each driven by its own host thread (one ctx per thread, "
                         "include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--gn", type=int, default=1,
                    help="joint rig Gauss-Newton after the per-camera pipeline (SURVEY §8 d config 3); 0 = reference-parity only")
     p.add_argument("--gn-iterations", type=int, default=8)
+    p.add_argument("--max-contour-points", type=int, default=98304,
+                   help="per-frame contour point pool (720p frames use ~22k, max seen 28k; overflow is reported as an error)")
     return p.parse_args()
 
 
@@ -95,7 +97,8 @@ def main():
     ctxs = []
     for _ in range(nctx):
         mc = M.Mantis(M.default_config(device=local, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H,
-                                       gn_enable=a.gn, gn_iterations=a.gn_iterations))
+                                       gn_enable=a.gn, gn_iterations=a.gn_iterations,
+                                       max_contour_points=a.max_contour_points))
         mc.set_map(white, red, green)
         ctxs.append(mc)
     m = ctxs[0]
