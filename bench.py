@@ -36,8 +36,11 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # FP64 operations of one ObjPose iteration (one AbsKernel: the 3x3 accumulations,
 # OpenCV's one-sided Jacobi SVD, R, t and the error), counted by
-# tools/rpp_flops.cpp on the host build of mk_rpp.h (+,-,*,/,sqrt,hypot = 1 each)
-FLOPS_PER_OBJPOSE_ITER = 4282
+# tools/rpp_flops.cpp on the host build of mk_rpp.h (+,-,*,/,sqrt,hypot = 1 each).
+# 1704 = what the device executes: the Jacobi noise-phase fast-forward
+# (mk_rpp.h jacobi_noise_ff) skips the ~19 sweeps that only shrink the
+# rank-deficient row (the full reference sweep count is 4282 per iteration).
+FLOPS_PER_OBJPOSE_ITER = 1704
 W, H = 1280, 720
 CAMS = 4
 LANDMARKS = 720

@@ -492,11 +492,58 @@ MK_HD bool jacobi_pair(double* At, double* W, double* Vt, int i, int j) {
   return true;
 }
 
+// Noise-phase fast-forward for a 3x3 At whose third components are exactly
+// zero (a planar model makes M = sum p q^T have a zero row, so its three
+// columns span a plane). Once rows 0 and 1 are converged and row 2 is a small
+// residual, every later rotation is (0,2) or (1,2) in the c == 1 branch and
+// only shrinks row 2, by ~1e-14 per sweep, until its squares underflow; the
+// loop then ends (or hits max_iter) with W[2] == 0, and the regeneration after
+// the loop overwrites row 2 from rows 0 and 1 alone. This test certifies, with
+// a factor-2 margin on every bound, that none of those rotations can move a
+// bit of rows 0/1, of W[0]/W[1] or of Vt, and that row 2 underflows before
+// max_iter; then the remaining sweeps are skipped with row 2 set to zero.
+// Bounds (n0 = max |row 2 component|, Bn <= |row b|, s = rotation sine):
+//   |s| <= 3 n0 / Bn;  c == 1 branch needs n0 <= 2^-64 Bn;
+//   row b unchanged:   |s row2[k]| <= 4.5 n0^2 / Bn < 2^-55 min|row b[k]|;
+//   Vt unchanged:      |s Vt[k]|   <= 3 n0 / Bn    < 2^-55 min|Vt[k]|;
+//   underflow:         n0 (1e-14)^(sweeps left - 1) < 1e-163.
+// The only bits it does not reproduce are signs of the zero third
+// components of rows 0/1 (+-0 + +-0), which no later result depends on.
+MK_HD bool jacobi_noise_ff(const double* At, const double* W, const double* Vt, int sweeps_left) {
+  if (!(At[2] == 0 && At[5] == 0 && At[8] == 0)) return false;
+  const double eps = DBL_EPSILON * 10;
+  double p = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) p += At[k] * At[3 + k];  // jacobi_pair's skip test of (0, 1)
+  if (!(fabs(p) <= eps * sqrt(W[0] * W[1]))) return false;
+  const double n0 = fmax(fabs(At[6]), fabs(At[7]));
+  const double bmin = fmin(fmin(fabs(At[0]), fabs(At[1])), fmin(fabs(At[3]), fabs(At[4])));
+  const double Bn = fmin(fmax(fabs(At[0]), fabs(At[1])), fmax(fabs(At[3]), fabs(At[4])));
+  double vmin = fabs(Vt[0]);
+#pragma unroll
+  for (int k = 1; k < 9; k++) vmin = fmin(vmin, fabs(Vt[k]));
+  if (!(n0 <= 0x1p-64 * Bn)) return false;
+  if (!(4.5 * n0 * n0 < 0x1p-55 * bmin * Bn)) return false;
+  if (!(3.0 * n0 < 0x1p-55 * vmin * Bn)) return false;
+  double bound = 1.5 * n0;
+#pragma unroll 1
+  for (int r = 1; r < sweeps_left && bound >= 1e-163; r++) bound *= 1e-14;
+  return bound < 1e-163;
+}
+
+#ifndef MK_JACOBI_FF
+#define MK_JACOBI_FF 1
+#endif
+
 template <int M, int N>
 MK_HD void jacobi_sweeps(double* At, double* W, double* Vt) {
   const int max_iter = M > 30 ? M : 30;
 #pragma unroll 1
   for (int iter = 0; iter < max_iter; iter++) {
+    if (MK_JACOBI_FF && M == 3 && N == 3 && Vt && iter > 0 && jacobi_noise_ff(At, W, Vt, max_iter - iter)) {
+      At[6] = At[7] = At[8] = 0;
+      break;
+    }
     bool changed = false;
 #pragma unroll
     for (int i = 0; i < N - 1; i++)

@@ -39,6 +39,8 @@ inline bool operator>=(CD a, CD b) { return a.v >= b.v; }
 inline bool operator==(CD a, CD b) { return a.v == b.v; }
 inline bool operator!=(CD a, CD b) { return a.v != b.v; }
 inline CD fabs(CD a) { return CD(std::fabs(a.v)); }
+inline CD fmax(CD a, CD b) { return CD(std::fmax(a.v, b.v)); }
+inline CD fmin(CD a, CD b) { return CD(std::fmin(a.v, b.v)); }
 inline CD sqrt(CD a) { ++g_ops; return CD(std::sqrt(a.v)); }
 inline CD hypot(CD a, CD b) { ++g_ops; return CD(std::hypot(a.v, b.v)); }
 inline CD atan2(CD a, CD b) { ++g_ops; return CD(std::atan2(a.v, b.v)); }
