@@ -8,6 +8,10 @@
 #include <cstring>
 #include <vector>
 
+// runtime switch for the Jacobi noise-phase fast-forward (mk_rpp.h), so the
+// tests can compare it bit for bit against the full sweep sequence
+static int g_jacobi_ff = 1;
+#define MK_JACOBI_FF g_jacobi_ff
 #include "mk_bits.h"
 #include "mk_contour.h"
 #include "mk_math.h"
@@ -15,6 +19,8 @@
 #include "mk_sort.h"
 
 extern "C" {
+
+void hc_set_jacobi_ff(int on) { g_jacobi_ff = on; }
 
 int hc_rpp(const double* model, const double* iprts, double* R, double* t, double* errs, int* err_code) {
   mk::rpp::Result r = mk::rpp::solve(model, iprts);

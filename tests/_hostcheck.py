@@ -50,6 +50,11 @@ def rpp(model, iprts):
     return st, R.reshape(3, 3), t, e, code.value
 
 
+def set_jacobi_ff(on):
+    """Toggle the Jacobi noise-phase fast-forward of the host build (mk_rpp.h)."""
+    lib().hc_set_jacobi_ff(C.c_int(1 if on else 0))
+
+
 def rpoly(coef):
     coef = np.ascontiguousarray(coef, np.float64)
     deg = len(coef) - 1
