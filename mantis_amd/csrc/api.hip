@@ -124,7 +124,8 @@ struct Ctx {
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
   size_t bstride = 0;                                           // words per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
-  CcCand* d_cand = nullptr;
+  int32_t* d_rowb = nullptr;  // run CCL row bases, rstride per frame
+  size_t rstride = 0;
   size_t dstride = 0;
   FrameDesc* d_frames = nullptr;
   Border* d_borders = nullptr;
@@ -285,16 +286,15 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
 mantis_status run_contours(Ctx* c, int n, int W, int H) {
   const size_t P = c->plane;
   const int Wp = W + 2, Hp = H + 2;
-  const size_t np = (size_t)Wp * Hp;
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
-  dim3 gp(blocks_for(np), n);
-  dim3 gtile((Wp + CW - 1) / CW, (Hp + CH - 1) / CH, n);
-  k_cc_tile<<<gtile, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_st, Wp, Hp, P);
-  const size_t nseam = (size_t)((Wp - 1) / CW) * Hp + (size_t)((Hp - 1) / CH) * Wp;
-  if (nseam) k_cc_seam<<<dim3((unsigned)((nseam + 255) / 256), n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, Wp, Hp,
-                                                                         P);
-  k_border_emit<<<dim3(64, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_lab, c->d_cand, c->d_borders, c->d_st, Wp,
-                                               P, kMaxBorders);
+  dim3 grow((Hp + 3) / 4, n);
+  uint16_t* rx = c->d_lroot;  // free after hysteresis: run starts (u16, one run per pixel at most)
+  k_run_count<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, Wp, Hp);
+  k_run_scan<<<n, 1024, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
+  k_run_emit<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
+  k_run_union<<<dim3((Hp + 2) / 4, n), 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
+  k_run_border<<<grow, 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, c->d_borders, c->d_st, Wp, Hp,
+                                       kMaxBorders);
   mark(c, "components");
   k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
                                                 c->d_scratch, c->pool_cap, Wp, kMaxBorders);
@@ -596,7 +596,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
-  chk(dalloc(c, &c->d_cand, (size_t)F * kMaxCand));
+  c->rstride = (size_t)c->Hmax + 3;
+  chk(dalloc(c, &c->d_rowb, (size_t)F * c->rstride));
   chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_frames, (size_t)F));
@@ -647,7 +648,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_cand,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)

@@ -5,7 +5,8 @@
 //   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_seam / _mark / _edge
 //   dilate x2 / erode x1             QuadDetection.h:213-214         k_bh / k_bv / k_pack_det (bit planes)
 //   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_bm0 + k_bh / k_bv
-//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_cc_tile / _seam / _flatten + k_border_emit
+//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_run_count/_scan/_emit/_union/_border (run CCL)
+//                                                                    + k_trace_borders
 //                                                                    + k_frame_contours
 //   approxPolyDP / Quadrilateral /
 //   removeDuplicateQuads / undistort QuadDetection.h:13-171, 219-228, 289-298   k_frame_contours
@@ -71,7 +72,6 @@ __device__ inline void lds_union(int* L, int a, int b) {
     a = old;
   }
 }
-constexpr int CW = 64, CH = 32;  // union-find tile
 
 // ============================================== Canny: classes + hysteresis
 // cvtColor(BGR2GRAY) -> GaussianBlur 3x3 (x256 kernel [84,89,84], OpenCV <= 3.3,
@@ -548,156 +548,178 @@ __global__ __launch_bounds__(256) void k_pack_det(const uint32_t* __restrict__ s
 }
 
 // ==================================================== contour components
-// On the zero-ringed detector binary (Wp x Hp): foreground 8-connected,
-// background 4-connected; the ring makes the outside background component 0.
-// Labels end as the component's minimum padded index. Three launches:
-//   k_cc_tile  64x32 tiles, union-find in LDS (row runs first, redundant
-//              unions skipped), each pixel labelled with its tile-local root
-//   k_cc_seam  unions across tile seams only, global union-find
-//   k_cc_flatten  every pixel -> its global root
-__global__ __launch_bounds__(256) void k_cc_tile(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                 int32_t* __restrict__ lab, CcCand* __restrict__ cand,
-                                                 FrameState* st, int Wp, int Hp, size_t plane) {
-  __shared__ uint8_t C[CH * CW];  // 0 background, 1 foreground, 2 outside the image
-  __shared__ int L[CH * CW];
-  const int f = blockIdx.z;
-  const int x0 = blockIdx.x * CW, y0 = blockIdx.y * CH;
-  const uint32_t* B = dbits + (size_t)f * dstride;
-  const int wpw = dbits_wpw(Wp);
-  int32_t* l = lab + (size_t)f * plane;
-  const int t = threadIdx.x;
-  for (int i = t; i < CH * CW; i += 256) {
-    const int x = x0 + (i % CW), y = y0 + (i / CW);
-    C[i] = (x < Wp && y < Hp) ? (uint8_t)dbit(B, wpw, x, y) : 2;
+// Run-length CCL of the zero-ringed detector binary (Wp x Hp, row-aligned bit
+// plane): foreground 8-connected, background 4-connected. A row's runs
+// (maximal spans of equal bits) alternate bg / fg from the ring pixel at
+// x = 0 and are numbered in raster order, so the smallest run of a component
+// starts at its raster-first pixel: where the sequential Suzuki–Abe scan
+// (findContours, QuadDetection.h:216) discovers the component's border. A
+// 720p detector frame has ~36k runs against 0.93 M pixels. Run starts go to
+// a u16 plane (x), labels to an int32 plane (run ids, frame-local), both
+// sized for one run per pixel, so nothing can overflow.
+//   k_run_count   wave per row: transitions -> runs of the row
+//   k_run_scan    block per frame: row bases (exclusive scan)
+//   k_run_emit    wave per row: run starts, labels = own ids
+//   k_run_union   wave per row: unions with the overlapping same-colour runs
+//                 of the row above (fg: [a-1, b+1], bg: [a, b])
+//   k_run_border  wave per row: component roots -> border records
+// Transitions of word w of a padded row: bit b set where x = 32 w + b starts a run.
+__device__ inline uint32_t run_starts(const uint32_t* row, int w) {
+  const uint32_t cur = row[w], prv = w > 0 ? row[w - 1] : 0u;
+  return cur ^ ((cur << 1) | (prv >> 31));
+}
+__device__ inline int wave_sum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ inline int wave_incl_scan(int v, int lane) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
   }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_run_count(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                   int32_t* __restrict__ rowb, size_t rstride, int Wp, int Hp) {
+  const int f = blockIdx.y;
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= Hp) return;
+  const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+  const int nw = (Wp + 31) / 32;
+  int c = 0;
+  for (int w = lane; w < nw; w += 64) c += __popc(run_starts(row, w));
+  c = wave_sum(c);
+  if (lane == 0) rowb[(size_t)f * rstride + y] = c + 1;
+}
+
+__global__ __launch_bounds__(1024) void k_run_scan(int32_t* __restrict__ rowb, size_t rstride, FrameState* st,
+                                                   int Hp) {
+  __shared__ int32_t wsum[16];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  int32_t* r = rowb + (size_t)f * rstride;
+  const int per = (Hp + 1023) / 1024, y0 = t * per;
+  int loc = 0;
+  for (int k = 0; k < per; k++)
+    if (y0 + k < Hp) loc += r[y0 + k];
+  const int inc = wave_incl_scan(loc, lane);
+  if (lane == 63) wsum[wave] = inc;
   __syncthreads();
-  {  // row runs: 8 threads per row, 8 pixels each, sequential within the segment
-    const int base = (t >> 3) * CW + (t & 7) * 8;
-    int run = base;
-    L[base] = base;
-    for (int k = 1; k < 8; k++) {
-      const int i = base + k;
-      if (C[i] != C[i - 1]) run = i;
-      L[i] = run;
+  int off = 0;
+  for (int k = 0; k < wave; k++) off += wsum[k];
+  int acc = off + inc - loc;
+  for (int k = 0; k < per; k++)
+    if (y0 + k < Hp) {
+      const int v = r[y0 + k];
+      r[y0 + k] = acc;
+      acc += v;
     }
-  }
-  __syncthreads();
-  for (int i = t; i < CH * CW; i += 256) {
-    const int c = C[i];
-    if (c == 2) continue;
-    const int lx = i % CW, ly = i / CW;
-    const int left = lx > 0 ? C[i - 1] : 3;
-    if ((lx & 7) == 0 && left == c) lds_union(L, i, i - 1);
-    if (ly == 0) continue;
-    const int up = C[i - CW];
-    const int upl = lx > 0 ? C[i - CW - 1] : 3;
-    if (c == 1) {
-      if (up == 1) {
-        if (!(left == 1 && upl == 1)) lds_union(L, i, i - CW);
-      } else {
-        if (upl == 1 && left != 1) lds_union(L, i, i - CW - 1);
-        if (lx + 1 < CW && C[i - CW + 1] == 1) lds_union(L, i, i - CW + 1);
-      }
-    } else if (up == 0) {
-      if (!(left == 0 && upl == 0)) lds_union(L, i, i - CW);
-    }
-  }
-  __syncthreads();
-  // labels only where later kernels look: tile-boundary pixels (seam unions,
-  // hole parents left of a tile) and the tile roots themselves
-  for (int i = t; i < CH * CW; i += 256) {
-    if (C[i] == 2) continue;
-    const int lx = i % CW, ly = i / CW;
-    const int r = lds_find(L, i);
-    const int x = x0 + lx, y = y0 + ly;
-    const int gp = y * Wp + x;
-    const int gr = (y0 + r / CW) * Wp + x0 + (r % CW);
-    const bool edge = lx == 0 || ly == 0 || lx == CW - 1 || ly == CH - 1 || x == Wp - 1 || y == Hp - 1;
-    if (edge || r == i) l[gp] = gr;
-    if (r == i) {
-      int hint = -1;
-      if (C[i] == 0 && x > 0) {
-        if (lx > 0) {
-          const int rl = lds_find(L, i - 1);
-          hint = (y0 + rl / CW) * Wp + x0 + (rl % CW);
-        } else {
-          hint = gp - 1;  // right column of the left tile: labelled
-        }
-      }
-      const int k = atomicAdd(&st[f].n_cand, 1);
-      if (k < kMaxCand) cand[(size_t)f * kMaxCand + k] = CcCand{gp, hint};
-      else atomicOr(&st[f].overflow, 1);
-    }
+  if (t == 1023) {
+    r[Hp] = acc;
+    st[f].n_runs = acc;
   }
 }
 
-// one thread per seam pixel: vertical seams (x = k*CW) then horizontal (y = k*CH)
-__global__ __launch_bounds__(256) void k_cc_seam(const uint32_t* __restrict__ dbits, size_t dstride, int32_t* lab,
-                                                 int Wp, int Hp, size_t plane) {
+__global__ __launch_bounds__(256) void k_run_emit(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                  const int32_t* __restrict__ rowb, size_t rstride,
+                                                  uint16_t* __restrict__ rx, int32_t* __restrict__ lab, size_t plane,
+                                                  int Wp, int Hp) {
   const int f = blockIdx.y;
-  const uint32_t* B = dbits + (size_t)f * dstride;
-  const int wpw = dbits_wpw(Wp);
-  int32_t* l = lab + (size_t)f * plane;
-  const int nvs = (Wp - 1) / CW, nhs = (Hp - 1) / CH;
-  const size_t nv = (size_t)nvs * Hp, n = nv + (size_t)nhs * Wp;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    int x, y;
-    const bool vert = k < nv;
-    if (vert) { x = (int)(k / Hp + 1) * CW; y = (int)(k % Hp); }
-    else { const size_t h = k - nv; y = (int)(h / Wp + 1) * CH; x = (int)(h % Wp); }
-    const int p = y * Wp + x;
-    const uint32_t c = dbit(B, wpw, x, y);
-    // A 4-neighbour pair across the seam whose predecessor along the seam
-    // was the same kind of pair between the same two sets is implied: skip.
-    // Foreground diagonals are only needed when the 4-neighbour across the
-    // seam is background (otherwise they join through it).
-    if (vert) {
-      const uint32_t cl = dbit(B, wpw, x - 1, y);
-      if (cl == c) {
-        const bool implied = y > 0 && dbit(B, wpw, x, y - 1) == c && dbit(B, wpw, x - 1, y - 1) == c &&
-                             l[p] == l[p - Wp] && l[p - 1] == l[p - 1 - Wp];
-        if (!implied) uf_union_c(l, p, p - 1);
-      } else if (c) {
-        if (y > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
-        if (y + 1 < Hp && dbit(B, wpw, x - 1, y + 1)) uf_union_c(l, p, p + Wp - 1);
-      }
-    } else {
-      const uint32_t cu = dbit(B, wpw, x, y - 1);
-      if (cu == c) {
-        const bool implied = x > 0 && dbit(B, wpw, x - 1, y) == c && dbit(B, wpw, x - 1, y - 1) == c &&
-                             l[p] == l[p - 1] && l[p - Wp] == l[p - Wp - 1];
-        if (!implied) uf_union_c(l, p, p - Wp);
-      } else if (c) {
-        if (x > 0 && dbit(B, wpw, x - 1, y - 1)) uf_union_c(l, p, p - Wp - 1);
-        if (x + 1 < Wp && dbit(B, wpw, x + 1, y - 1)) uf_union_c(l, p, p - Wp + 1);
-      }
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= Hp) return;
+  const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+  uint16_t* X = rx + (size_t)f * plane;
+  int32_t* L = lab + (size_t)f * plane;
+  const int nw = (Wp + 31) / 32;
+  int base = rowb[(size_t)f * rstride + y];
+  if (lane == 0) { X[base] = 0; L[base] = base; }
+  base++;
+  for (int w0 = 0; w0 < nw; w0 += 64) {
+    const int w = w0 + lane;
+    uint32_t T = w < nw ? run_starts(row, w) : 0u;
+    const int c = __popc(T);
+    const int inc = wave_incl_scan(c, lane);
+    int o = base + inc - c;
+    while (T) {
+      const int b = __ffs(T) - 1;
+      T &= T - 1;
+      X[o] = (uint16_t)(32 * w + b);
+      L[o] = o;
+      o++;
     }
+    base += __shfl(inc, 63);
   }
 }
-// One border per fg component (outer, at its root) and per enclosed bg
-// component (hole, left of its root); the root of a component is the tile
-// root that stayed a root through the seam unions.
-__global__ __launch_bounds__(256) void k_border_emit(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                     int32_t* lab, const CcCand* __restrict__ cand,
-                                                     Border* __restrict__ borders, FrameState* st, int Wp,
-                                                     size_t plane, int cap) {
+
+// largest k in [0, n) with x[k] <= v (x[0] == 0 <= v)
+__device__ inline int run_at(const uint16_t* x, int n, int v) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int)x[mid] <= v) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_run_union(const int32_t* __restrict__ rowb, size_t rstride,
+                                                   const uint16_t* __restrict__ rx, int32_t* lab, size_t plane,
+                                                   int Wp, int Hp) {
   const int f = blockIdx.y;
-  const int nc = min(st[f].n_cand, kMaxCand);
-  const uint32_t* B = dbits + (size_t)f * dstride;
-  const int wpw = dbits_wpw(Wp);
-  int32_t* l = lab + (size_t)f * plane;
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nc; k += gridDim.x * blockDim.x) {
-    const CcCand cd = cand[(size_t)f * kMaxCand + k];
-    const int p = cd.root;
-    if (l[p] != p) continue;
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6) + 1, lane = threadIdx.x & 63;
+  if (y >= Hp) return;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
+  int32_t* L = lab + (size_t)f * plane;
+  const int bp = r[y - 1], np = r[y] - bp, by = r[y], ny = r[y + 1] - by;
+  const uint16_t* Xp = X + bp;
+  for (int j = lane; j < ny; j += 64) {
+    const int fg = j & 1;
+    const int a = X[by + j], b = (j + 1 < ny ? (int)X[by + j + 1] : Wp) - 1;
+    const int lo = a - fg, hi = b + fg;
+    for (int k = run_at(Xp, np, lo); k < np && (int)Xp[k] <= hi; k++)
+      if ((k & 1) == fg) uf_union_c(L, by + j, bp + k);
+  }
+}
+
+// row of run id: largest y with rowb[y] <= id
+__device__ inline int run_at_row(const int32_t* rowb, int Hp, int id) {
+  int lo = 0, hi = Hp - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rowb[mid] <= id) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ rowb, size_t rstride,
+                                                    const uint16_t* __restrict__ rx, int32_t* lab, size_t plane,
+                                                    Border* __restrict__ borders, FrameState* st, int Wp, int Hp,
+                                                    int cap) {
+  const int f = blockIdx.y;
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= Hp) return;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
+  int32_t* L = lab + (size_t)f * plane;
+  const int by = r[y], ny = r[y + 1] - by;
+  for (int j = lane; j < ny; j += 64) {
+    const int id = by + j;
+    if (id == 0 || uf_find_c(L, id) != id) continue;  // run 0 (ring) is the outside background
+    const int key = y * Wp + X[id];
     Border b;
-    if (dbit(B, wpw, p % Wp, p / Wp)) {
-      b.key = p; b.start = p; b.hole = 0; b.parent = p;
+    b.key = key;
+    if (j & 1) {
+      b.start = key; b.hole = 0; b.parent = key;
     } else {
-      if (p == 0) continue;
-      b.key = p; b.start = p - 1; b.hole = 1; b.parent = uf_find_c(l, cd.hint);
+      // hole: the run on its left is foreground; its component's root run
+      // starts at the key of the enclosing outer border
+      const int pr = uf_find_c(L, id - 1);
+      const int py = run_at_row(r, Hp, pr);
+      b.start = key - 1; b.hole = 1; b.parent = py * Wp + X[pr];
     }
-    int idx = atomicAdd(&st[f].n_borders, 1);
+    const int idx = atomicAdd(&st[f].n_borders, 1);
     if (idx < cap) borders[(size_t)f * cap + idx] = b;
     else atomicOr(&st[f].overflow, 1);
   }

@@ -85,10 +85,6 @@ struct FrameDebug {
 };
 
 // Per-frame counters / status written by the kernels.
-struct CcCand {  // a tile-local component root and, for background, where its parent is found
-  int32_t root, hint;
-};
-constexpr int kMaxCand = 65536;
 
 struct FrameState {
   int32_t n_borders;
@@ -100,7 +96,7 @@ struct FrameState {
   int32_t reaches_pf;
   int32_t gauss_offset;  // index into the gaussian stream (floats)
   int32_t overflow;      // bit 0 borders, 1 points, 2 quads, 3 hyps
-  int32_t n_cand;        // component-root candidates (tile roots) of the contour CCL
+  int32_t n_runs;        // runs of the detector binary (contour CCL, k_run_*)
   int32_t ticks[6];      // k_frame_contours phase ends, 10 ns wall-clock ticks from its start
   int32_t rpp_iters[2];  // AbsKernel calls of the first / candidate ObjPoses (k_objpose_q)
   int32_t trace_steps_max;  // longest border walk (steps) of k_trace_borders

@@ -88,6 +88,29 @@ def test_quads_bit_exact(mantis, frames, landmark_map):
         assert np.array_equal(got, ref)
 
 
+def test_contour_borders_match_find_contours(mantis, frames):
+    """Run-length CCL + parallel border following against findContours(CCOMP,
+    SIMPLE) on the detector binary: same number of borders (outer + hole) and
+    the same total of chain points, on real frames and on blob-noise images
+    with many nested components and holes."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(99)
+    imgs = [fr[0] for fr in frames[:2]]
+    for (w, h, cell) in [(1280, 720, 6), (640, 480, 3), (333, 97, 2)]:
+        base = (rng.random((h // cell + 2, w // cell + 2)) > 0.5).astype(np.float64) * 200 + 20
+        img = np.repeat(np.repeat(base, cell, 0), cell, 1)[:h, :w]
+        imgs.append(np.repeat(img[:, :, None], 3, 2).astype(np.uint8))
+    for img in imgs:
+        mantis.detect_quads(M.make_image(img, K, D))
+        cnt = mantis.frame_counters(0)
+        cs, holes = O.find_contours(O.detector_binary(O.canny(img)), 2)
+        assert cnt[8] == 0, f"overflow flags {cnt[8]}"
+        assert cnt[0] == len(cs), f"borders {cnt[0]} vs findContours {len(cs)}"
+        assert cnt[1] == sum(len(c) for c in cs), f"points {cnt[1]} vs {sum(len(c) for c in cs)}"
+
+
 def test_rpp_batch_matches_oracle(mantis):
     rng = np.random.default_rng(7)
     s = 0.16
