@@ -201,8 +201,8 @@ def main():
         "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
         # candidate bits read, edge bits written
         "hysteresis": ("hbm", frames_step * (W * H // 4)),
-        "det_morph": ("hbm", frames_step * (2 * W * H // 8)),
-        "mask_morph": ("hbm", frames_step * (2 * W * H // 8 * 15 + W * H)),
+        # edge bits read once; padded detector bits and mask bits written
+        "morph": ("hbm", frames_step * (W * H // 8 + (W + 2) * (H + 2) // 8 + W * H // 8)),
         "components": ("hbm", frames_step * (5 * (W + 2) * (H + 2))),
         "border_trace": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),

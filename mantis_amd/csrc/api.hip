@@ -122,6 +122,7 @@ struct Ctx {
           *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
+  uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   int32_t* d_rowb = nullptr;  // run CCL row bases, rstride per frame
@@ -190,6 +191,9 @@ inline void bind_device(const Ctx* c) {
   if (hipGetDevice(&d) != hipSuccess || d != c->cfg.device) (void)hipSetDevice(c->cfg.device);
 }
 
+// dynamic LDS of k_morph: three band buffers of (MB_BH + 2 MB_HALO) rows
+inline size_t morph_lds(int W) { return (size_t)3 * (MB_BH + 2 * MB_HALO) * ((W + 31) / 32) * sizeof(uint32_t); }
+
 inline int blocks_for(size_t n, int per = 256, int cap = 4096) {
   size_t b = (n + per - 1) / per;
   return (int)std::min<size_t>(std::max<size_t>(b, 1), (size_t)cap);
@@ -239,9 +243,6 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
 mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false, bool det_bytes = false) {
   const size_t P = c->plane;
-  const size_t npx = (size_t)W * H;
-  const int Wp = W + 2, Hp = H + 2;
-  if (det_bytes) HIP_OK(hipMemsetAsync(c->d_det, 0, P * n, c->s));
   mark(c, "start");
   const size_t B = c->bstride;
   dim3 gf((W + FTW - 1) / FTW, (H + FTH - 1) / FTH, n);
@@ -256,29 +257,12 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   k_hyst_edge<<<gf, 256, 0, c->s>>>(c->d_lroot, c->d_lab, c->d_strong, c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H, P,
                                     B);
   mark(c, "hysteresis");
-  // detector: dilate(iter 2) = 5x5 rect, erode(iter 1) = 3x3 rect -> zero-ringed det bytes
-  k_bh<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B, 2, 1);
-  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, nullptr, W, H, B, P, 2, 1, 0);
-  k_bh<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, W, H, B, 1, 0);
-  k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, nullptr, W, H, B, P, 1, 0, 0);
-  const size_t ndw = (size_t)dbits_wpw(W + 2) * (H + 2);
-  k_pack_det<<<dim3(blocks_for(ndw), n), 256, 0, c->s>>>(c->d_b2, c->d_dbits, W, H, B, c->dstride);
-  if (det_bytes) k_bv<<<gw, 256, 0, c->s>>>(c->d_b1, nullptr, c->d_det, W, H, B, P, 1, 0, 2);
-  mark(c, "det_morph");
-  // cleanImageByEdge mask: M0 then 3 x {dilate, erode}(3+i) and erode(3) -> mask bytes
-  k_bm0<<<gw, 256, 0, c->s>>>(c->d_eb, c->d_b1, W, H, B);
-  for (int i = 0; i < 3; i++) {
-    const int r = 3 + i;
-    k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, r, 1);
-    k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, nullptr, W, H, B, P, r, 1, 0);
-    k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, r, 0);
-    k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_b1, nullptr, W, H, B, P, r, 0, 0);
-  }
-  k_bh<<<gw, 256, 0, c->s>>>(c->d_b1, c->d_b2, W, H, B, 3, 0);
-  k_bv<<<gw, 256, 0, c->s>>>(c->d_b2, nullptr, c->d_mask, W, H, B, P, 3, 0, 1);
-  mark(c, "mask_morph");
-  (void)Wp;
-  (void)Hp;
+  // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
+  dim3 gm((H + MB_BH - 1) / MB_BH, n);
+  k_morph<<<gm, 256, morph_lds(W), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride);
+  if (det_bytes) k_bits_to_bytes<<<blocks_for((size_t)(W + 2) * (H + 2)), 256, 0, c->s>>>(c->d_dbits, c->d_det, W + 2, H + 2,
+                                                                                          dbits_wpw(W + 2));
+  mark(c, "morph");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -361,7 +345,7 @@ mantis_status run_score(Ctx* c, int n) {
   HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n, hipMemcpyHostToDevice, c->s));
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
-  k_frame_score<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mask, c->plane, L, c->d_st, c->d_hyps, c->d_gauss,
+  k_frame_score<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_gauss,
                                                c->d_res, c->d_dbg, c->cfg.particles, c->cfg.iterations,
                                                c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");
@@ -583,6 +567,14 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->bstride = (size_t)((c->Wmax + 31) / 32) * c->Hmax;
   c->dstride = (size_t)dbits_wpw(c->Wmax + 2) * (c->Hmax + 2);
   c->pool_cap = cfg.max_contour_points;
+  if (morph_lds(c->Wmax) > 160 * 1024 ||
+      hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize, (int)morph_lds(c->Wmax)) !=
+          hipSuccess) {
+    g_create_err = "max_width too large for the morphology band kernel";
+    (void)hipStreamDestroy(c->s);
+    delete c;
+    return MANTIS_ERR_ARG;
+  }
   const int F = c->F;
   const int per = cfg.particles * cfg.iterations * 6;
   mantis_status st = MANTIS_OK;
@@ -590,15 +582,16 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
   chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_lroot, (size_t)F * c->plane));
-  chk(dalloc(c, &c->d_edge, (size_t)F * c->plane));
-  chk(dalloc(c, &c->d_det, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_edge, c->plane));  // debug / single-frame byte planes (frame 0)
+  chk(dalloc(c, &c->d_det, c->plane));
   chk(dalloc(c, &c->d_eb, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
   c->rstride = (size_t)c->Hmax + 3;
   chk(dalloc(c, &c->d_rowb, (size_t)F * c->rstride));
-  chk(dalloc(c, &c->d_mask, (size_t)F * c->plane));
+  chk(dalloc(c, &c->d_mask, c->plane));
+  chk(dalloc(c, &c->d_mbits, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_lab, (size_t)F * c->plane));
   chk(dalloc(c, &c->d_frames, (size_t)F));
   chk(dalloc(c, &c->d_borders, (size_t)F * kMaxBorders));
@@ -648,7 +641,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_dbits, c->d_rowb,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
@@ -814,7 +807,10 @@ mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out,
   if (det_out) {
     HIP_OK(hipMemcpy2DAsync(det_out, W, c->d_det + (W + 2) + 1, W + 2, W, H, hipMemcpyDeviceToHost, c->s));
   }
-  if (mask_out) HIP_OK(hipMemcpyAsync(mask_out, c->d_mask, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
+  if (mask_out) {
+    k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_mbits, c->d_mask, W, H, 0);
+    HIP_OK(hipMemcpyAsync(mask_out, c->d_mask, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
+  }
   HIP_OK(hipStreamSynchronize(c->s));
   for (size_t i = 0; det_out && i < (size_t)W * H; i++) det_out[i] = det_out[i] ? 255 : 0;
   for (size_t i = 0; mask_out && i < (size_t)W * H; i++) mask_out[i] = mask_out[i] ? 255 : 0;

@@ -3,8 +3,8 @@
 // Stage map (reference -> kernel):
 //   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_uf (+ tile union-find)
 //   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_seam / _mark / _edge
-//   dilate x2 / erode x1             QuadDetection.h:213-214         k_bh / k_bv / k_pack_det (bit planes)
-//   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_bm0 + k_bh / k_bv
+//   dilate x2 / erode x1             QuadDetection.h:213-214         k_morph (bit planes, LDS bands)
+//   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_morph (same pass)
 //   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_run_count/_scan/_emit/_union/_border (run CCL)
 //                                                                    + k_trace_borders
 //                                                                    + k_frame_contours
@@ -472,55 +472,6 @@ __global__ __launch_bounds__(256) void k_hyst_edge(const uint16_t* __restrict__ 
   }
 }
 
-// ============================================================== morphology
-// Bit-packed rectangle dilate/erode passes and the cleanImageByEdge M0 plane
-// (mk_bits.h); one 32-pixel word per work-item.
-__global__ __launch_bounds__(256) void k_bh(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W, int H,
-                                            size_t bstride, int r, int dil) {
-  const int f = blockIdx.y;
-  const int WW = bits::words(W);
-  const size_t n = (size_t)WW * H;
-  const uint32_t* s = src + (size_t)f * bstride;
-  uint32_t* d = dst + (size_t)f * bstride;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const int w = (int)(k % WW), y = (int)(k / WW);
-    d[k] = bits::hword(s + (size_t)y * WW, w, W, r, dil != 0);
-  }
-}
-// mode 0: bits to dst; 1: bytes to out (W x H); 2: bytes into the interior of
-// the zero-ringed (W+2) x (H+2) plane out
-__global__ __launch_bounds__(256) void k_bv(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                            uint8_t* __restrict__ out, int W, int H, size_t bstride, size_t plane,
-                                            int r, int dil, int mode) {
-  const int f = blockIdx.y;
-  const int WW = bits::words(W);
-  const size_t n = (size_t)WW * H;
-  const uint32_t* s = src + (size_t)f * bstride;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const int w = (int)(k % WW), y = (int)(k / WW);
-    const uint32_t v = bits::vword(s, w, y, W, H, r, dil != 0);
-    if (mode == 0) {
-      dst[(size_t)f * bstride + k] = v;
-    } else {
-      uint8_t* o = out + (size_t)f * plane +
-                   (mode == 1 ? (size_t)y * W + 32 * w : (size_t)(y + 1) * (W + 2) + 1 + 32 * w);
-      const int xe = min(32, W - 32 * w);
-      for (int b = 0; b < xe; b++) o[b] = (uint8_t)((v >> b) & 1u);
-    }
-  }
-}
-__global__ __launch_bounds__(256) void k_bm0(const uint32_t* __restrict__ E, uint32_t* __restrict__ dst, int W, int H,
-                                             size_t bstride) {
-  const int f = blockIdx.y;
-  const int WW = bits::words(W);
-  const size_t n = (size_t)WW * H;
-  const uint32_t* e = E + (size_t)f * bstride;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const int w = (int)(k % WW), y = (int)(k / WW);
-    dst[(size_t)f * bstride + k] = bits::m0word(e, w, y, W, H);
-  }
-}
-
 // Padded detector binary as a row-aligned bit plane: (W+2) x (H+2) with the
 // zero ring, WPW = ceil((W+2)/32) + 1 words per row (the spare word lets a
 // 64-bit window at any x be read without a bounds test).
@@ -528,22 +479,132 @@ __device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
 __device__ inline uint32_t dbit(const uint32_t* B, int wpw, int x, int y) {
   return (B[(size_t)y * wpw + (x >> 5)] >> (x & 31)) & 1u;
 }
-__global__ __launch_bounds__(256) void k_pack_det(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W,
-                                                  int H, size_t bstride, size_t dstride) {
-  const int f = blockIdx.y;
-  const int WW = bits::words(W), Wp = W + 2, Hp = H + 2, wpw = dbits_wpw(Wp);
-  const size_t n = (size_t)wpw * Hp;
-  const uint32_t* s = src + (size_t)f * bstride;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    const int w = (int)(k % wpw), py = (int)(k / wpw);
-    uint32_t v = 0;
-    if (py > 0 && py < Hp - 1) {
-      const uint32_t* row = s + (size_t)(py - 1) * WW;
-      const uint32_t cur = w < WW ? row[w] : 0u;
-      const uint32_t prv = (w > 0 && w - 1 < WW) ? row[w - 1] : 0u;
-      v = (cur << 1) | (prv >> 31);  // padded x = image x + 1
+// ============================================================== morphology
+// Detector binary and cleanImageByEdge mask in one pass over the edge bit
+// plane (mk_bits.h word ops; one 32-pixel word per work-item). A block owns a
+// band of MB_BH output rows of one frame and keeps the band plus a MB_HALO-row
+// halo on each side in LDS (three row buffers), so the 2 + 16 stages of the
+// two chains never touch HBM between them: each stage recomputes the rows its
+// successors still need (its valid range shrinks by its vertical reach, except
+// at the image edge, where the clipped-window rules of mk_bits.h apply).
+//   detector  QuadDetection.h:213-214: dilate 5x5 (iterations 2), erode 3x3
+//             -> padded bit plane (zero ring) for the contour CCL
+//   mask      HypothesisEvaluation.h:319-363: M0 = edge | border(NOT gradient),
+//             3 x {dilate, erode}(3 + i), erode(3) -> mask bit plane
+constexpr int MB_BH = 64;     // output rows per band
+constexpr int MB_HALO = 29;   // mask chain reach: M0 2 + (3+3+4+4+5+5) + 3
+struct RowRange {
+  int lo, hi;  // absolute rows [lo, hi) valid in a buffer
+  __device__ RowRange shrink(int r, int H) const { return {lo == 0 ? 0 : lo + r, hi == H ? H : hi - r}; }
+};
+// buf holds absolute rows [y0, y0 + nrows); row y of the plane at buf + (y - y0) * WW
+__device__ inline void mb_h(const uint32_t* src, uint32_t* dst, RowRange rr, int y0, int WW, int W, int r, bool dil,
+                            int t, int nt) {
+  const int n = (rr.hi - rr.lo) * WW;
+  for (int k = t; k < n; k += nt) {
+    const int y = rr.lo + k / WW, w = k - (k / WW) * WW;
+    dst[(y - y0) * WW + w] = bits::hword(src + (y - y0) * WW, w, W, r, dil);
+  }
+}
+__device__ inline void mb_v(const uint32_t* src, uint32_t* dst, RowRange rr, int y0, int WW, int W, int H, int r,
+                            bool dil, int t, int nt) {
+  const uint32_t* base = src - (ptrdiff_t)y0 * WW;  // virtual plane base: only rows inside the buffer are read
+  const int n = (rr.hi - rr.lo) * WW;
+  for (int k = t; k < n; k += nt) {
+    const int y = rr.lo + k / WW, w = k - (k / WW) * WW;
+    dst[(y - y0) * WW + w] = bits::vword(base, w, y, W, H, r, dil);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
+                                               uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
+                                               size_t dstride) {
+  extern __shared__ uint32_t mb_lds[];
+  const int f = blockIdx.y, t = threadIdx.x, nt = blockDim.x;
+  const int WW = bits::words(W);
+  const int yb = blockIdx.x * MB_BH, ye = min(H, yb + MB_BH);
+  const int y0 = max(0, yb - MB_HALO), y1 = min(H, ye + MB_HALO);
+  const int rows = MB_BH + 2 * MB_HALO;
+  uint32_t* A = mb_lds;
+  uint32_t* B = A + rows * WW;
+  uint32_t* Cb = B + rows * WW;
+  const uint32_t* E = eb + (size_t)f * bstride;
+  for (int k = t; k < (y1 - y0) * WW; k += nt) A[k] = E[(size_t)y0 * WW + k];
+  __syncthreads();
+  RowRange rr{y0, y1};
+  // mask M0 (reach 2) from the edges into B
+  {
+    const RowRange m = rr.shrink(2, H);
+    const uint32_t* base = A - (ptrdiff_t)y0 * WW;
+    for (int k = t; k < (m.hi - m.lo) * WW; k += nt) {
+      const int y = m.lo + k / WW, w = k - (k / WW) * WW;
+      B[(y - y0) * WW + w] = bits::m0word(base, w, y, W, H);
     }
-    dst[(size_t)f * dstride + k] = v;
+  }
+  // detector: dilate r2 (A -> C -> A), erode r1 (A -> C -> A)
+  mb_h(A, Cb, rr, y0, WW, W, 2, true, t, nt);
+  __syncthreads();
+  RowRange d = rr.shrink(2, H);
+  mb_v(Cb, A, d, y0, WW, W, H, 2, true, t, nt);
+  __syncthreads();
+  mb_h(A, Cb, d, y0, WW, W, 1, false, t, nt);
+  __syncthreads();
+  d = d.shrink(1, H);
+  mb_v(Cb, A, d, y0, WW, W, H, 1, false, t, nt);
+  __syncthreads();
+  // padded detector rows py = y + 1 of this band (ring rows 0 and Hp - 1 by the edge bands)
+  {
+    const int wpw = dbits_wpw(W + 2);
+    uint32_t* D = dbits + (size_t)f * dstride;
+    const int py0 = yb == 0 ? 0 : yb + 1, py1 = ye == H ? H + 2 : ye + 1;
+    for (int k = t; k < (py1 - py0) * wpw; k += nt) {
+      const int py = py0 + k / wpw, w = k - (k / wpw) * wpw;
+      uint32_t v = 0;
+      if (py > 0 && py < H + 1) {
+        const uint32_t* row = A + (py - 1 - y0) * WW;
+        const uint32_t cur = w < WW ? row[w] : 0u;
+        const uint32_t prv = (w > 0 && w - 1 < WW) ? row[w - 1] : 0u;
+        v = (cur << 1) | (prv >> 31);  // padded x = image x + 1
+      }
+      D[(size_t)py * wpw + w] = v;
+    }
+  }
+  // mask: 3 x {dilate, erode}(3 + i), erode(3); B <-> A, result in B
+  RowRange m = rr.shrink(2, H);
+  for (int i = 0; i < 3; i++) {
+    const int r = 3 + i;
+    __syncthreads();
+    mb_h(B, A, m, y0, WW, W, r, true, t, nt);
+    __syncthreads();
+    m = m.shrink(r, H);
+    mb_v(A, B, m, y0, WW, W, H, r, true, t, nt);
+    __syncthreads();
+    mb_h(B, A, m, y0, WW, W, r, false, t, nt);
+    __syncthreads();
+    m = m.shrink(r, H);
+    mb_v(A, B, m, y0, WW, W, H, r, false, t, nt);
+  }
+  __syncthreads();
+  mb_h(B, A, m, y0, WW, W, 3, false, t, nt);
+  __syncthreads();
+  {
+    uint32_t* M = mbits + (size_t)f * bstride;
+    const uint32_t* base = A - (ptrdiff_t)y0 * WW;
+    for (int k = t; k < (ye - yb) * WW; k += nt) {
+      const int y = yb + k / WW, w = k - (k / WW) * WW;
+      M[(size_t)y * WW + w] = bits::vword(base, w, y, W, H, 3, false);
+    }
+  }
+}
+
+// debug bytes (frame 0): a W x H bit plane (wpw = 0: ceil(W/32) words per
+// row) or the padded detector plane (wpw = its words per row) -> one byte per pixel
+__global__ __launch_bounds__(256) void k_bits_to_bytes(const uint32_t* __restrict__ src, uint8_t* __restrict__ out,
+                                                       int W, int H, int wpw) {
+  const int WW = wpw ? wpw : bits::words(W);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < W * H; k += gridDim.x * blockDim.x) {
+    const int y = k / W, x = k - y * W;
+    out[k] = (uint8_t)((src[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u);
   }
 }
 
@@ -1542,18 +1603,38 @@ struct Landmarks {
   int32_t nw, nr, ng;
 };
 
-// cleaned (mask != nullptr) or original BGR pixel, linear-offset semantics
-// for cvRound(px) == W / == H: out-of-buffer reads are 0.
-__device__ inline void fetch_px(const uint8_t* bgr, const uint8_t* mask, int W, int H, int x, int y, int& b, int& g,
+// Masks of the cleaned image (HypothesisEvaluation.h:364 img.copyTo(out, mask)):
+// none (original image), host bytes (standalone scoring API) or the k_morph
+// bit plane (pipeline). Pixels are addressed by linear offset (below).
+struct MaskNone {
+  __device__ bool operator()(long, int, int) const { return true; }
+};
+struct MaskBytes {
+  const uint8_t* m;
+  __device__ bool operator()(long lin, int, int) const { return m[lin] != 0; }
+};
+struct MaskBits {
+  const uint32_t* m;
+  int WW, W;
+  __device__ bool operator()(long lin, int x, int y) const {
+    if (x < 0 || x >= W) { y = (int)(lin / W); x = (int)(lin - (long)y * W); }
+    return (m[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
+  }
+};
+// cleaned or original BGR pixel, linear-offset semantics for cvRound(px) ==
+// W / == H: out-of-buffer reads are 0.
+template <class MK>
+__device__ inline void fetch_px(const uint8_t* bgr, const MK& mask, int W, int H, int x, int y, int& b, int& g,
                                 int& r) {
   long lin = (long)y * W + x;
-  if (lin < 0 || lin >= (long)W * H || (mask && !mask[lin])) { b = g = r = 0; return; }
+  if (lin < 0 || lin >= (long)W * H || !mask(lin, x, y)) { b = g = r = 0; return; }
   const uint8_t* p = bgr + 3 * lin;
   b = p[0]; g = p[1]; r = p[2];
 }
 
 // fast error terms of one landmark: returns 1 if counted
-__device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, const uint8_t* bgr, const uint8_t* mask,
+template <class MK>
+__device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, const uint8_t* bgr, const MK& mask,
                                 int W, int H, int& e) {
   double rp[3];
   xf_apply(c2w, X, rp);
@@ -1569,8 +1650,9 @@ __device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, c
 }
 
 // one wave scores one hypothesis over all landmarks (64 lanes, int64 sum)
+template <class MK>
 __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
-                                       const uint8_t* mask, int W, int H, double* err_out, int* n_out) {
+                                       const MK& mask, int W, int H, double* err_out, int* n_out) {
   const int lane = threadIdx.x & 63;
   long long s = 0;
   int n = 0;
@@ -1608,7 +1690,7 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
           for (double ox = -5.0; ox < 5.0; ox += 1)
             for (double oy = -5.0; oy < 5.0; oy += 1) {
               int b, g, r;
-              fetch_px(bgr, nullptr, W, H, cv_round(u + ox), cv_round(v + oy), b, g, r);
+              fetch_px(bgr, MaskNone{}, W, H, cv_round(u + ox), cv_round(v + oy), b, g, r);
               int e0 = b - 50, e1 = g - 255, e2 = r - 85;
               err += (double)(e0 * e0 + e1 * e1 + e2 * e2);
             }
@@ -1641,14 +1723,14 @@ struct PoseLds {
 };
 
 __global__ __launch_bounds__(kScoreThreads) void k_frame_score(
-    const FrameDesc* __restrict__ frames, const uint8_t* __restrict__ masks, size_t plane, Landmarks lmk,
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     FrameState* st, HypRec* __restrict__ hyps, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
     FrameDebug* dbg, int particles, int iterations, double grid_spacing, int grid_size) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const uint8_t* mask = masks + (size_t)f * plane;
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
   mantis_cam_result& R = res[f];
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
@@ -1889,7 +1971,8 @@ __global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__
   double e;
   int np;
   const int nl = lmk.nw + lmk.nr + lmk.ng;
-  if (fast) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, mask, fd.w, fd.h, &e, &np);
+  if (fast && mask) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskBytes{mask}, fd.w, fd.h, &e, &np);
+  else if (fast) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskNone{}, fd.w, fd.h, &e, &np);
   else wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, terms[wave], &e, &np);
   if (lane == 0) {
     err[h] = e;
