@@ -480,48 +480,73 @@ __device__ inline uint32_t dbit(const uint32_t* B, int wpw, int x, int y) {
   return (B[(size_t)y * wpw + (x >> 5)] >> (x & 31)) & 1u;
 }
 // ============================================================== morphology
-// Detector binary and cleanImageByEdge mask in one pass over the edge bit
-// plane (mk_bits.h word ops; one 32-pixel word per work-item). A block owns a
-// band of MB_BH output rows of one frame and keeps the band plus a MB_HALO-row
-// halo on each side in LDS (three row buffers), so the 2 + 16 stages of the
-// two chains never touch HBM between them: each stage recomputes the rows its
-// successors still need (its valid range shrinks by its vertical reach, except
-// at the image edge, where the clipped-window rules of mk_bits.h apply).
-//   detector  QuadDetection.h:213-214: dilate 5x5 (iterations 2), erode 3x3
-//             -> padded bit plane (zero ring) for the contour CCL
-//   mask      HypothesisEvaluation.h:319-363: M0 = edge | border(NOT gradient),
-//             3 x {dilate, erode}(3 + i), erode(3) -> mask bit plane
 constexpr int MB_BH = 64;     // output rows per band
 constexpr int MB_HALO = 29;   // mask chain reach: M0 2 + (3+3+4+4+5+5) + 3
 struct RowRange {
   int lo, hi;  // absolute rows [lo, hi) valid in a buffer
   __device__ RowRange shrink(int r, int H) const { return {lo == 0 ? 0 : lo + r, hi == H ? H : hi - r}; }
 };
-// buf holds absolute rows [y0, y0 + nrows); row y of the plane at buf + (y - y0) * WW
-__device__ inline void mb_h(const uint32_t* src, uint32_t* dst, RowRange rr, int y0, int WW, int W, int r, bool dil,
-                            int t, int nt) {
-  const int n = (rr.hi - rr.lo) * WW;
-  for (int k = t; k < n; k += nt) {
-    const int y = rr.lo + k / WW, w = k - (k / WW) * WW;
-    dst[(y - y0) * WW + w] = bits::hword(src + (y - y0) * WW, w, W, r, dil);
+// Work-item layout inside a band: work-item (w, g) owns word column w and the
+// g-th of G contiguous row segments of each pass's output range, so the
+// vertical window slides down its column in registers (one new row per output
+// row) instead of re-reading 2r + 1 rows, and no index is divided per word.
+struct MbLane {
+  int w, g, G;
+  __device__ bool active() const { return g < G; }
+  __device__ void seg(RowRange rr, int& a, int& b) const {
+    const int s = (rr.hi - rr.lo + G - 1) / G;
+    a = rr.lo + g * s;
+    b = min(rr.hi, a + s);
   }
-}
-__device__ inline void mb_v(const uint32_t* src, uint32_t* dst, RowRange rr, int y0, int WW, int W, int H, int r,
-                            bool dil, int t, int nt) {
-  const uint32_t* base = src - (ptrdiff_t)y0 * WW;  // virtual plane base: only rows inside the buffer are read
-  const int n = (rr.hi - rr.lo) * WW;
-  for (int k = t; k < n; k += nt) {
-    const int y = rr.lo + k / WW, w = k - (k / WW) * WW;
-    dst[(y - y0) * WW + w] = bits::vword(base, w, y, W, H, r, dil);
+};
+// One separable rectangle pass (radius R; dilate or erode), horizontal and
+// vertical fused: out(y) = OP_{|k|<=R, 0<=y+k<H} hword(in, y+k). src/dst hold
+// absolute rows [y0, ...) at row pitch WW; dst row y goes to dst + (y - y0) * WW.
+template <int R, bool DIL>
+__device__ inline void mb_hv(const uint32_t* src, uint32_t* dst, RowRange out, int y0, int WW, int W, int H,
+                             const MbLane& L) {
+  if (!L.active()) return;
+  int a, b;
+  L.seg(out, a, b);
+  if (a >= b) return;
+  const uint32_t ident = DIL ? 0u : 0xffffffffu;
+  const uint32_t vmask = bits::valid(L.w, W);
+  uint32_t ring[2 * R + 1];
+#pragma unroll
+  for (int k = 0; k < 2 * R; k++) {
+    const int yy = a - R + k;
+    ring[k] = (yy >= 0 && yy < H) ? bits::hword(src + (yy - y0) * WW, L.w, W, R, DIL) : ident;
+  }
+  for (int y = a; y < b; y++) {
+    const int yy = y + R;
+    ring[2 * R] = yy < H ? bits::hword(src + (yy - y0) * WW, L.w, W, R, DIL) : ident;
+    uint32_t acc = ring[0];
+#pragma unroll
+    for (int k = 1; k <= 2 * R; k++) acc = DIL ? (acc | ring[k]) : (acc & ring[k]);
+    dst[(y - y0) * WW + L.w] = acc & vmask;
+#pragma unroll
+    for (int k = 0; k < 2 * R; k++) ring[k] = ring[k + 1];
   }
 }
 
+// Detector binary and cleanImageByEdge mask in one pass over the edge bit
+// plane (mk_bits.h word semantics). A block owns a band of MB_BH output rows of
+// one frame and keeps the band plus a MB_HALO-row halo on each side in LDS
+// (three row buffers), so the stages of the two chains never touch HBM between
+// them: each stage recomputes the rows its successors still need (its valid
+// range shrinks by its vertical reach, except at the image edge, where the
+// clipped-window rules of mk_bits.h apply).
+//   detector  QuadDetection.h:213-214: dilate 5x5 (iterations 2), erode 3x3
+//             -> padded bit plane (zero ring) for the contour CCL
+//   mask      HypothesisEvaluation.h:319-363: NG = NOT(gradient), M0 = edge |
+//             border(NG), 3 x {dilate, erode}(3 + i), erode(3) -> mask bit plane
 __global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
                                                size_t dstride) {
   extern __shared__ uint32_t mb_lds[];
   const int f = blockIdx.y, t = threadIdx.x, nt = blockDim.x;
   const int WW = bits::words(W);
+  const MbLane L{t % WW, t / WW, nt / WW};
   const int yb = blockIdx.x * MB_BH, ye = min(H, yb + MB_BH);
   const int y0 = max(0, yb - MB_HALO), y1 = min(H, ye + MB_HALO);
   const int rows = MB_BH + 2 * MB_HALO;
@@ -531,26 +556,43 @@ __global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, 
   const uint32_t* E = eb + (size_t)f * bstride;
   for (int k = t; k < (y1 - y0) * WW; k += nt) A[k] = E[(size_t)y0 * WW + k];
   __syncthreads();
-  RowRange rr{y0, y1};
-  // mask M0 (reach 2) from the edges into B
-  {
-    const RowRange m = rr.shrink(2, H);
+  const RowRange rr{y0, y1};
+  const uint32_t vmask = bits::valid(L.w, W);
+  // NG (reach 1): A -> Cb
+  const RowRange rng = rr.shrink(1, H);
+  if (L.active()) {
+    int a, b;
+    L.seg(rng, a, b);
     const uint32_t* base = A - (ptrdiff_t)y0 * WW;
-    for (int k = t; k < (m.hi - m.lo) * WW; k += nt) {
-      const int y = m.lo + k / WW, w = k - (k / WW) * WW;
-      B[(y - y0) * WW + w] = bits::m0word(base, w, y, W, H);
+    for (int y = a; y < b; y++) Cb[(y - y0) * WW + L.w] = bits::ngword(base, L.w, y, W, H);
+  }
+  __syncthreads();
+  // M0 = edge | border(NG) (reach 2): (A, Cb) -> B
+  const RowRange rm0 = rng.shrink(1, H);
+  if (L.active()) {
+    int a, b;
+    L.seg(rm0, a, b);
+    const int w = L.w;
+    for (int y = a; y < b; y++) {
+      const uint32_t* nr = Cb + (y - y0) * WW;
+      const uint32_t ng = nr[w];
+      const uint32_t ngl = w > 0 ? nr[w - 1] : 0u;
+      const uint32_t ngr = w + 1 < WW ? nr[w + 1] : 0u;
+      const uint32_t left = (ng << 1) | (ngl >> 31);   // ng(x - 1), 0 left of the image
+      const uint32_t right = (ng >> 1) | (ngr << 31);  // ng(x + 1), 0 right of the image
+      const uint32_t up = y > 0 ? nr[w - WW] : 0u;
+      const uint32_t down = y + 1 < H ? nr[w + WW] : 0u;
+      const uint32_t bd = ng & (~left | ~right | ~up | ~down);
+      B[(y - y0) * WW + w] = (A[(y - y0) * WW + w] | bd) & vmask;
     }
   }
-  // detector: dilate r2 (A -> C -> A), erode r1 (A -> C -> A)
-  mb_h(A, Cb, rr, y0, WW, W, 2, true, t, nt);
   __syncthreads();
+  // detector: dilate r2 (A -> Cb), erode r1 (Cb -> A)
   RowRange d = rr.shrink(2, H);
-  mb_v(Cb, A, d, y0, WW, W, H, 2, true, t, nt);
-  __syncthreads();
-  mb_h(A, Cb, d, y0, WW, W, 1, false, t, nt);
+  mb_hv<2, true>(A, Cb, d, y0, WW, W, H, L);
   __syncthreads();
   d = d.shrink(1, H);
-  mb_v(Cb, A, d, y0, WW, W, H, 1, false, t, nt);
+  mb_hv<1, false>(Cb, A, d, y0, WW, W, H, L);
   __syncthreads();
   // padded detector rows py = y + 1 of this band (ring rows 0 and Hp - 1 by the edge bands)
   {
@@ -569,32 +611,29 @@ __global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, 
       D[(size_t)py * wpw + w] = v;
     }
   }
-  // mask: 3 x {dilate, erode}(3 + i), erode(3); B <-> A, result in B
-  RowRange m = rr.shrink(2, H);
-  for (int i = 0; i < 3; i++) {
-    const int r = 3 + i;
-    __syncthreads();
-    mb_h(B, A, m, y0, WW, W, r, true, t, nt);
-    __syncthreads();
-    m = m.shrink(r, H);
-    mb_v(A, B, m, y0, WW, W, H, r, true, t, nt);
-    __syncthreads();
-    mb_h(B, A, m, y0, WW, W, r, false, t, nt);
-    __syncthreads();
-    m = m.shrink(r, H);
-    mb_v(A, B, m, y0, WW, W, H, r, false, t, nt);
-  }
+  // mask: {dilate, erode}(3), (4), (5) ping-pong B <-> A, then erode(3) -> HBM
+  RowRange m = rm0.shrink(3, H);
   __syncthreads();
-  mb_h(B, A, m, y0, WW, W, 3, false, t, nt);
+  mb_hv<3, true>(B, A, m, y0, WW, W, H, L);
   __syncthreads();
-  {
-    uint32_t* M = mbits + (size_t)f * bstride;
-    const uint32_t* base = A - (ptrdiff_t)y0 * WW;
-    for (int k = t; k < (ye - yb) * WW; k += nt) {
-      const int y = yb + k / WW, w = k - (k / WW) * WW;
-      M[(size_t)y * WW + w] = bits::vword(base, w, y, W, H, 3, false);
-    }
-  }
+  m = m.shrink(3, H);
+  mb_hv<3, false>(A, B, m, y0, WW, W, H, L);
+  __syncthreads();
+  m = m.shrink(4, H);
+  mb_hv<4, true>(B, A, m, y0, WW, W, H, L);
+  __syncthreads();
+  m = m.shrink(4, H);
+  mb_hv<4, false>(A, B, m, y0, WW, W, H, L);
+  __syncthreads();
+  m = m.shrink(5, H);
+  mb_hv<5, true>(B, A, m, y0, WW, W, H, L);
+  __syncthreads();
+  m = m.shrink(5, H);
+  mb_hv<5, false>(A, B, m, y0, WW, W, H, L);
+  __syncthreads();
+  // final erode(3) straight to the mask plane: output rows [yb, ye)
+  uint32_t* M = mbits + (size_t)f * bstride;
+  mb_hv<3, false>(B, M + (ptrdiff_t)y0 * WW, RowRange{yb, ye}, y0, WW, W, H, L);
 }
 
 // debug bytes (frame 0): a W x H bit plane (wpw = 0: ceil(W/32) words per
