@@ -114,6 +114,7 @@ struct Ctx {
   int nw = 0, nr = 0, ng = 0;
   // capacity
   int F = 0, Wmax = 0, Hmax = 0;
+  int n_cu = 256;  // compute units of the device (block-size choices)
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
@@ -150,6 +151,7 @@ struct Ctx {
   int gn_rigs = 0, gn_cpr = 0;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
+  ScoreState* d_sst = nullptr;  // scoring state between k_score_init / _pf / _final
   FrameDebug* d_dbg = nullptr;
   mantis_cam_result* d_res = nullptr;
   float* d_gauss = nullptr;
@@ -345,9 +347,12 @@ mantis_status run_score(Ctx* c, int n) {
   HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n, hipMemcpyHostToDevice, c->s));
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
-  k_frame_score<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_gauss,
-                                               c->d_res, c->d_dbg, c->cfg.particles, c->cfg.iterations,
-                                               c->cfg.grid_spacing, 9);
+  k_score_init<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
+                                              c->d_dbg, c->d_sst);
+  k_score_pf<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res,
+                                            c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
+  k_score_final<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
+                                               c->d_sst, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
@@ -560,6 +565,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     delete c;
     return MANTIS_ERR_DEVICE;
   }
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg.device) != hipSuccess || c->n_cu < 1)
+    c->n_cu = 256;
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
@@ -609,6 +616,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_st, (size_t)F));
+  chk(dalloc(c, &c->d_sst, (size_t)F));
   chk(dalloc(c, &c->d_dbg, (size_t)F));
   chk(dalloc(c, &c->d_res, (size_t)F));
   chk(dalloc(c, &c->d_gauss, (size_t)F * per));
@@ -643,7 +651,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
-                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
+                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   for (void* p : c->user_allocs) (void)hipFree(p);

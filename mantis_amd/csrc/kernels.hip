@@ -1645,12 +1645,19 @@ struct Landmarks {
 // Masks of the cleaned image (HypothesisEvaluation.h:364 img.copyTo(out, mask)):
 // none (original image), host bytes (standalone scoring API) or the k_morph
 // bit plane (pipeline). Pixels are addressed by linear offset (below).
+// Each mask offers operator() (one pixel, for fetch_px) and a split form for
+// the pipelined fast scorer: word() issues the load of the mask word holding
+// pixel (x, y) (x already normalised to [0, W)), test() extracts the bit.
 struct MaskNone {
   __device__ bool operator()(long, int, int) const { return true; }
+  __device__ uint32_t word(long, int, int) const { return 1u; }
+  __device__ bool test(uint32_t, int) const { return true; }
 };
 struct MaskBytes {
   const uint8_t* m;
   __device__ bool operator()(long lin, int, int) const { return m[lin] != 0; }
+  __device__ uint32_t word(long lin, int, int) const { return m[lin]; }
+  __device__ bool test(uint32_t w, int) const { return w != 0; }
 };
 struct MaskBits {
   const uint32_t* m;
@@ -1659,6 +1666,8 @@ struct MaskBits {
     if (x < 0 || x >= W) { y = (int)(lin / W); x = (int)(lin - (long)y * W); }
     return (m[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
   }
+  __device__ uint32_t word(long, int x, int y) const { return m[(size_t)y * WW + (x >> 5)]; }
+  __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 // cleaned or original BGR pixel, linear-offset semantics for cvRound(px) ==
 // W / == H: out-of-buffer reads are 0.
@@ -1688,16 +1697,73 @@ __device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, c
   return 1;
 }
 
-// one wave scores one hypothesis over all landmarks (64 lanes, int64 sum)
+// B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
+// last pixel of the frame reads one byte early so the load stays in the buffer.
+__device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
+  const bool last = lin == npx - 1;
+  uint32_t v;
+  __builtin_memcpy(&v, bgr + 3 * lin - (last ? 1 : 0), 4);
+  return last ? (v >> 8) : v;
+}
+
+// one wave scores one hypothesis over all landmarks (64 lanes, int64 sum).
+// Software-pipelined: kFastUnroll landmarks per lane are projected first, then
+// their mask-word and pixel loads are issued together (the pixel load does
+// not wait for the mask bit), then the terms are summed -- the gathers of a
+// group overlap instead of costing two L2 round trips per landmark.
+// Term of a landmark with z > 0 and inFrame (computePointErrorFAST,
+// HypothesisEvaluation.h:218-227 on the cleaned image): the squared distance
+// of its BGR to white, or 3 * 255^2 when the pixel is masked out or lies past
+// the end of the buffer (linear-offset read of cvRound(px) == W / == H).
+constexpr int kFastUnroll = 4;
 template <class MK>
 __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
                                        const MK& mask, int W, int H, double* err_out, int* n_out) {
   const int lane = threadIdx.x & 63;
+  const long npx = (long)W * H;
   long long s = 0;
   int n = 0;
-  for (int l = lane; l < nl; l += 64) {
-    int e;
-    if (fast_term(c2w, lm + 3 * l, cm, bgr, mask, W, H, e)) { s += e; n++; }
+  for (int l0 = lane; l0 < nl; l0 += 64 * kFastUnroll) {
+    long lin[kFastUnroll];
+    int px[kFastUnroll], py[kFastUnroll];
+    bool in[kFastUnroll], ok[kFastUnroll];
+    // branch-free projections (z <= 0 or an off-frame point just fails the
+    // flags), so the kFastUnroll independent FP64 chains interleave
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) {
+      const int l = l0 + 64 * k;
+      const double* X = lm + 3 * (l < nl ? l : nl - 1);
+      double rp[3];
+      xf_apply(c2w, X, rp);
+      double u, v;
+      distort(cm, rp[0], rp[1], rp[2], &u, &v);
+      in[k] = l < nl && rp[2] > 0 && in_frame(u, v, H, W);
+      int x = in[k] ? cv_round(u) : 0, y = in[k] ? cv_round(v) : 0;
+      long li = (long)y * W + x;
+      ok[k] = in[k] && li >= 0 && li < npx;
+      if (x >= W) { x -= W; y += 1; }  // cvRound(u) == W: next row (linear offset)
+      if (!ok[k]) { li = 0; x = 0; y = 0; }
+      lin[k] = li;
+      px[k] = x;
+      py[k] = y;
+    }
+    uint32_t mw[kFastUnroll], pv[kFastUnroll];
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) pv[k] = load_bgr(bgr, lin[k], npx);
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) {
+      if (!in[k]) continue;
+      n++;
+      int e = 3 * 255 * 255;
+      if (ok[k] && mask.test(mw[k], px[k])) {
+        const int b = (int)(pv[k] & 0xffu), g = (int)((pv[k] >> 8) & 0xffu), r = (int)((pv[k] >> 16) & 0xffu);
+        const int e0 = b - 255, e1 = g - 255, e2 = r - 255;
+        e = e0 * e0 + e1 * e1 + e2 * e2;
+      }
+      s += e;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o);
@@ -1752,7 +1818,15 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
   __builtin_amdgcn_wave_barrier();
 }
 
-constexpr int kScoreThreads = 512;
+// Scoring is three kernels per frame batch (one block per frame each), so
+// the particle filter -- 500 of the ~620 scored hypotheses of a frame -- runs
+// in a lean kernel whose register budget is not set by the sorting and
+// publishing code (VGPRs bound the waves a CU keeps in flight):
+//   k_score_init   evaluateHypotheses(C hyps) + getBestNHypotheses(1)
+//   k_score_pf     optimizeHypothesisWithParticleFilter (10 x 50)
+//   k_score_final  81 shifts, top-20, determineBestYaw, publish gate
+// Block size: 10 waves per frame (50 particles = 5 rounds of waves).
+constexpr int kScoreThreads = 640;
 constexpr int kWaves = kScoreThreads / 64;
 
 struct PoseLds {
@@ -1760,11 +1834,32 @@ struct PoseLds {
   Quat q;
   double err;
 };
+// per-frame state handed from one scoring kernel to the next
+struct ScoreState {
+  PoseLds cur;
+  int32_t nsc, pad;
+};
 
-__global__ __launch_bounds__(kScoreThreads) void k_frame_score(
+// wave-uniform double into SGPRs (pose operands of the projection loop)
+__device__ inline double rfl(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ inline Xf rfl(const Xf& T) {
+  Xf u;
+#pragma unroll
+  for (int k = 0; k < 9; k++) u.R[k] = rfl(T.R[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) u.t[k] = rfl(T.t[k]);
+  return u;
+}
+
+__global__ __launch_bounds__(kScoreThreads) void k_score_init(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
-    FrameState* st, HypRec* __restrict__ hyps, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
-    FrameDebug* dbg, int particles, int iterations, double grid_spacing, int grid_size) {
+    FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
+    ScoreState* __restrict__ sst) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const FrameDesc fd = frames[f];
@@ -1774,13 +1869,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_frame_score(
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   __shared__ double lm[3 * 768];
-  __shared__ PoseLds P[96];
   __shared__ ErrIdx ei[kMaxHyps];
-  __shared__ double terms[kWaves][64];
-  __shared__ int32_t np_s[96];
   __shared__ PoseLds cur;
-  __shared__ double shv[9];
-  __shared__ double yerr[4];
   __shared__ int32_t nsc;
   if (!st[f].reaches_pf) {
     if (tid == 0) {
@@ -1831,8 +1921,40 @@ __global__ __launch_bounds__(kScoreThreads) void k_frame_score(
     nsc = C + 1;
   }
   __syncthreads();
-  // optimizeHypothesisWithParticleFilter: particles are w2c_sample * rand,
-  // rand = Transform(setRPY(g,g,g), (g,g,g)) drawn yaw, pitch, roll, z, y, x.
+  if (tid == 0) {
+    sst[f].cur = cur;
+    sst[f].nsc = nsc;
+  }
+}
+
+// optimizeHypothesisWithParticleFilter (PoseAdjustment.h:13-60): particles are
+// w2c_sample * rand, rand = Transform(setRPY(g,g,g), (g,g,g)) drawn yaw, pitch,
+// roll, z, y, x; best = first strict minimum (argmin by (error, index) over
+// the 50, taken only when strictly below the current error).
+__global__ __launch_bounds__(kScoreThreads) void k_score_pf(
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
+    const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
+    FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (!st[f].reaches_pf) return;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  FrameDebug& D = dbg[f];
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  __shared__ double lm[3 * 768];
+  __shared__ Xf Pc[96], Pw[96];
+  __shared__ double Pe[96];
+  __shared__ Xf cur_c2w, cur_w2c;
+  __shared__ double cur_err;
+  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  if (tid == 0) {
+    cur_c2w = sst[f].cur.c2w;
+    cur_w2c = sst[f].cur.w2c;
+    cur_err = sst[f].cur.err;
+  }
+  __syncthreads();
   const float* gs = gauss + st[f].gauss_offset;
   for (int it = 0; it < iterations; it++) {
     if (tid < particles) {
@@ -1840,33 +1962,80 @@ __global__ __launch_bounds__(kScoreThreads) void k_frame_score(
       double yaw = (double)g6[0] * 0.03, pitch = (double)g6[1] * 0.03, roll = (double)g6[2] * 0.03;
       double tz = (double)g6[3] * 0.01, ty = (double)g6[4] * 0.01, tx = (double)g6[5] * 0.01;
       Xf rnd;
-      basis_from_rpy(roll, pitch, yaw, rnd.R);
+      basis_from_rpy_small(roll, pitch, yaw, rnd.R);  // |angle| < 2 rad: float gaussian x 0.03
       rnd.t[0] = tx; rnd.t[1] = ty; rnd.t[2] = tz;
-      Hyp h;
-      hyp_set_w2c(h, xf_mul(cur.w2c, rnd));
-      P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
+      const Xf w2c = xf_mul(cur_w2c, rnd);
+      Pw[tid] = w2c;
+      Pc[tid] = xf_inverse(w2c);
     }
     __syncthreads();
-    for (int j = wave; j < particles; j += kWaves) {
+    for (int j = __builtin_amdgcn_readfirstlane(wave); j < particles; j += kWaves) {
       double e;
       int n;
-      wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
-      if (lane == 0) P[j].err = e;
+      wave_score_fast(rfl(Pc[j]), lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+      if (lane == 0) Pe[j] = e;
     }
     __syncthreads();
-    if (tid == 0) {
-      for (int j = 0; j < particles; j++)
-        if (P[j].err < cur.err) cur = P[j];
-      D.pf_iter_err[it + 1] = cur.err;
+    if (wave == 0) {
+      double be = DBL_MAX;
+      int bj = 0x7fffffff;
+      for (int j = lane; j < particles; j += 64)
+        if (Pe[j] < be || bj == 0x7fffffff) { be = Pe[j]; bj = j; }
+      for (int o = 32; o > 0; o >>= 1) {
+        const double oe = __shfl_xor(be, o);
+        const int oj = __shfl_xor(bj, o);
+        if (oe < be || (oe == be && oj < bj)) { be = oe; bj = oj; }
+      }
+      if (lane == 0) {
+        if (bj < particles && be < cur_err) {
+          cur_err = be;
+          cur_c2w = Pc[bj];
+          cur_w2c = Pw[bj];
+        }
+        D.pf_iter_err[it + 1] = cur_err;
+      }
     }
     __syncthreads();
   }
   if (tid == 0) {
-    nsc += iterations * particles;
-    for (int k = 0; k < 9; k++) D.pf_c2w[k] = cur.c2w.R[k];
-    for (int k = 0; k < 3; k++) D.pf_c2w[9 + k] = cur.c2w.t[k];
-    D.pf_err = cur.err;
-    R.pf_error = cur.err;
+    ScoreState& S = sst[f];
+    S.cur.c2w = cur_c2w;
+    S.cur.w2c = cur_w2c;
+    S.cur.q = basis_to_quat(cur_w2c.R);
+    S.cur.err = cur_err;
+    S.nsc += iterations * particles;
+    for (int k = 0; k < 9; k++) D.pf_c2w[k] = cur_c2w.R[k];
+    for (int k = 0; k < 3; k++) D.pf_c2w[9 + k] = cur_c2w.t[k];
+    D.pf_err = cur_err;
+    res[f].pf_error = cur_err;
+  }
+}
+
+__global__ __launch_bounds__(kScoreThreads) void k_score_final(
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
+    const FrameState* __restrict__ st, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
+    const ScoreState* __restrict__ sst, double grid_spacing, int grid_size) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (!st[f].reaches_pf) return;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  mantis_cam_result& R = res[f];
+  FrameDebug& D = dbg[f];
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  __shared__ double lm[3 * 768];
+  __shared__ PoseLds P[96];
+  __shared__ ErrIdx ei[96];
+  __shared__ double terms[kWaves][64];
+  __shared__ PoseLds cur;
+  __shared__ double shv[9];
+  __shared__ double yerr[4];
+  __shared__ int32_t nsc;
+  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  if (tid == 0) {
+    cur = sst[f].cur;
+    nsc = sst[f].nsc;
     // shift values accumulate in double exactly as the reference loop does
     double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
     int k = 0;

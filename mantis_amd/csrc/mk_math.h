@@ -14,6 +14,8 @@
 #include <cmath>
 #include <cstdint>
 
+#include "mk_dmath.h"
+
 #ifdef __HIPCC__
 #define MK_HD __host__ __device__ inline
 #else
@@ -109,6 +111,22 @@ MK_HD void basis_from_rpy(double roll, double pitch, double yaw, double* R) {
   R[3] = cj * sh; R[4] = sj * ss + cc; R[5] = sj * cs - sc;
   R[6] = -sj; R[7] = cj * si; R[8] = cj * ci;
 }
+// basis_from_rpy for |angles| < 2^30: on the device mk_dmath.h sincos_small
+// (= ocml sin/cos without the large-argument path), glibc on the host
+MK_HD void basis_from_rpy_small(double roll, double pitch, double yaw, double* R) {
+#if !MK_DM_DEVICE
+  basis_from_rpy(roll, pitch, yaw, R);
+#else
+  double si, ci, sj, cj, sh, ch;
+  dm::sincos_small(roll, &si, &ci);
+  dm::sincos_small(pitch, &sj, &cj);
+  dm::sincos_small(yaw, &sh, &ch);
+  double cc = ci * ch, cs = ci * sh, sc = si * ch, ss = si * sh;
+  R[0] = cj * ch; R[1] = sj * sc - cs; R[2] = sj * cc + ss;
+  R[3] = cj * sh; R[4] = sj * ss + cc; R[5] = sj * cs - sc;
+  R[6] = -sj; R[7] = cj * si; R[8] = cj * ci;
+#endif
+}
 // getRPY (getEulerYPR solution 1)
 MK_HD void basis_to_rpy(const double* m, double* roll, double* pitch, double* yaw) {
   if (fabs(m[6]) >= 1) {
@@ -154,7 +172,11 @@ MK_HD void distort(const Cam& cm, double X, double Y, double Z, double* u, doubl
   double x = X / Z, y = Y / Z;
   double r2 = x * x + y * y;
   double r = sqrt(r2);
+#if MK_DM_DEVICE
+  double theta = dm::atan(r);  // ocml atan, op for op (mk_dmath.h)
+#else
   double theta = atan(r);
+#endif
   double theta2 = theta * theta, theta3 = theta2 * theta, theta4 = theta2 * theta2, theta5 = theta4 * theta,
          theta6 = theta3 * theta3, theta7 = theta6 * theta, theta8 = theta4 * theta4, theta9 = theta8 * theta;
   double theta_d = theta + cm.k[0] * theta3 + cm.k[1] * theta5 + cm.k[2] * theta7 + cm.k[3] * theta9;
