@@ -115,6 +115,10 @@ struct Ctx {
   // capacity
   int F = 0, Wmax = 0, Hmax = 0;
   int n_cu = 256;  // compute units of the device (block-size choices)
+  // k_trace_borders_lds (bit plane in LDS) for batches of at most trace_lds_frames frames
+  bool trace_lds_ok = false;
+  size_t trace_lds_max = 0;
+  int trace_lds_frames = 0;
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
@@ -282,8 +286,13 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   k_run_border<<<grow, 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, c->d_borders, c->d_st, Wp, Hp,
                                        kMaxBorders);
   mark(c, "components");
-  k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
-                                                c->d_scratch, c->pool_cap, Wp, kMaxBorders);
+  const size_t tb_lds = (size_t)dbits_wpw(Wp) * Hp * sizeof(uint32_t);
+  if (c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames)
+    k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
+                                                   c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders);
+  else
+    k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
+                                                  c->d_scratch, c->pool_cap, Wp, kMaxBorders);
   mark(c, "border_trace");
   k_frame_contours<<<n, 1024, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
                                          c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
@@ -324,7 +333,7 @@ mantis_status run_pose(Ctx* c, int n) {
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
   const int per = c->cfg.particles * c->cfg.iterations * 6;
-  k_gauss_offsets<<<1, 1, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
+  k_gauss_offsets<<<1, 1024, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -574,6 +583,14 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->bstride = (size_t)((c->Wmax + 31) / 32) * c->Hmax;
   c->dstride = (size_t)dbits_wpw(c->Wmax + 2) * (c->Hmax + 2);
   c->pool_cap = cfg.max_contour_points;
+  {
+    // dynamic LDS budget of k_trace_borders_lds: 160 KB minus its static LUT
+    c->trace_lds_max = 160 * 1024 - 512 * 8 - 64;
+    c->trace_lds_ok = hipFuncSetAttribute((const void*)k_trace_borders_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)c->trace_lds_max) == hipSuccess;
+    const char* e = getenv("MANTIS_TRACE_LDS_FRAMES");
+    c->trace_lds_frames = e ? atoi(e) : c->n_cu / 4;
+  }
   if (morph_lds(c->Wmax) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize, (int)morph_lds(c->Wmax)) !=
           hipSuccess) {

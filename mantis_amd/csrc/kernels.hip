@@ -1070,6 +1070,50 @@ __global__ __launch_bounds__(256) void k_trace_borders(const uint32_t* __restric
   }
 }
 
+// Latency variant of k_trace_borders for small batches: one 1024-thread block
+// per frame stages the padded bit plane in LDS (when it fits), so each step of
+// a walk waits on an LDS read instead of an L2 round trip -- the longest walk of
+// a frame is on the per-rig latency path.
+extern __shared__ uint32_t tb_lds[];
+struct BitsNBLds {
+  int wpw;
+  __device__ uint32_t row3(int x, int y) const {
+    const int o = y * wpw + ((x - 1) >> 5);
+    const uint64_t v = ((uint64_t)tb_lds[o + 1] << 32) | tb_lds[o];
+    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  }
+  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
+};
+__global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                            const Border* __restrict__ borders, FrameState* st,
+                                                            int32_t* __restrict__ counts,
+                                                            int32_t* __restrict__ scratch, int pool_cap, int Wp,
+                                                            int Hp, int border_cap) {
+  __shared__ uint8_t next_lut[512 * 8];
+  const int f = blockIdx.x;
+  build_next_lut(next_lut, threadIdx.x, blockDim.x);
+  const int wpw = dbits_wpw(Wp);
+  const uint32_t* B = dbits + (size_t)f * dstride;
+  for (int k = threadIdx.x; k < wpw * Hp; k += blockDim.x) tb_lds[k] = B[k];
+  __syncthreads();
+  int nb = st[f].n_borders;
+  if (nb > border_cap) nb = border_cap;
+  const Border* bs = borders + (size_t)f * border_cap;
+  int32_t* cnt = counts + (size_t)f * border_cap;
+  int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
+  const int max_chunks = pool_cap / kChunk;
+  int32_t* chunks = sc;
+  int32_t* owner = sc + 2 * (size_t)pool_cap;
+  int32_t* ordv = owner + max_chunks;
+  const BitsNBLds nbh{wpw};
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const Border b = bs[i];
+    ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, i, -1, 0, 0, false};
+    cnt[i] = trace_border_lut(nbh, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em, &st[f].trace_steps_max);
+    if (em.ovf) atomicOr(&st[f].overflow, 2);
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_frame_contours(const uint32_t* __restrict__ dbits, size_t dstride,
                                                          const Border* __restrict__ borders,
                                                          FrameState* st, int32_t* __restrict__ counts,
@@ -1626,14 +1670,29 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
 
 // prefix over frames: draws of the shared cv::RNG stream happen only for
 // frames that reach the particle filter, in frame order
-__global__ void k_gauss_offsets(FrameState* st, int nf, int per_frame, int32_t* total) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int acc = 0;
-  for (int f = 0; f < nf; f++) {
+// (one 1024-thread block: per-thread serial chunk, wave scans, block scan)
+__global__ __launch_bounds__(1024) void k_gauss_offsets(FrameState* st, int nf, int per_frame, int32_t* total) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int chunk = (nf + 1023) / 1024;
+  const int f0 = min(nf, t * chunk), f1 = min(nf, f0 + chunk);
+  int mine = 0;
+  for (int f = f0; f < f1; f++) mine += st[f].reaches_pf ? per_frame : 0;
+  int incl = mine;  // inclusive scan over the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wave; w++) base += wsum[w];
+  int acc = base + incl - mine;
+  for (int f = f0; f < f1; f++) {
     st[f].gauss_offset = acc;
     if (st[f].reaches_pf) acc += per_frame;
   }
-  *total = acc;
+  if (t == 1023) *total = base + incl;
 }
 
 // ============================================================== scoring

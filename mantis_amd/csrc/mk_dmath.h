@@ -23,6 +23,9 @@ namespace dm {
 // turn it back into VGPR literal moves.
 template <unsigned long long B>
 __device__ inline double sk() {
+#ifdef MK_DM_LITERAL_CONSTANTS  // A/B builds: let the compiler place the constants
+  return __longlong_as_double((long long)B);
+#endif
   unsigned lo, hi;
   asm("s_mov_b32 %0, %1" : "=s"(lo) : "i"((unsigned)(B & 0xffffffffu)));
   asm("s_mov_b32 %0, %1" : "=s"(hi) : "i"((unsigned)(B >> 32)));
