@@ -333,19 +333,17 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   // bit planes: candidates, strong tile roots (4 words per tile row)
   const int WW = bits::words(W);
   const size_t ob = (size_t)f * bstride;
-  if (t < FTH * (FTW / 32)) {
-    const int ly = t / (FTW / 32), wi = t % (FTW / 32);
-    const int y = y0 + ly, w = (x0 >> 5) + wi;
-    if (y < H && w < WW) {
-      uint32_t cw = 0, rw = 0;
-      const int i0 = ly * FTW + 32 * wi;
-#pragma unroll 8
-      for (int b = 0; b < 32; b++) {
-        cw |= (uint32_t)(K[i0 + b] != 0) << b;
-        rw |= (uint32_t)(S[i0 + b] != 0) << b;
+  // (a wave covers 64 consecutive pixels of one tile row: two ballots give
+  // two words per plane)
+  for (int i = t; i < FTW * FTH; i += 256) {
+    const uint64_t cm = __ballot(K[i] != 0), rm = __ballot(S[i] != 0);
+    const int lane = t & 63;
+    if ((lane & 31) == 0) {
+      const int y = y0 + i / FTW, w = (x0 + i % FTW) >> 5;
+      if (y < H && w < WW) {
+        cbits[ob + (size_t)y * WW + w] = (uint32_t)(cm >> lane);
+        rbits[ob + (size_t)y * WW + w] = (uint32_t)(rm >> lane);
       }
-      cbits[ob + (size_t)y * WW + w] = cw;
-      rbits[ob + (size_t)y * WW + w] = rw;
     }
   }
   // per-pixel tile root (0xffff: not a candidate); sparse labels: tile roots
@@ -448,18 +446,13 @@ __global__ __launch_bounds__(256) void k_hyst_edge(const uint16_t* __restrict__ 
     if (r == i) Fl[i] = sg[uf_find_c(l, y * W + x)];
   }
   __syncthreads();
-  if (t < FTH * (FTW / 32)) {
-    const int ly = t / (FTW / 32), wi = t % (FTW / 32);
-    const int y = y0 + ly, w = (x0 >> 5) + wi;
-    if (y < H && w < WW) {
-      uint32_t ew = 0;
-      const int i0 = ly * FTW + 32 * wi;
-#pragma unroll 8
-      for (int b = 0; b < 32; b++) {
-        const uint16_t r = R[i0 + b];
-        ew |= (uint32_t)(r != 0xffff && Fl[r]) << b;
-      }
-      ebits[ob + (size_t)y * WW + w] = ew;
+  for (int i = t; i < FTW * FTH; i += 256) {  // ballot per 64 pixels of a tile row
+    const uint16_t r = R[i];
+    const uint64_t em = __ballot(r != 0xffff && Fl[r]);
+    const int lane = t & 63;
+    if ((lane & 31) == 0) {
+      const int y = y0 + i / FTW, w = (x0 + i % FTW) >> 5;
+      if (y < H && w < WW) ebits[ob + (size_t)y * WW + w] = (uint32_t)(em >> lane);
     }
   }
   if (edge) {
@@ -1774,7 +1767,10 @@ __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
 // HypothesisEvaluation.h:218-227 on the cleaned image): the squared distance
 // of its BGR to white, or 3 * 255^2 when the pixel is masked out or lies past
 // the end of the buffer (linear-offset read of cvRound(px) == W / == H).
-constexpr int kFastUnroll = 4;
+#ifndef MK_FAST_UNROLL
+#define MK_FAST_UNROLL 3
+#endif
+constexpr int kFastUnroll = MK_FAST_UNROLL;
 template <class MK>
 __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
                                        const MK& mask, int W, int H, double* err_out, int* n_out) {
@@ -1834,47 +1830,84 @@ __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, 
   }
 }
 
-// COLOR (slow) error of one hypothesis, green landmarks, 10x10 window;
-// lanes take landmarks, lane 0 sums the per-landmark means in map order.
+// COLOR (slow) error of one hypothesis (computePointError, HypothesisEvaluation.h:
+// 233-266): for each green landmark with z > 0 in frame, the mean over the
+// 10 x 10 window cvRound(px + ox, py + oy), o in -5..4 (no bounds check:
+// linear offset, out-of-buffer reads 0), of the squared BGR
+// distance to GREEN (50, 255, 85); the error is the sum of the means in map
+// order / (n * 1.1). One wave per hypothesis: lanes project the landmarks
+// once, then take (landmark, window row) items -- ten independent pixel
+// gathers each -- and add their integer row sums into the landmark's LDS
+// accumulator (the window sum is an exact integer, so its order is free);
+// lane 0 sums the means in landmark order.
+struct ColorLds {
+  double u[64], v[64];
+  int32_t acc[64], ok[64];
+};
 __device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
-                                        const uint8_t* bgr, int W, int H, double* sh_terms, double* err_out,
+                                        const uint8_t* bgr, int W, int H, ColorLds* cl, double* err_out,
                                         int* n_out) {
   const int lane = threadIdx.x & 63;
+  const long npx = (long)W * H;
+  double total = 0;
+  int n = 0;
   for (int base = 0; base < ngr; base += 64) {
-    int l = base + lane;
-    double term = -1.0;
-    if (l < ngr) {
-      double rp[3];
-      xf_apply(c2w, green + 3 * l, rp);
-      if (rp[2] > 0) {
-        double u, v;
+    const int nb = min(64, ngr - base);
+    {
+      const int l = base + lane;
+      int ok = 0;
+      double u = 0, v = 0;
+      if (lane < nb) {
+        double rp[3];
+        xf_apply(c2w, green + 3 * l, rp);
         distort(cm, rp[0], rp[1], rp[2], &u, &v);
-        if (in_frame(u, v, H, W)) {
-          double err = 0;
-          for (double ox = -5.0; ox < 5.0; ox += 1)
-            for (double oy = -5.0; oy < 5.0; oy += 1) {
-              int b, g, r;
-              fetch_px(bgr, MaskNone{}, W, H, cv_round(u + ox), cv_round(v + oy), b, g, r);
-              int e0 = b - 50, e1 = g - 255, e2 = r - 85;
-              err += (double)(e0 * e0 + e1 * e1 + e2 * e2);
-            }
-          term = err / (double)(10 * 10);
-        }
+        ok = rp[2] > 0 && in_frame(u, v, H, W);
       }
+      cl->u[lane] = u;
+      cl->v[lane] = v;
+      cl->ok[lane] = ok;
+      cl->acc[lane] = 0;
     }
-    if (l < ngr) sh_terms[l] = term;
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    for (int k = lane; k < nb * 10; k += 64) {
+      const int li = k / 10, r = k - 10 * li;
+      if (!cl->ok[li]) continue;
+      const double u = cl->u[li];
+      const int y = cv_round(cl->v[li] + (-5.0 + (double)r));
+      int rs = 0;
+#pragma unroll
+      for (int ox = 0; ox < 10; ox++) {
+        const int x = cv_round(u + (-5.0 + (double)ox));
+        const long lin = (long)y * W + x;
+        int b = 0, g = 0, rr = 0;
+        if (lin >= 0 && lin < npx) {
+          const uint32_t pv = load_bgr(bgr, lin, npx);
+          b = (int)(pv & 0xffu);
+          g = (int)((pv >> 8) & 0xffu);
+          rr = (int)((pv >> 16) & 0xffu);
+        }
+        const int e0 = b - 50, e1 = g - 255, e2 = rr - 85;
+        rs += e0 * e0 + e1 * e1 + e2 * e2;
+      }
+      atomicAdd(&cl->acc[li], rs);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    if (lane == 0) {
+      for (int l = 0; l < nb; l++)
+        if (cl->ok[l]) {
+          total += (double)cl->acc[l] / (double)(10 * 10);
+          n++;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
   }
-  __builtin_amdgcn_wave_barrier();
-  __threadfence_block();
   if (lane == 0) {
-    double total = 0;
-    int n = 0;
-    for (int l = 0; l < ngr; l++)
-      if (sh_terms[l] >= 0) { total += sh_terms[l]; n++; }
     *n_out = n;
     *err_out = n <= 0 ? DBL_MAX : total / ((double)n * 1.1);
   }
-  __builtin_amdgcn_wave_barrier();
 }
 
 // Scoring is three kernels per frame batch (one block per frame each), so
@@ -2086,7 +2119,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
   __shared__ double lm[3 * 768];
   __shared__ PoseLds P[96];
   __shared__ ErrIdx ei[96];
-  __shared__ double terms[kWaves][64];
+  __shared__ ColorLds cls[kWaves];
   __shared__ PoseLds cur;
   __shared__ double shv[9];
   __shared__ double yerr[4];
@@ -2154,7 +2187,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
     for (int j = wave; j < 20; j += kWaves) {
       double e;
       int n;
-      wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, terms[wave], &e, &n);
+      wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
       if (lane == 0) yset_err[j] = e;
     }
     __syncthreads();
@@ -2229,7 +2262,7 @@ __global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__
                                                    double* __restrict__ err, int32_t* __restrict__ nproj) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int h = blockIdx.x * 4 + wave;
-  __shared__ double terms[4][64];
+  __shared__ ColorLds cls[4];
   if (h >= n) return;
   const FrameDesc fd = frames[0];
   Xf T;
@@ -2240,7 +2273,7 @@ __global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   if (fast && mask) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskBytes{mask}, fd.w, fd.h, &e, &np);
   else if (fast) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskNone{}, fd.w, fd.h, &e, &np);
-  else wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, terms[wave], &e, &np);
+  else wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, &cls[wave], &e, &np);
   if (lane == 0) {
     err[h] = e;
     nproj[h] = np;
