@@ -1603,27 +1603,45 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
   }
   if (tid == 0) nclus = 0;
   __syncthreads();
+  // BFcluster (PoseClusterer.cpp:51-116): seeds in index order; the members
+  // within 1.5 r of the seed are found in parallel (ballot words), their
+  // float centre is summed by one thread in index order (float adds are
+  // order-sensitive) over the set bits only, then the members within r of the
+  // centre join the cluster in parallel.
+  __shared__ uint64_t hitw[kMaxHyps / 64];
+  __shared__ int32_t csz;
+  const int lane = tid & 63;
   for (int i = 0; i < n; i++) {
     if (cid[i] >= 0) continue;  // uniform: cid[] is shared and stable here
-    // neighbours within 1.5 * radius (double distance of float differences)
-    for (int j = tid; j < n; j += blockDim.x) {
+    for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+      const int j = j0 + tid;
       int hit = 0;
-      if (cid[j] < 0) {
+      if (j < n && cid[j] < 0) {
         double dx = ax[i] - ax[j], dy = ay[i] - ay[j], dz = az[i] - az[j];
         hit = sqrt(dx * dx + dy * dy + dz * dz) <= max_angle * 1.5;
       }
-      flag[j] = hit;
+      const uint64_t m = __ballot(hit);
+      if (lane == 0 && j0 + (tid & ~63) < n) hitw[(j0 + (tid & ~63)) >> 6] = m;
     }
+    if (tid == 0) csz = 0;
     __syncthreads();
     if (tid == 0) {
       float cx = 0, cy = 0, cz = 0;
       int cntm = 0;
-      for (int j = 0; j < n; j++)
-        if (flag[j]) { cx += ax[j]; cy += ay[j]; cz += az[j]; cntm++; }
+      for (int w = 0; w < (n + 63) / 64; w++) {
+        uint64_t m = hitw[w];
+        while (m) {
+          const int j = 64 * w + __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          cx += ax[j]; cy += ay[j]; cz += az[j];
+          cntm++;
+        }
+      }
       double sz = (double)cntm;
       cen[0] = (float)(cx / sz); cen[1] = (float)(cy / sz); cen[2] = (float)(cz / sz);
     }
     __syncthreads();
+    const int c = nclus;
     for (int j = tid; j < n; j += blockDim.x) {
       int hit = 0;
       if (cid[j] < 0) {
@@ -1633,11 +1651,15 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
       flag[j] = hit;
     }
     __syncthreads();
+    for (int j = tid; j < n; j += blockDim.x) {
+      if (flag[j]) {
+        cid[j] = c;
+        atomicAdd(&csz, 1);
+      }
+    }
+    __syncthreads();
     if (tid == 0) {
-      int c = nclus, s = 0;
-      for (int j = 0; j < n; j++)
-        if (flag[j]) { cid[j] = c; s++; }
-      csize[c] = s;
+      csize[c] = csz;
       nclus = c + 1;
     }
     __syncthreads();
