@@ -2020,12 +2020,36 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_init(
     }
   }
   __syncthreads();
-  // getBestNHypotheses(1): std::sort, keep back()
+  // getBestNHypotheses(1): std::sort, keep back(). When the minimum error is
+  // unique, back() is that element whatever the sort's tie order, so wave 0
+  // finds it with a reduction and the serial sort runs only on ties.
+  __shared__ int32_t uniq_bi;
+  if (wave == 0) {
+    double be = DBL_MAX;
+    int bj = 0x7fffffff, cnt = 0;
+    for (int h = lane; h < C; h += 64) {
+      const double e = ei[h].e;
+      if (e < be || bj == 0x7fffffff) { be = e; bj = h; cnt = 1; }
+      else if (e == be) cnt++;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double oe = __shfl_xor(be, o);
+      const int oj = __shfl_xor(bj, o), oc = __shfl_xor(cnt, o);
+      if (oe < be) { be = oe; bj = oj; cnt = oc; }
+      else if (oe == be) { cnt += oc; if (oj < bj) bj = oj; }
+    }
+    if (lane == 0) uniq_bi = cnt == 1 ? bj : -1;
+  }
+  __syncthreads();
   if (tid == 0) {
     int bi = 0;
     if (C > 1) {
-      std_sort_desc(ei, ei + C);
-      bi = ei[C - 1].i;
+      if (uniq_bi >= 0) {
+        bi = uniq_bi;
+      } else {
+        std_sort_desc(ei, ei + C);
+        bi = ei[C - 1].i;
+      }
     }
     cur.c2w = Hh[bi].c2w; cur.w2c = Hh[bi].w2c; cur.q = Hh[bi].q; cur.err = Hh[bi].error;
     for (int k = 0; k < 9; k++) D.best1_c2w[k] = cur.c2w.R[k];
@@ -2175,10 +2199,35 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
     if (lane == 0) { P[j].err = e; ei[j].e = e; ei[j].i = j; D.shift_err[j] = e; }
   }
   __syncthreads();
+  // getBestNHypotheses(20) (HypothesisEvaluation.h:484-518): std::sort by
+  // descending error, keep the last 20. When the 20 smallest errors are all
+  // distinct from every other error, their sorted positions follow from
+  // their ranks (no tie order involved); otherwise tid 0 runs the
+  // libstdc++-order sort.
   __shared__ int32_t top[20];
+  __shared__ int32_t tie20;
+  if (tid == 0) tie20 = 0;
+  __syncthreads();
+  if (tid < NS) {
+    const double e = ei[tid].e;
+    int lt = 0, eq = 0;
+    for (int j = 0; j < NS; j++) {
+      const double o = ei[j].e;
+      lt += o < e;
+      eq += o == e;
+    }
+    if (lt < 20) {
+      if (eq != 1) tie20 = 1;
+      else top[19 - lt] = tid;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {
-    std_sort_desc(ei, ei + NS);
-    for (int k = 0; k < 20; k++) { top[k] = ei[NS - 20 + k].i; D.top20_err[k] = ei[NS - 20 + k].e; }
+    if (tie20) {
+      std_sort_desc(ei, ei + NS);
+      for (int k = 0; k < 20; k++) top[k] = ei[NS - 20 + k].i;
+    }
+    for (int k = 0; k < 20; k++) D.top20_err[k] = P[top[k]].err;
     nsc += NS;
   }
   __syncthreads();
