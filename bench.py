@@ -213,7 +213,7 @@ def main():
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
 
-    def roofline(stage):
+    def roofline(stage, avg=avg):
         if stage not in avg or stage not in work:
             return None
         kind, amount = work[stage]
@@ -244,6 +244,21 @@ def main():
         roof["stages_ms"] = {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}
         roof["objpose_iterations_per_launch"] = iters
     roof_front = roofline("canny_nms")
+
+    # ---- the same stages with context 0 running alone (one step, after the
+    # timed region): the timed-region launch durations above include the
+    # other contexts' kernels sharing the CUs; these are the kernels' own
+    if nctx > 1 and roof is not None:
+        m.set_profiling(True)
+        ctxs[0].process(per_ctx[0], rigs_ctx)
+        iso = {k: v for k, v in m.kernel_times()}
+        m.set_profiling(False)
+        for r, stg in ((roof, dom), (roof_front, "canny_nms")):
+            ri = roofline(stg, iso) if r is not None else None
+            if ri is not None:
+                r["isolated"] = {"avg_launch_ms": ri["avg_launch_ms"], "achieved": ri["achieved"], "frac": ri["frac"],
+                                 "note": "context 0 alone, one step after the timed region"}
+        roof["stages_ms_isolated"] = {k: round(v, 4) for k, v in sorted(iso.items(), key=lambda kv: -kv[1])}
     path_bytes = n_frames * (6 * W * H + 3 * (s_fast + s_slow))
 
     # ---- p50 latency of one rig (host submit -> result on host)

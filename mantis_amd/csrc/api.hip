@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <chrono>
 #include <cmath>
@@ -143,6 +144,7 @@ struct Ctx {
   int32_t *d_jobs0 = nullptr, *d_jobs1 = nullptr;  // RPP ObjPose job queues
   RppQueue* d_rq = nullptr;
   int rpp_blocks = 0;
+  bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
   double *d_dense_c2w = nullptr, *d_dense_err = nullptr, *d_pairs = nullptr;
@@ -303,11 +305,21 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   return MANTIS_OK;
 }
 
+// Live contexts per device in this process: the persistent ObjPose lanes are
+// latency-bound (a long dependent FP64 chain per lane), and at 224 VGPRs two
+// resident blocks per CU hold most of its register file, so with several
+// contexts sharing a GPU each takes a proportional share of the CUs and
+// leaves the rest to the other contexts' kernels (3 contexts: +5 % rig
+// poses/s over filling every CU, bench sweep in DESIGN.md).
+std::atomic<int> g_live_ctx[64];
+
 // Grid of a persistent ObjPose launch: enough lanes for ~2 jobs each at the
-// typical ~150 items per frame, at most rpp_blocks (MANTIS_RPP_BLOCKS) blocks.
+// typical ~150 items per frame, at most 1.5 * CUs / (live contexts on the
+// device) blocks (MANTIS_RPP_BLOCKS overrides).
 unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
   size_t b = (expected_jobs + 511) / 512;
-  const size_t cap = c->rpp_blocks > 0 ? (size_t)c->rpp_blocks : 1024;
+  const int live = std::max(1, g_live_ctx[c->cfg.device & 63].load());
+  const size_t cap = c->rpp_blocks > 0 ? (size_t)c->rpp_blocks : (size_t)std::max(64, 3 * c->n_cu / (2 * live));
   return (unsigned)std::max<size_t>(1, std::min(b, cap));
 }
 
@@ -656,6 +668,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     mantis_destroy(c);
     return MANTIS_ERR_DEVICE;
   }
+  g_live_ctx[cfg.device & 63].fetch_add(1);
+  c->counted = true;
   *out_ctx = c;
   return MANTIS_OK;
 }
@@ -664,6 +678,7 @@ mantis_status mantis_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (c) bind_device(c);
   if (!c) return MANTIS_ERR_ARG;
+  if (c->counted) g_live_ctx[c->cfg.device & 63].fetch_sub(1);
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_rowb,
