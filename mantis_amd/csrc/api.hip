@@ -327,7 +327,8 @@ void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, 
                        RppOut* out, FrameState* st, size_t ni, size_t expected_items) {
   k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q, st);
   mark(c, "rpp_first");
-  k_rpp_s1b<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, jobs1, q);
+  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
+      items, jobs0, jobs1, q);
   mark(c, "rpp_2nd");
   k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st);
   mark(c, "rpp_cand");

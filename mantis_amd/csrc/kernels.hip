@@ -1487,20 +1487,26 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
 }
 
 // Get2ndPose setup (candidate rotations from the quartic) per active item;
-// every candidate that enters the search becomes a MODE-1 job
-__global__ __launch_bounds__(256) void k_rpp_s1b(RppItem* __restrict__ items, size_t n_items,
-                                                 int32_t* __restrict__ jobs1, RppQueue* q) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items || !items[i].active) return;
-  double model[12];
+// every candidate that enters the search becomes a MODE-1 job. One wave per
+// block over the first-ObjPose job list (the active items only): the stage
+// needs ~390 registers per lane, so a 64-thread block fits on one SIMD
+// instead of waiting for a whole CU to drain.
+__global__ __launch_bounds__(64) void k_rpp_s1b(RppItem* __restrict__ items, const int32_t* __restrict__ jobs0,
+                                                int32_t* __restrict__ jobs1, RppQueue* q) {
+  const int n0 = q->n0;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n0; k += gridDim.x * blockDim.x) {
+    const int32_t i = jobs0[k];
+    if (!items[i].active) continue;
+    double model[12];
 #pragma unroll
-  for (int k = 0; k < 12; k++) model[k] = items[i].P[k];
-  rpp::stage1b(model, items[i].s);
-  const int m = items[i].s.error == 1 ? 0 : items[i].s.keep_mask;
-  if (m) {
-    int b = atomicAdd(&q->n1, __popc(m));
-    for (int j = 0; j < rpp::kCand; j++)
-      if ((m >> j) & 1) jobs1[b++] = (int32_t)(i * rpp::kCand + j);
+    for (int j = 0; j < 12; j++) model[j] = items[i].P[j];
+    rpp::stage1b(model, items[i].s);
+    const int m = items[i].s.error == 1 ? 0 : items[i].s.keep_mask;
+    if (m) {
+      int b = atomicAdd(&q->n1, __popc(m));
+      for (int j = 0; j < rpp::kCand; j++)
+        if ((m >> j) & 1) jobs1[b++] = (int32_t)(i * rpp::kCand + j);
+    }
   }
 }
 
