@@ -282,7 +282,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   dim3 grow((Hp + 3) / 4, n);
   uint16_t* rx = c->d_lroot;  // free after hysteresis: run starts (u16, one run per pixel at most)
   k_run_count<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, Wp, Hp);
-  k_run_scan<<<n, 1024, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
+  k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
   k_run_emit<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
   k_run_union<<<dim3((Hp + 2) / 4, n), 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
   k_run_border<<<grow, 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, c->d_borders, c->d_st, Wp, Hp,
@@ -296,7 +296,9 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
     k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
                                                   c->d_scratch, c->pool_cap, Wp, kMaxBorders);
   mark(c, "border_trace");
-  k_frame_contours<<<n, 1024, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
+  // small batches (latency): 1024 threads per frame; large ones: 256, so the
+  // per-frame blocks fit beside other contexts' kernels on a CU
+  k_frame_contours<<<n, n <= c->trace_lds_frames ? 1024 : 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
                                          c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
                                          Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon,
                                          c->cfg.search_radius_multiplier);

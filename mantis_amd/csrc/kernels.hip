@@ -686,12 +686,12 @@ __global__ __launch_bounds__(256) void k_run_count(const uint32_t* __restrict__ 
   if (lane == 0) rowb[(size_t)f * rstride + y] = c + 1;
 }
 
-__global__ __launch_bounds__(1024) void k_run_scan(int32_t* __restrict__ rowb, size_t rstride, FrameState* st,
+__global__ __launch_bounds__(256) void k_run_scan(int32_t* __restrict__ rowb, size_t rstride, FrameState* st,
                                                    int Hp) {
-  __shared__ int32_t wsum[16];
+  __shared__ int32_t wsum[4];  // 256 threads: fits beside other contexts' kernels
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int32_t* r = rowb + (size_t)f * rstride;
-  const int per = (Hp + 1023) / 1024, y0 = t * per;
+  const int per = (Hp + 255) / 256, y0 = t * per;
   int loc = 0;
   for (int k = 0; k < per; k++)
     if (y0 + k < Hp) loc += r[y0 + k];
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(1024) void k_run_scan(int32_t* __restrict__ rowb, s
       r[y0 + k] = acc;
       acc += v;
     }
-  if (t == 1023) {
+  if (t == 255) {
     r[Hp] = acc;
     st[f].n_runs = acc;
   }
