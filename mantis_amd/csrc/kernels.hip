@@ -88,7 +88,10 @@ __device__ inline void lds_union(int* L, int a, int b) {
 //   k_hyst_mark  strong tile roots mark their global root
 //   k_hyst_edge  per tile: the same LDS union-find again; edge = candidate
 //                whose global root is marked (bit plane, bytes on request)
-constexpr int FTW = 128, FTH = 16;            // front-end tile
+#ifndef MK_FTH
+#define MK_FTH 16
+#endif
+constexpr int FTW = 128, FTH = MK_FTH;         // front-end tile
 constexpr int FSEG = FTW * FTH / 256;          // pixels per thread-run in the tile union-find
 constexpr int FGW = FTW + 8, FGH = FTH + 6;    // gray tile: x0-4 .. x0+FTW+3 (4-aligned), y0-3 .. y0+FTH+2
 constexpr int FRW = FTW + 4;                   // blurred columns x0-2 .. x0+FTW+1
@@ -160,6 +163,94 @@ __device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* coun
   return n;
 }
 
+// Interior tiles, four horizontally adjacent pixels per work-item: every
+// stencil stage reads aligned dwords / qwords of LDS rows and writes one, so
+// the per-pixel byte gathers and index arithmetic of the generic path go. All
+// interior buffers share the gray tile's columns (x0-4 .. x0+FTW+3, FGW = 136
+// = 34 groups of 4); columns outside a stage's valid range hold values that
+// no later stage reads. Integer arithmetic as the generic path (the
+// [84,89,84] sums are exact, so 84(a+c) + 89b is the same number).
+constexpr int FG4 = FGW / 4;  // 4-pixel groups per interior row
+static_assert(FGW % 4 == 0 && FGH * FGW * 2 <= 2 * FTW * FTH * 2, "interior blur rows fit the gradient buffer");
+__device__ inline uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; }
+// horizontal blur of gray rows 0 .. FGH-1 into hb (u16, FGH x FGW)
+__device__ inline void hblur4(const uint8_t* g, uint16_t* hb, int t) {
+  for (int u = t; u < FGH * FG4; u += 256) {
+    const int ly = u / FG4, k = u - ly * FG4;
+    const uint32_t* row = (const uint32_t*)(g + ly * FGW);
+    const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
+    uint32_t b[6];
+    b[0] = wp >> 24;
+#pragma unroll
+    for (int j = 0; j < 4; j++) b[1 + j] = byte_of(wc, j);
+    b[5] = wn & 0xffu;
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) o[j] = 84u * (b[j] + b[j + 2]) + 89u * b[j + 1];
+    *(uint2*)(hb + ly * FGW + 4 * k) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
+  }
+}
+// vertical blur: bl rows 0 .. FTH+3 (image rows y0-2 ..) from hb rows ly .. ly+2
+__device__ inline void vblur4(const uint16_t* hb, uint8_t* bl, int t) {
+  constexpr int BLH = FTH + 4;
+  for (int u = t; u < BLH * FG4; u += 256) {
+    const int ly = u / FG4, k = u - ly * FG4;
+    const uint2 a = *(const uint2*)(hb + ly * FGW + 4 * k);
+    const uint2 b = *(const uint2*)(hb + (ly + 1) * FGW + 4 * k);
+    const uint2 c = *(const uint2*)(hb + (ly + 2) * FGW + 4 * k);
+    const uint32_t av[4] = {a.x & 0xffffu, a.x >> 16, a.y & 0xffffu, a.y >> 16};
+    const uint32_t bv[4] = {b.x & 0xffffu, b.x >> 16, b.y & 0xffffu, b.y >> 16};
+    const uint32_t cv[4] = {c.x & 0xffffu, c.x >> 16, c.y & 0xffffu, c.y >> 16};
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t r = (84u * (av[j] + cv[j]) + 89u * bv[j] + (1u << 15)) >> 16;
+      w |= (r > 255u ? 255u : r) << (8 * j);
+    }
+    *(uint32_t*)(bl + ly * FGW + 4 * k) = w;
+  }
+}
+// Sobel + L1 magnitude on rows 0 .. FTH+1 (image rows y0-1 ..), all columns;
+// gx / gy kept for the tile's own pixels (rows 1 .. FTH, columns 4 .. FTW+3)
+__device__ inline void sobel4(const uint8_t* bl, int16_t* mag, int16_t* gx_s, int16_t* gy_s, int t) {
+  for (int u = t; u < (FTH + 2) * FG4; u += 256) {
+    const int ly = u / FG4, k = u - ly * FG4;
+    int s[3][4], d[3][4];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const uint32_t* row = (const uint32_t*)(bl + (ly + r) * FGW);
+      const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
+      int b[6];
+      b[0] = (int)(wp >> 24);
+#pragma unroll
+      for (int j = 0; j < 4; j++) b[1 + j] = (int)byte_of(wc, j);
+      b[5] = (int)(wn & 0xffu);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        s[r][j] = b[j] + 2 * b[j + 1] + b[j + 2];  // l + 2m + q
+        d[r][j] = b[j + 2] - b[j];                 // q - l
+      }
+    }
+    int m[4], gxv[4], gyv[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      gxv[j] = d[0][j] + 2 * d[1][j] + d[2][j];
+      gyv[j] = s[2][j] - s[0][j];
+      m[j] = abs(gxv[j]) + abs(gyv[j]);
+    }
+    *(uint2*)(mag + ly * FGW + 4 * k) =
+        make_uint2((uint32_t)(uint16_t)m[0] | ((uint32_t)(uint16_t)m[1] << 16),
+                   (uint32_t)(uint16_t)m[2] | ((uint32_t)(uint16_t)m[3] << 16));
+    if (ly >= 1 && ly <= FTH && k >= 1 && k <= FTW / 4) {
+      const int jj = (ly - 1) * FTW + 4 * (k - 1);
+      *(uint2*)(gx_s + jj) = make_uint2((uint32_t)(uint16_t)gxv[0] | ((uint32_t)(uint16_t)gxv[1] << 16),
+                                        (uint32_t)(uint16_t)gxv[2] | ((uint32_t)(uint16_t)gxv[3] << 16));
+      *(uint2*)(gy_s + jj) = make_uint2((uint32_t)(uint16_t)gyv[0] | ((uint32_t)(uint16_t)gyv[1] << 16),
+                                        (uint32_t)(uint16_t)gyv[2] | ((uint32_t)(uint16_t)gyv[3] << 16));
+    }
+  }
+}
+
 // The Canny stages of one tile into K (classes). IN: the tile and its halo
 // (x0-4 .. x0+FTW+3, y0-3 .. y0+FTH+2) lie inside the image and the rows
 // allow dword loads, so the border rules (reflect/replicate/zero) drop out.
@@ -200,6 +291,14 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     }
   }
   __syncthreads();
+  if (IN) {
+    hblur4(g, (uint16_t*)gxy, t);
+    __syncthreads();
+    vblur4((const uint16_t*)gxy, bl, t);
+    __syncthreads();
+    sobel4(bl, mag, gx_s, gy_s, t);
+    __syncthreads();
+  } else {
   // horizontal blur on rows y0-3 .. y0+FTH+2, columns x0-2 .. x0+FTW+1
   // (BORDER_REFLECT_101); staged in the gradient buffer, not live yet
   uint16_t* rowb = (uint16_t*)gxy;  // FGH * FRW <= 2 * FTW * FTH
@@ -257,7 +356,10 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     mag[i] = (int16_t)m;
   }
   __syncthreads();
-  // NMS -> classes (0 none, 1 weak candidate, 2 strong)
+  }
+  // NMS -> classes (0 none, 1 weak candidate, 2 strong); magnitude pitch and
+  // column offset of the tile's pixels: interior FGW / 4, generic FMW / 1
+  constexpr int MP = IN ? FGW : FMW, MO = IN ? 4 : 1;
   const int SHIFT = 15;
   const int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
   for (int i = t; i < FTW * FTH; i += 256) {
@@ -265,8 +367,8 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     const int x = x0 + lx, y = y0 + ly;
     uint8_t c = 0;
     if (IN || (x < W && y < H)) {
-      const int cy = ly + 1, cx = lx + 1;
-      const int m = mag[cy * FMW + cx];
+      const int cy = ly + 1, cx = lx + MO;
+      const int m = mag[cy * MP + cx];
       if (m > low) {
         const int xs = gx_s[i], ys = gy_s[i];
         const int ax = abs(xs);
@@ -274,14 +376,14 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
         const int tg22x = ax * TG22;
         bool push;
         if (ay < tg22x) {
-          push = m > mag[cy * FMW + cx - 1] && m >= mag[cy * FMW + cx + 1];
+          push = m > mag[cy * MP + cx - 1] && m >= mag[cy * MP + cx + 1];
         } else {
           const int tg67x = tg22x + (ax << (SHIFT + 1));
           if (ay > tg67x) {
-            push = m > mag[(cy - 1) * FMW + cx] && m >= mag[(cy + 1) * FMW + cx];
+            push = m > mag[(cy - 1) * MP + cx] && m >= mag[(cy + 1) * MP + cx];
           } else {
             const int sg = (xs ^ ys) < 0 ? -1 : 1;
-            push = m > mag[(cy - 1) * FMW + cx - sg] && m > mag[(cy + 1) * FMW + cx + sg];
+            push = m > mag[(cy - 1) * MP + cx - sg] && m > mag[(cy + 1) * MP + cx + sg];
           }
         }
         if (push) c = (m > high) ? 2 : 1;
@@ -310,9 +412,11 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   //   R2: blurred (x0-2 .., y0-2 ..)
   //   R3: horizontal blur -> gx | gy of the tile -> union-find labels
   constexpr int BLH = FTH + 4;                     // blurred rows y0-2 .. y0+FTH+1
-  constexpr int R1 = FMH * FMW * 2 > FGH * FGW ? FMH * FMW * 2 : FGH * FGW;
-  __shared__ __align__(16) uint8_t r1[R1 > FTW * FTH * 2 ? R1 : FTW * FTH * 2];
-  __shared__ uint8_t bl[BLH * FRW];
+  // (interior tiles: magnitude FMH x FGW int16, blurred BLH x FGW bytes)
+  constexpr int R1a = FMH * FGW * 2 > FGH * FGW ? FMH * FGW * 2 : FGH * FGW;
+  constexpr int R1 = R1a > FTW * FTH * 2 ? R1a : FTW * FTH * 2;
+  __shared__ __align__(16) uint8_t r1[R1];
+  __shared__ __align__(16) uint8_t bl[BLH * FGW];
   __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];
   __shared__ uint8_t K[FTW * FTH], S[FTW * FTH];
   __shared__ int ncount;
