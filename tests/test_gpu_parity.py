@@ -200,3 +200,45 @@ def test_full_pipeline_matches_oracle(mantis, frames, landmark_map):
         assert cams[i].reason == o.reason
         assert cams[i].publish == o.publish
     assert mantis.rng_state == orc.rng_state, "cv::RNG stream must advance exactly as the reference's"
+
+
+def test_throughput_mode_kernels_match_latency_mode(frames, landmark_map):
+    """Large batches take other kernel shapes (border walks from L2 instead of an
+    LDS copy of the bit plane, 256-thread contour blocks): force them on a small
+    batch (MANTIS_TRACE_LDS_FRAMES=0) and compare everything against the
+    latency-mode context (itself checked against the oracle above)."""
+    import os
+
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    imgs = [M.make_image(fr[0], K, D) for fr in frames[:4]]
+    old = os.environ.get("MANTIS_TRACE_LDS_FRAMES")
+    os.environ["MANTIS_TRACE_LDS_FRAMES"] = "0"
+    try:
+        mt = M.Mantis(max_cams=4, max_width=1280, max_height=720)
+    finally:
+        if old is None:
+            del os.environ["MANTIS_TRACE_LDS_FRAMES"]
+        else:
+            os.environ["MANTIS_TRACE_LDS_FRAMES"] = old
+    ml = M.Mantis(max_cams=4, max_width=1280, max_height=720)
+    try:
+        for m in (mt, ml):
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+        _, ct = mt.process(imgs)
+        _, cl = ml.process(imgs)
+        for f in range(len(imgs)):
+            gt, gl = mt.frame_debug(f), ml.frame_debug(f)
+            assert list(mt.frame_counters(f)[:2]) == list(ml.frame_counters(f)[:2])  # borders, points
+            assert gt.n_quads == gl.n_quads and gt.n_quads > 0
+            n = gt.n_quads
+            assert np.array_equal(np.array(gt.quads)[:n], np.array(gl.quads)[:n])
+            assert gt.pf_err == gl.pf_err and gt.n_hyps == gl.n_hyps
+            assert ct[f].reason == cl[f].reason and ct[f].publish == cl[f].publish
+            assert list(ct[f].position) == list(cl[f].position)
+        assert mt.rng_state == ml.rng_state
+    finally:
+        mt.close()
+        ml.close()
