@@ -11,7 +11,7 @@ CSRC = mantis_amd/csrc
 all: product tools oracle
 
 product: mantis_amd/libmantis_amd.so
-mantis_amd/libmantis_amd.so: $(CSRC)/api.hip $(CSRC)/kernels.hip $(CSRC)/gn_impl.hip $(CSRC)/dense_impl.hip $(wildcard $(CSRC)/*.h) include/mantis.h
+mantis_amd/libmantis_amd.so: $(CSRC)/api.hip $(CSRC)/kernels.hip $(CSRC)/gn_impl.hip $(CSRC)/dense_impl.hip $(wildcard $(CSRC)/*.h) include/mantis.h include/mantis_ros.h
 	$(HIPCC) $(HIPFLAGS) -shared -pthread -o $@ $(CSRC)/api.hip -lrccl
 
 tools: build/libmantis_hostcheck.so tools/libmantis_synth.so

@@ -122,6 +122,59 @@ _SIGS = {
 }
 
 
+# include/mantis_ros.h (ROS side of the drop-in; mirrored in mantis_amd/ros.py)
+class RosHeader(C.Structure):
+    _fields_ = [("seq", C.c_uint32), ("stamp_sec", C.c_uint32), ("stamp_nsec", C.c_uint32),
+                ("frame_id", C.c_void_p), ("frame_id_len", C.c_uint32)]
+
+
+class RosImage(C.Structure):
+    _fields_ = [("header", RosHeader), ("height", C.c_uint32), ("width", C.c_uint32), ("encoding", C.c_void_p),
+                ("encoding_len", C.c_uint32), ("is_bigendian", C.c_uint8), ("step", C.c_uint32),
+                ("data", C.c_void_p), ("data_len", C.c_uint32)]
+
+
+class RosCameraInfo(C.Structure):
+    _fields_ = [("header", RosHeader), ("height", C.c_uint32), ("width", C.c_uint32),
+                ("distortion_model", C.c_void_p), ("distortion_model_len", C.c_uint32), ("D_len", C.c_uint32),
+                ("D", C.c_double * 16), ("K", C.c_double * 9), ("R", C.c_double * 9), ("P", C.c_double * 12),
+                ("binning_x", C.c_uint32), ("binning_y", C.c_uint32), ("roi_x_offset", C.c_uint32),
+                ("roi_y_offset", C.c_uint32), ("roi_height", C.c_uint32), ("roi_width", C.c_uint32),
+                ("roi_do_rectify", C.c_uint8)]
+
+
+class RosPoseStamped(C.Structure):
+    _fields_ = [("seq", C.c_uint32), ("stamp_sec", C.c_uint32), ("stamp_nsec", C.c_uint32),
+                ("frame_id", C.c_char * 32), ("position", C.c_double * 3), ("orientation_xyzw", C.c_double * 4),
+                ("covariance", C.c_double * 36)]
+
+
+class RosServiceResponse(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("orientation_xyzw", C.c_double * 4), ("weight", C.c_double),
+                ("num_particles", C.c_int32)]
+
+
+_SIGS.update({
+    "mantis_ros_parse_image": (C.c_int64, [C.c_void_p, C.c_size_t, C.POINTER(RosImage)]),
+    "mantis_ros_parse_camera_info": (C.c_int64, [C.c_void_p, C.c_size_t, C.POINTER(RosCameraInfo)]),
+    "mantis_ros_parse_service_request": (C.c_int64, [C.c_void_p, C.c_size_t, C.POINTER(RosImage),
+                                                     C.POINTER(C.c_int32), C.POINTER(RosCameraInfo),
+                                                     C.POINTER(C.c_int32), C.c_int32, C.POINTER(MantisMotion)]),
+    "mantis_ros_write_pose": (C.c_int64, [C.POINTER(RosPoseStamped), C.c_void_p, C.c_size_t]),
+    "mantis_ros_write_service_response": (C.c_int64, [C.POINTER(RosServiceResponse), C.c_void_p, C.c_size_t]),
+    "mantis_ros_to_image": (C.c_int, [C.POINTER(RosImage), C.POINTER(RosCameraInfo), C.POINTER(MantisImage)]),
+    "mantis_ros_pose_from_result": (C.c_int32, [C.POINTER(MantisCamResult), C.POINTER(RosHeader), C.c_int32,
+                                                C.POINTER(RosPoseStamped)]),
+    "mantis_ros_service_response_from_result": (C.c_int, [C.POINTER(MantisResult),
+                                                           C.POINTER(RosServiceResponse)]),
+    "mantis_ros_image_callback": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int32,
+                                            C.c_void_p, C.c_size_t, C.POINTER(C.c_int64),
+                                            C.POINTER(MantisCamResult)]),
+    "mantis_ros_service_call": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                          C.POINTER(C.c_int64), C.POINTER(MantisResult)]),
+})
+
+
 def lib():
     """Load libmantis_amd.so (raises if it was not built)."""
     global _lib

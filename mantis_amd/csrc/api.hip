@@ -1044,3 +1044,4 @@ mantis_status mantis_set_profiling(void* ctx, int32_t on) {
 
 #include "gn_impl.hip"
 #include "dense_impl.hip"
+#include "ros_wire.h"

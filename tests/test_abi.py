@@ -1,5 +1,5 @@
 """The drop-in boundary: libmantis_amd.so loads on a CPU-only host, exports
-every entry point include/mantis.h declares, and its host-only functions
+every entry point include/mantis.h and include/mantis_ros.h declare, and its host-only functions
 (defaults, map parsing, the 6x6 GN solve, error paths) behave. No compute
 calls are made without a GPU.
 """
@@ -14,13 +14,15 @@ import _gn_ref as G
 import _oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "mantis.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("mantis.h", "mantis_ros.h")]
 
 
 def _declared():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mantis_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(mantis_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():

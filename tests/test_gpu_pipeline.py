@@ -219,3 +219,61 @@ def test_rig_gn_refines_pose(landmark_map):
     assert len(e0) >= 3
     assert np.mean(e1) < np.mean(e0), (e0, e1)
     assert max(e1) < 0.02, e1
+
+
+def test_ros_wire_callbacks_match_process(landmark_map):
+    """The ROS side of the drop-in end to end (include/mantis_ros.h): the
+    serialized sensor_msgs/Image + CameraInfo through mantis_ros_image_callback
+    give the same frame result as mantis_process and the oracle's decision, and
+    the serialized PoseWithCovarianceStamped carries it (frame "world", stamp 0
+    as the reference); the mantisService request through
+    mantis_ros_service_call answers with pose / weight / num_particles of the
+    rig result."""
+    import mantis_amd as M
+    from mantis_amd import ros
+
+    white, red, green = landmark_map
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(17)
+    frames = []
+    for f in range(3):
+        R, pos = synth.random_pose(rng)
+        frames.append(synth.render_host(synth.make_cam(R, pos), synth.frame_seed(4, f)))
+    a = M.Mantis(max_cams=4)
+    b = M.Mantis(max_cams=4)
+    try:
+        for m in (a, b):
+            m.set_map(white, red, green)
+            m.rng_state = 1
+        orc = O.Oracle(white, red, green, seed=1)
+        ci = ros.camera_info_bytes(np.asarray(K).reshape(9), list(D), 1280, 720)
+        published = 0
+        for img in frames:
+            msg = ros.image_bytes(img, step=3 * 1280 + 32, stamp=(100, 200), frame_id="cam0")
+            pose, cr = ros.image_callback(a, msg, ci)
+            _, ref = b.process([M.make_image(img, K, D)])
+            o = orc.process(img, K, D)
+            assert cr.reason == ref[0].reason == o.reason and cr.publish == ref[0].publish == o.publish
+            assert list(cr.position) == list(ref[0].position)
+            assert np.allclose(list(cr.position), list(o.position), atol=1e-9)
+            if cr.publish:
+                published += 1
+                d = ros.parse_pose_bytes(pose)
+                assert d["frame_id"] == "world" and d["stamp"] == (0, 0)
+                assert d["position"] == tuple(cr.position)
+                assert d["orientation_xyzw"] == tuple(cr.orientation_xyzw)
+                assert d["covariance"] == tuple(cr.covariance)
+            else:
+                assert pose is None
+        assert a.rng_state == b.rng_state == orc.rng_state
+        # mantisService: two cameras as one rig
+        req = ros.service_request_bytes([ros.image_bytes(i) for i in frames[:2]], [ci, ci])
+        resp, rr = ros.service_call(a, req)
+        _, _ = b.process([M.make_image(i, K, D) for i in frames[:2]])
+        d = ros.parse_service_response_bytes(resp)
+        assert d["position"] == tuple(rr.position) and d["weight"] == rr.weight
+        assert d["num_particles"] == rr.num_particles > 0
+        assert a.rng_state == b.rng_state
+    finally:
+        a.close()
+        b.close()
