@@ -123,7 +123,8 @@ struct Ctx {
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
-  uint16_t* d_lroot = nullptr;  // per-pixel Canny tile root (k_canny_uf -> k_hyst_edge)
+  uint16_t* d_lroot = nullptr;  // Canny candidates' tile roots (k_canny_uf -> k_hyst_edge), then run starts
+  size_t lstride = 0;            // d_lroot entries per frame: max(plane, tiles x FTW x FTH)
   uint8_t *d_bgr = nullptr, *d_strong = nullptr, *d_edge = nullptr,
           *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
@@ -255,15 +256,15 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const size_t B = c->bstride;
   dim3 gf((W + FTW - 1) / FTW, (H + FTH - 1) / FTH, n);
   k_canny_uf<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
-                                   c->d_b2, c->d_lroot, c->d_lab, c->d_strong, P, B);
+                                   c->d_b2, c->d_lroot, c->lstride, c->d_lab, c->d_strong, P, B);
   mark(c, "canny_nms");
   const size_t nhseam = (size_t)((W - 1) / FTW) * H + (size_t)((H - 1) / FTH) * W;
   if (nhseam) k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_b1, c->d_lab, W, H, P, B);
   const size_t nw = (size_t)((W + 31) / 32) * H;
   dim3 gw(blocks_for(nw), n);
   k_hyst_mark<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_lab, c->d_strong, W, H, P, B);
-  k_hyst_edge<<<gf, 256, 0, c->s>>>(c->d_lroot, c->d_lab, c->d_strong, c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H, P,
-                                    B);
+  k_hyst_edge<<<gf, 256, 0, c->s>>>(c->d_b1, c->d_lroot, c->lstride, c->d_lab, c->d_strong, c->d_eb,
+                                    edge_bytes ? c->d_edge : nullptr, W, H, P, B);
   mark(c, "hysteresis");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   dim3 gm((H + MB_BH - 1) / MB_BH, n);
@@ -620,7 +621,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
   chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
   chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
-  chk(dalloc(c, &c->d_lroot, (size_t)F * c->plane));
+  c->lstride = std::max(c->plane, (size_t)((c->Wmax + FTW - 1) / FTW) * ((c->Hmax + FTH - 1) / FTH) * FTW * FTH);
+  chk(dalloc(c, &c->d_lroot, (size_t)F * c->lstride));
   chk(dalloc(c, &c->d_edge, c->plane));  // debug / single-frame byte planes (frame 0)
   chk(dalloc(c, &c->d_det, c->plane));
   chk(dalloc(c, &c->d_eb, (size_t)F * c->bstride));

@@ -400,7 +400,7 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
 // rolling register windows (one LDS read per new row instead of a 3x3 gather).
 __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ frames, int low, int high, int vec,
                                                   uint32_t* __restrict__ cbits, uint32_t* __restrict__ rbits,
-                                                  uint16_t* __restrict__ lroot, int32_t* __restrict__ lab,
+                                                  uint16_t* __restrict__ croot, size_t lstride, int32_t* __restrict__ lab,
                                                   uint8_t* __restrict__ strong, size_t plane, size_t bstride) {
   const int f = blockIdx.z;
   const FrameDesc fd = frames[f];
@@ -438,10 +438,13 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   const int WW = bits::words(W);
   const size_t ob = (size_t)f * bstride;
   // (a wave covers 64 consecutive pixels of one tile row: two ballots give
-  // two words per plane)
+  // two words per plane; the candidate masks are kept for the root list)
+  __shared__ uint64_t gm[FTW * FTH / 64];
+  __shared__ int32_t gpre[FTW * FTH / 64];
   for (int i = t; i < FTW * FTH; i += 256) {
     const uint64_t cm = __ballot(K[i] != 0), rm = __ballot(S[i] != 0);
     const int lane = t & 63;
+    if (lane == 0) gm[i >> 6] = cm;
     if ((lane & 31) == 0) {
       const int y = y0 + i / FTW, w = (x0 + i % FTW) >> 5;
       if (y < H && w < WW) {
@@ -450,15 +453,29 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
       }
     }
   }
-  // per-pixel tile root (0xffff: not a candidate); sparse labels: tile roots
-  // (own index, strong flag cleared) and the tile-border candidates the seam
-  // unions start from
+  // the candidates' tile roots, 2 B each, in raster order within the tile
+  // (croot: index = candidates before it = prefix over the 64-pixel masks);
+  // k_hyst_edge finds them again from the candidate bit plane. Sparse
+  // labels: tile roots (own index, strong flag cleared) and the tile-border
+  // candidates the seam unions start from.
+  __syncthreads();
+  if (t < 64) {
+    constexpr int NGM = FTW * FTH / 64;
+    const int c = t < NGM ? __popcll(gm[t]) : 0;
+    int inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (t >= o) inc += v;
+    }
+    if (t < NGM) gpre[t] = inc - c;
+  }
+  __syncthreads();
   int32_t* l = lab + (size_t)f * plane;
   uint8_t* sg = strong + (size_t)f * plane;
-  uint16_t* lr = lroot + (size_t)f * plane;
-  for (int i = t; i < FTW * FTH; i += 256) {
-    const int x = x0 + (i % FTW), y = y0 + (i / FTW);
-    if (x < W && y < H) lr[(size_t)y * W + x] = K[i] ? (uint16_t)L[i] : (uint16_t)0xffff;
+  uint16_t* cr = croot + (size_t)f * lstride + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (FTW * FTH);
+  for (int k = t; k < ncand; k += 256) {
+    const int i = list[k];
+    cr[gpre[i >> 6] + __popcll(gm[i >> 6] & ((1ull << (i & 63)) - 1))] = (uint16_t)L[i];
   }
   for (int k = t; k < ncand; k += 256) {
     const int i = list[k];
@@ -526,28 +543,57 @@ __global__ __launch_bounds__(256) void k_hyst_mark(const uint32_t* __restrict__ 
   }
 }
 
-// edge = candidate whose global root is marked: per tile, each tile root
-// looks up its global root once, every candidate reads its tile root's flag
-__global__ __launch_bounds__(256) void k_hyst_edge(const uint16_t* __restrict__ lroot, int32_t* lab,
+// edge = candidate whose global root is marked: per tile, the candidates come
+// from the candidate bit plane and their tile roots from k_canny_uf's root
+// list (croot, raster order); each tile root looks up its global root once,
+// every candidate reads its tile root's flag
+__global__ __launch_bounds__(256) void k_hyst_edge(const uint32_t* __restrict__ cbits,
+                                                   const uint16_t* __restrict__ croot, size_t lstride, int32_t* lab,
                                                    const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
                                                    uint8_t* __restrict__ edge, int W, int H, size_t plane,
                                                    size_t bstride) {
+  constexpr int NGM = FTW * FTH / 64;
   __shared__ uint16_t R[FTW * FTH];
   __shared__ uint8_t Fl[FTW * FTH];
+  __shared__ uint64_t gm[NGM];
+  __shared__ int32_t gpre[NGM];
   const int f = blockIdx.z;
   const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
   if (x0 >= W || y0 >= H) return;
   const int t = threadIdx.x;
   const int WW = bits::words(W);
   const size_t ob = (size_t)f * bstride;
-  const uint16_t* lr = lroot + (size_t)f * plane;
+  const uint32_t* cb = cbits + ob;
   int32_t* l = lab + (size_t)f * plane;
   const uint8_t* sg = strong + (size_t)f * plane;
+  const uint16_t* cr = croot + (size_t)f * lstride + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (FTW * FTH);
+  if (t < 64) {
+    uint64_t m = 0;
+    if (t < NGM) {
+      const int y = y0 + (t >> 1), w = (x0 >> 5) + 2 * (t & 1);
+      if (y < H) {
+        const uint64_t lo = w < WW ? cb[(size_t)y * WW + w] : 0u, hi = w + 1 < WW ? cb[(size_t)y * WW + w + 1] : 0u;
+        m = lo | (hi << 32);
+      }
+      gm[t] = m;
+    }
+    const int c = __popcll(m);
+    int inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (t >= o) inc += v;
+    }
+    if (t < NGM) gpre[t] = inc - c;
+  }
+  __syncthreads();
   for (int i = t; i < FTW * FTH; i += 256) {
-    const int x = x0 + (i % FTW), y = y0 + (i / FTW);
-    const uint16_t r = (x < W && y < H) ? lr[(size_t)y * W + x] : (uint16_t)0xffff;
+    const uint64_t m = gm[i >> 6];
+    uint16_t r = 0xffff;
+    if ((m >> (i & 63)) & 1u) {
+      r = cr[gpre[i >> 6] + __popcll(m & ((1ull << (i & 63)) - 1))];
+      if (r == i) Fl[i] = sg[uf_find_c(l, (y0 + i / FTW) * W + x0 + (i % FTW))];
+    }
     R[i] = r;
-    if (r == i) Fl[i] = sg[uf_find_c(l, y * W + x)];
   }
   __syncthreads();
   for (int i = t; i < FTW * FTH; i += 256) {  // ballot per 64 pixels of a tile row

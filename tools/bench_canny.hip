@@ -62,9 +62,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  k_canny_uf<<<g, 256>>>(fd, 50, 150, 1, cb, rb, lr, lab, sg, plane, bstride);
+  k_canny_uf<<<g, 256>>>(fd, 50, 150, 1, cb, rb, lr, plane, lab, sg, plane, bstride);
   (void)hipEventRecord(e0);
-  for (int r = 0; r < 3; r++) k_canny_uf<<<g, 256>>>(fd, 50, 150, 1, cb, rb, lr, lab, sg, plane, bstride);
+  for (int r = 0; r < 3; r++) k_canny_uf<<<g, 256>>>(fd, 50, 150, 1, cb, rb, lr, plane, lab, sg, plane, bstride);
   (void)hipEventRecord(e1);
   (void)hipEventSynchronize(e1);
   float ms = 0;
