@@ -242,3 +242,42 @@ def test_throughput_mode_kernels_match_latency_mode(frames, landmark_map):
     finally:
         mt.close()
         ml.close()
+
+
+def test_mixed_batch_skipped_frames_keep_rng_stream(mantis, frames, landmark_map):
+    """Frames that return early (no quadrilaterals: a flat frame, a noise-only
+    frame; the reference's early returns, src/mantis3.cpp:82-84) draw no
+    gaussians, so the particle filters of the later frames in the same batch
+    read the stream from the same position as the sequential reference does
+    (device prefix over the frames that reach the particle filter). Also a
+    frame with a ragged width (row stride > 3 W)."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    flat = np.full((720, 1280, 3), 90, np.uint8)
+    rng = np.random.default_rng(4)
+    noise = rng.integers(80, 120, (720, 1280, 3), dtype=np.uint8)
+    seq = [frames[0][0], flat, frames[1][0], noise, frames[2][0], flat]
+    orc = O.Oracle(*landmark_map, seed=1)
+    mantis.rng_state = 1
+    imgs = []
+    for k, img in enumerate(seq):
+        if k == 2:  # padded rows: step = 3 W + 48
+            padded = np.zeros((720, 3 * 1280 + 48), np.uint8)
+            padded[:, :3 * 1280] = img.reshape(720, -1)
+            im = M.make_image(img, K, D)
+            keep = padded
+            im.bgr = keep.ctypes.data
+            im.step_bytes = 3 * 1280 + 48
+            imgs.append((im, keep))
+        else:
+            imgs.append((M.make_image(img, K, D), None))
+    rig, cams = mantis.process([im for im, _ in imgs], rigs=len(imgs))
+    for i, img in enumerate(seq):
+        o = orc.process(img, K, D)
+        assert cams[i].reason == o.reason, f"frame {i}: reason {cams[i].reason} vs {o.reason}"
+        assert cams[i].publish == o.publish
+        if o.reason != 1:  # frames with quads: same decisions and pose as the reference
+            _cmp_debug(mantis.frame_debug(i), o, f"frame {i}")
+    assert cams[1].reason == 1 and cams[5].reason == 1, "flat frames have no quadrilaterals"
+    assert mantis.rng_state == orc.rng_state
