@@ -316,11 +316,11 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
 // poses/s over filling every CU, bench sweep in DESIGN.md).
 std::atomic<int> g_live_ctx[64];
 
-// Grid of a persistent ObjPose launch: enough lanes for ~2 jobs each at the
+// Grid of a persistent ObjPose launch: two lanes per job at the
 // typical ~150 items per frame, at most 1.5 * CUs / (live contexts on the
 // device) blocks (MANTIS_RPP_BLOCKS overrides).
 unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
-  size_t b = (expected_jobs + 511) / 512;
+  size_t b = (expected_jobs + 127) / 128;  // ~0.5 jobs per lane: small batches start every job at once
   const int live = std::max(1, g_live_ctx[c->cfg.device & 63].load());
   const size_t cap = c->rpp_blocks > 0 ? (size_t)c->rpp_blocks : (size_t)std::max(64, 3 * c->n_cu / (2 * live));
   return (unsigned)std::max<size_t>(1, std::min(b, cap));
@@ -374,8 +374,15 @@ mantis_status run_score(Ctx* c, int n) {
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
   k_score_init<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
                                               c->d_dbg, c->d_sst);
-  k_score_pf<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res,
-                                            c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
+  // small batches (latency): 16 waves per frame, two per particle over halves
+  // of the landmarks; large batches: 10 waves, one per particle
+  if (n <= c->trace_lds_frames)
+    k_score_pf<1024, 2><<<n, 1024, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res,
+                                              c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
+  else
+    k_score_pf<kScoreThreads, 1><<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st,
+                                                                c->d_gauss, c->d_res, c->d_dbg, c->d_sst,
+                                                                c->cfg.particles, c->cfg.iterations);
   k_score_final<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
                                                c->d_sst, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");

@@ -1949,14 +1949,16 @@ __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
 #define MK_FAST_UNROLL 3
 #endif
 constexpr int kFastUnroll = MK_FAST_UNROLL;
+// Raw sums over the landmarks [lb, le): integer error sum and count (wave-reduced)
 template <class MK>
-__device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
-                                       const MK& mask, int W, int H, double* err_out, int* n_out) {
+__device__ inline void wave_sums_fast(const Xf& c2w, const double* lm, int lb, int le, const Cam& cm,
+                                      const uint8_t* bgr, const MK& mask, int W, int H, long long& s_out, int& n_out) {
   const int lane = threadIdx.x & 63;
   const long npx = (long)W * H;
+  const int nl = le;
   long long s = 0;
   int n = 0;
-  for (int l0 = lane; l0 < nl; l0 += 64 * kFastUnroll) {
+  for (int l0 = lb + lane; l0 < nl; l0 += 64 * kFastUnroll) {
     long lin[kFastUnroll];
     int px[kFastUnroll], py[kFastUnroll];
     bool in[kFastUnroll], ok[kFastUnroll];
@@ -1965,7 +1967,7 @@ __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, 
 #pragma unroll
     for (int k = 0; k < kFastUnroll; k++) {
       const int l = l0 + 64 * k;
-      const double* X = lm + 3 * (l < nl ? l : nl - 1);
+      const double* X = lm + 3 * (l < nl ? l : nl - 1);  // nl > lb: a valid landmark
       double rp[3];
       xf_apply(c2w, X, rp);
       double u, v;
@@ -2002,7 +2004,16 @@ __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, 
     s += __shfl_xor(s, o);
     n += __shfl_xor(n, o);
   }
-  if (lane == 0) {
+  s_out = s;
+  n_out = n;
+}
+template <class MK>
+__device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
+                                       const MK& mask, int W, int H, double* err_out, int* n_out) {
+  long long s;
+  int n;
+  wave_sums_fast(c2w, lm, 0, nl, cm, bgr, mask, W, H, s, n);
+  if ((threadIdx.x & 63) == 0) {
     *n_out = n;
     *err_out = n <= 0 ? DBL_MAX : (double)s / ((double)n * 1.1);
   }
@@ -2225,7 +2236,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_init(
 // w2c_sample * rand, rand = Transform(setRPY(g,g,g), (g,g,g)) drawn yaw, pitch,
 // roll, z, y, x; best = first strict minimum (argmin by (error, index) over
 // the 50, taken only when strictly below the current error).
-__global__ __launch_bounds__(kScoreThreads) void k_score_pf(
+template <int NT, int SPLIT>
+__global__ __launch_bounds__(NT) void k_score_pf(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
     FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations) {
@@ -2240,6 +2252,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_pf(
   __shared__ double lm[3 * 768];
   __shared__ Xf Pc[96], Pw[96];
   __shared__ double Pe[96];
+  __shared__ long long Ps[96 * SPLIT];
+  __shared__ int32_t Pn[96 * SPLIT];
+  constexpr int kW = NT / 64;
   __shared__ Xf cur_c2w, cur_w2c;
   __shared__ double cur_err;
   for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
@@ -2263,11 +2278,27 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_pf(
       Pc[tid] = xf_inverse(w2c);
     }
     __syncthreads();
-    for (int j = __builtin_amdgcn_readfirstlane(wave); j < particles; j += kWaves) {
-      double e;
-      int n;
-      wave_score_fast(rfl(Pc[j]), lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
-      if (lane == 0) Pe[j] = e;
+    // SPLIT waves per particle (landmark slices; integer sums, so the
+    // partials combine exactly in any order)
+    for (int task = __builtin_amdgcn_readfirstlane(wave); task < particles * SPLIT; task += kW) {
+      const int j = task / SPLIT, h = task - j * SPLIT;
+      long long sum;
+      int cnt;
+      wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr, mask, W, H, sum, cnt);
+      if (lane == 0) {
+        Ps[task] = sum;
+        Pn[task] = cnt;
+      }
+    }
+    __syncthreads();
+    if (tid < particles) {
+      long long sum = 0;
+      int cnt = 0;
+      for (int h = 0; h < SPLIT; h++) {
+        sum += Ps[tid * SPLIT + h];
+        cnt += Pn[tid * SPLIT + h];
+      }
+      Pe[tid] = cnt <= 0 ? DBL_MAX : (double)sum / ((double)cnt * 1.1);
     }
     __syncthreads();
     if (wave == 0) {
