@@ -1875,58 +1875,25 @@ struct Landmarks {
 // Masks of the cleaned image (HypothesisEvaluation.h:364 img.copyTo(out, mask)):
 // none (original image), host bytes (standalone scoring API) or the k_morph
 // bit plane (pipeline). Pixels are addressed by linear offset (below).
-// Each mask offers operator() (one pixel, for fetch_px) and a split form for
-// the pipelined fast scorer: word() issues the load of the mask word holding
-// pixel (x, y) (x already normalised to [0, W)), test() extracts the bit.
+// Each mask offers a split test for the pipelined fast scorer: word() issues
+// the load of the mask word holding pixel (x, y) (x already normalised to
+// [0, W)), test() extracts the bit. Out-of-buffer offsets (cvRound(px) == W /
+// == H) read as black; the caller never passes them in.
 struct MaskNone {
-  __device__ bool operator()(long, int, int) const { return true; }
   __device__ uint32_t word(long, int, int) const { return 1u; }
   __device__ bool test(uint32_t, int) const { return true; }
 };
 struct MaskBytes {
   const uint8_t* m;
-  __device__ bool operator()(long lin, int, int) const { return m[lin] != 0; }
   __device__ uint32_t word(long lin, int, int) const { return m[lin]; }
   __device__ bool test(uint32_t w, int) const { return w != 0; }
 };
 struct MaskBits {
   const uint32_t* m;
   int WW, W;
-  __device__ bool operator()(long lin, int x, int y) const {
-    if (x < 0 || x >= W) { y = (int)(lin / W); x = (int)(lin - (long)y * W); }
-    return (m[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
-  }
   __device__ uint32_t word(long, int x, int y) const { return m[(size_t)y * WW + (x >> 5)]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
-// cleaned or original BGR pixel, linear-offset semantics for cvRound(px) ==
-// W / == H: out-of-buffer reads are 0.
-template <class MK>
-__device__ inline void fetch_px(const uint8_t* bgr, const MK& mask, int W, int H, int x, int y, int& b, int& g,
-                                int& r) {
-  long lin = (long)y * W + x;
-  if (lin < 0 || lin >= (long)W * H || !mask(lin, x, y)) { b = g = r = 0; return; }
-  const uint8_t* p = bgr + 3 * lin;
-  b = p[0]; g = p[1]; r = p[2];
-}
-
-// fast error terms of one landmark: returns 1 if counted
-template <class MK>
-__device__ inline int fast_term(const Xf& c2w, const double* X, const Cam& cm, const uint8_t* bgr, const MK& mask,
-                                int W, int H, int& e) {
-  double rp[3];
-  xf_apply(c2w, X, rp);
-  if (!(rp[2] > 0)) return 0;
-  double u, v;
-  distort(cm, rp[0], rp[1], rp[2], &u, &v);
-  if (!in_frame(u, v, H, W)) return 0;
-  int b, g, r;
-  fetch_px(bgr, mask, W, H, cv_round(u), cv_round(v), b, g, r);
-  int e0 = b - 255, e1 = g - 255, e2 = r - 255;
-  e = e0 * e0 + e1 * e1 + e2 * e2;
-  return 1;
-}
-
 // B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
 // last pixel of the frame reads one byte early so the load stays in the buffer.
 __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
