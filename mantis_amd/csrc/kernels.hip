@@ -803,8 +803,9 @@ __global__ __launch_bounds__(256) void k_bits_to_bytes(const uint32_t* __restric
 //   k_run_count   wave per row: transitions -> runs of the row
 //   k_run_scan    block per frame: row bases (exclusive scan)
 //   k_run_emit    wave per row: run starts, labels = own ids
-//   k_run_union   wave per row: unions with the overlapping same-colour runs
-//                 of the row above (fg: [a-1, b+1], bg: [a, b])
+//   k_run_band    block per 32-row band: unions with the overlapping same-colour
+//                 runs of the row above (fg: [a-1, b+1], bg: [a, b]) in LDS
+//   k_run_seam    wave per band boundary: the same unions across bands
 //   k_run_border  wave per row: component roots -> border records
 // Transitions of word w of a padded row: bit b set where x = 32 w + b starts a run.
 __device__ inline uint32_t run_starts(const uint32_t* row, int w) {
@@ -905,24 +906,79 @@ __device__ inline int run_at(const uint16_t* x, int n, int v) {
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_run_union(const int32_t* __restrict__ rowb, size_t rstride,
-                                                   const uint16_t* __restrict__ rx, int32_t* lab, size_t plane,
-                                                   int Wp, int Hp) {
-  const int f = blockIdx.y;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6) + 1, lane = threadIdx.x & 63;
-  if (y >= Hp) return;
-  const int32_t* r = rowb + (size_t)f * rstride;
-  const uint16_t* X = rx + (size_t)f * plane;
-  int32_t* L = lab + (size_t)f * plane;
-  const int bp = r[y - 1], np = r[y] - bp, by = r[y], ny = r[y + 1] - by;
+// Unions of row y's runs (ids by .. by+ny-1, starts X[by..]) with the
+// overlapping same-colour runs of row y-1 (ids bp .. bp+np-1): fg runs
+// 8-connected ([a-1, b+1]), bg runs 4-connected ([a, b]); one wave, lanes over
+// the runs. UF is lds_union on band-local ids or uf_union_c on frame ids.
+template <class UF>
+__device__ inline void run_row_union(const uint16_t* X, int bp, int np, int by, int ny, int Wp, int lane,
+                                     const UF& uni) {
   const uint16_t* Xp = X + bp;
   for (int j = lane; j < ny; j += 64) {
     const int fg = j & 1;
     const int a = X[by + j], b = (j + 1 < ny ? (int)X[by + j + 1] : Wp) - 1;
     const int lo = a - fg, hi = b + fg;
     for (int k = run_at(Xp, np, lo); k < np && (int)Xp[k] <= hi; k++)
-      if ((k & 1) == fg) uf_union_c(L, by + j, bp + k);
+      if ((k & 1) == fg) uni(by + j, bp + k);
   }
+}
+
+// Run unions in two levels, so the union-find paths stay short (a
+// frame-wide chain of per-row links had every find walk up to ~700 global
+// hops). k_run_band: one block per band of RB_ROWS rows, its runs' starts and
+// labels in LDS, unions inside the band, then every run's label = its band
+// root (the band component's smallest run id). k_run_seam: the unions across
+// band boundaries on the global labels. Roots stay the component's smallest
+// run id either way (both unions link the larger root under the smaller).
+// A band with more than RB_CAP runs does its in-band unions on the global
+// labels instead.
+constexpr int RB_ROWS = 32, RB_CAP = 4096;
+__global__ __launch_bounds__(256) void k_run_band(const int32_t* __restrict__ rowb, size_t rstride,
+                                                  const uint16_t* __restrict__ rx, int32_t* lab, size_t plane, int Wp,
+                                                  int Hp) {
+  __shared__ int32_t Ll[RB_CAP];
+  __shared__ uint16_t Xl[RB_CAP];
+  __shared__ int32_t rbl[RB_ROWS + 1];
+  const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int y0 = blockIdx.x * RB_ROWS;
+  if (y0 >= Hp) return;
+  const int y1 = min(y0 + RB_ROWS, Hp);
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
+  int32_t* L = lab + (size_t)f * plane;
+  const int g0 = r[y0], n = r[y1] - g0;
+  if (n > RB_CAP) {
+    const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
+    for (int y = y0 + 1 + wave; y < y1; y += 4) run_row_union(X, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], Wp, lane, uni);
+    return;
+  }
+  for (int i = t; i <= y1 - y0; i += 256) rbl[i] = r[y0 + i] - g0;
+  for (int i = t; i < n; i += 256) {
+    Xl[i] = X[g0 + i];
+    Ll[i] = i;
+  }
+  __syncthreads();
+  int* Li = Ll;
+  const auto uni = [Li](int a, int b) { lds_union(Li, a, b); };
+  for (int y = y0 + 1 + wave; y < y1; y += 4) {
+    const int q = y - y0;
+    run_row_union(Xl, rbl[q - 1], rbl[q] - rbl[q - 1], rbl[q], rbl[q + 1] - rbl[q], Wp, lane, uni);
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 256) L[g0 + i] = g0 + lds_find(Ll, i);
+}
+
+// one wave per band boundary row y = k * RB_ROWS (k >= 1) against row y-1
+__global__ __launch_bounds__(256) void k_run_seam(const int32_t* __restrict__ rowb, size_t rstride,
+                                                  const uint16_t* __restrict__ rx, int32_t* lab, size_t plane, int Wp,
+                                                  int Hp) {
+  const int f = blockIdx.y;
+  const int y = (blockIdx.x * 4 + (threadIdx.x >> 6) + 1) * RB_ROWS, lane = threadIdx.x & 63;
+  if (y >= Hp) return;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  int32_t* L = lab + (size_t)f * plane;
+  const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
+  run_row_union(rx + (size_t)f * plane, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], Wp, lane, uni);
 }
 
 // row of run id: largest y with rowb[y] <= id
