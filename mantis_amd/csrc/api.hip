@@ -263,8 +263,10 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const size_t nw = (size_t)((W + 31) / 32) * H;
   dim3 gw(blocks_for(nw), n);
   k_hyst_mark<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_lab, c->d_strong, W, H, P, B);
-  k_hyst_edge<<<gf, 256, 0, c->s>>>(c->d_b1, c->d_lroot, c->lstride, c->d_lab, c->d_strong, c->d_eb,
-                                    edge_bytes ? c->d_edge : nullptr, W, H, P, B);
+  const int ntiles = (int)(gf.x * gf.y);
+  k_hyst_edge<<<dim3((ntiles + 3) / 4, n), 256, 0, c->s>>>(c->d_b1, c->d_lroot, c->lstride, c->d_lab, c->d_strong,
+                                                          c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H, P, B,
+                                                          (int)gf.x, ntiles);
   mark(c, "hysteresis");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   dim3 gm((H + MB_BH - 1) / MB_BH, n);

@@ -543,74 +543,66 @@ __global__ __launch_bounds__(256) void k_hyst_mark(const uint32_t* __restrict__ 
   }
 }
 
-// edge = candidate whose global root is marked: per tile, the candidates come
-// from the candidate bit plane and their tile roots from k_canny_uf's root
-// list (croot, raster order); each tile root looks up its global root once,
-// every candidate reads its tile root's flag
+// edge = candidate whose global root is marked. One wave per tile, lane t
+// owning the tile's 32-pixel word t (row t / 4, quarter t % 4), so only the
+// sparse candidates are visited: their tile roots come from k_canny_uf's root
+// list (croot, raster order = lane order then bit order); each tile root looks
+// up its global root once (a bit of Fb), then every candidate reads its
+// tile root's bit. Four tiles per 256-thread block.
 __global__ __launch_bounds__(256) void k_hyst_edge(const uint32_t* __restrict__ cbits,
                                                    const uint16_t* __restrict__ croot, size_t lstride, int32_t* lab,
                                                    const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
                                                    uint8_t* __restrict__ edge, int W, int H, size_t plane,
-                                                   size_t bstride) {
-  constexpr int NGM = FTW * FTH / 64;
-  __shared__ uint16_t R[FTW * FTH];
-  __shared__ uint8_t Fl[FTW * FTH];
-  __shared__ uint64_t gm[NGM];
-  __shared__ int32_t gpre[NGM];
-  const int f = blockIdx.z;
-  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
-  if (x0 >= W || y0 >= H) return;
-  const int t = threadIdx.x;
+                                                   size_t bstride, int gx, int ntiles) {
+  static_assert(FTW == 128 && FTW * FTH == 32 * 64, "one 32-pixel word per lane");
+  __shared__ uint16_t Rl[4][FTW * FTH];
+  __shared__ uint32_t Fb[4][64];
+  const int f = blockIdx.y, t = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tile = blockIdx.x * 4 + wv;
+  const bool live = tile < ntiles;
+  const int bx = live ? tile % gx : 0, by = live ? tile / gx : 0;
+  const int x0 = bx * FTW, y0 = by * FTH;
   const int WW = bits::words(W);
   const size_t ob = (size_t)f * bstride;
-  const uint32_t* cb = cbits + ob;
+  const int y = y0 + (t >> 2), w = (x0 >> 5) + (t & 3);
+  const bool in = live && y < H && w < WW;
+  const uint32_t m = in ? cbits[ob + (size_t)y * WW + w] : 0u;
+  const int c = __popc(m);
+  int inc = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o);
+    if (t >= o) inc += v;
+  }
+  const uint16_t* cr = croot + (size_t)f * lstride + (size_t)tile * (FTW * FTH);
+  uint16_t* R = Rl[wv];
   int32_t* l = lab + (size_t)f * plane;
   const uint8_t* sg = strong + (size_t)f * plane;
-  const uint16_t* cr = croot + (size_t)f * lstride + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (FTW * FTH);
-  if (t < 64) {
-    uint64_t m = 0;
-    if (t < NGM) {
-      const int y = y0 + (t >> 1), w = (x0 >> 5) + 2 * (t & 1);
-      if (y < H) {
-        const uint64_t lo = w < WW ? cb[(size_t)y * WW + w] : 0u, hi = w + 1 < WW ? cb[(size_t)y * WW + w + 1] : 0u;
-        m = lo | (hi << 32);
-      }
-      gm[t] = m;
+  uint32_t fl = 0;
+  {
+    int j = inc - c;
+    for (uint32_t mm = m; mm; mm &= mm - 1, j++) {
+      const int b = __ffs(mm) - 1, i = 32 * t + b;
+      const uint16_t r = cr[j];
+      R[j] = r;
+      if (r == i && sg[uf_find_c(l, y * W + x0 + 32 * (t & 3) + b)]) fl |= 1u << b;
     }
-    const int c = __popcll(m);
-    int inc = c;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(inc, o);
-      if (t >= o) inc += v;
-    }
-    if (t < NGM) gpre[t] = inc - c;
   }
+  Fb[wv][t] = fl;
   __syncthreads();
-  for (int i = t; i < FTW * FTH; i += 256) {
-    const uint64_t m = gm[i >> 6];
-    uint16_t r = 0xffff;
-    if ((m >> (i & 63)) & 1u) {
-      r = cr[gpre[i >> 6] + __popcll(m & ((1ull << (i & 63)) - 1))];
-      if (r == i) Fl[i] = sg[uf_find_c(l, (y0 + i / FTW) * W + x0 + (i % FTW))];
-    }
-    R[i] = r;
-  }
-  __syncthreads();
-  for (int i = t; i < FTW * FTH; i += 256) {  // ballot per 64 pixels of a tile row
-    const uint16_t r = R[i];
-    const uint64_t em = __ballot(r != 0xffff && Fl[r]);
-    const int lane = t & 63;
-    if ((lane & 31) == 0) {
-      const int y = y0 + i / FTW, w = (x0 + i % FTW) >> 5;
-      if (y < H && w < WW) ebits[ob + (size_t)y * WW + w] = (uint32_t)(em >> lane);
+  uint32_t e = 0;
+  {
+    int j = inc - c;
+    for (uint32_t mm = m; mm; mm &= mm - 1, j++) {
+      const int r = R[j];
+      e |= ((Fb[wv][r >> 5] >> (r & 31)) & 1u) << (__ffs(mm) - 1);
     }
   }
-  if (edge) {
-    uint8_t* e = edge + (size_t)f * plane;
-    for (int i = t; i < FTW * FTH; i += 256) {
-      const int x = x0 + (i % FTW), y = y0 + (i / FTW);
-      const uint16_t r = R[i];
-      if (x < W && y < H) e[(size_t)y * W + x] = (r != 0xffff && Fl[r]) ? 1 : 0;
+  if (in) ebits[ob + (size_t)y * WW + w] = e;
+  if (edge && in) {
+    uint8_t* ep = edge + (size_t)f * plane + (size_t)y * W;
+    for (int b = 0; b < 32; b++) {
+      const int x = 32 * w + b;
+      if (x < W) ep[x] = (e >> b) & 1u;
     }
   }
 }
