@@ -258,7 +258,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   k_canny_uf<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
                                    c->d_b2, c->d_lroot, c->lstride, c->d_lab, c->d_strong, P, B);
   mark(c, "canny_nms");
-  const size_t nhseam = (size_t)((W - 1) / FTW) * H + (size_t)((H - 1) / FTH) * W;
+  const size_t nhseam = (size_t)((W - 1) / FTW) * H + (size_t)((H - 1) / FTH) * ((W + 31) / 32);
   if (nhseam) k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_b1, c->d_lab, W, H, P, B);
   const size_t nw = (size_t)((W + 31) / 32) * H;
   dim3 gw(blocks_for(nw), n);

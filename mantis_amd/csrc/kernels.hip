@@ -495,7 +495,9 @@ __device__ inline bool cbit(const uint32_t* cb, int WW, int x, int y) {
   return (cb[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
 }
 
-// one thread per seam pixel: vertical seams (x = k*FTW) then horizontal (y = k*FTH)
+// unions across tile seams: one thread per pixel of the vertical seams
+// (x = k*FTW), then one per 32-pixel word of the horizontal seams (y = k*FTH),
+// whose candidates meet the row above through shifted words
 __global__ __launch_bounds__(256) void k_hyst_seam(const uint32_t* __restrict__ cbits, int32_t* lab, int W, int H,
                                                    size_t plane, size_t bstride) {
   const int f = blockIdx.y;
@@ -503,22 +505,30 @@ __global__ __launch_bounds__(256) void k_hyst_seam(const uint32_t* __restrict__ 
   const int WW = bits::words(W);
   int32_t* l = lab + (size_t)f * plane;
   const int nvs = (W - 1) / FTW, nhs = (H - 1) / FTH;
-  const size_t nv = (size_t)nvs * H, n = nv + (size_t)nhs * W;
+  const size_t nv = (size_t)nvs * H, n = nv + (size_t)nhs * WW;
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    int x, y;
-    const bool vert = k < nv;
-    if (vert) { x = (int)(k / H + 1) * FTW; y = (int)(k % H); }
-    else { const size_t h = k - nv; y = (int)(h / W + 1) * FTH; x = (int)(h % W); }
-    if (!cbit(cb, WW, x, y)) continue;
-    const int p = y * W + x;
-    if (vert) {
+    if (k < nv) {
+      const int x = (int)(k / H + 1) * FTW, y = (int)(k % H);
+      if (!cbit(cb, WW, x, y)) continue;
+      const int p = y * W + x;
       if (cbit(cb, WW, x - 1, y)) uf_union_c(l, p, p - 1);
       if (y > 0 && cbit(cb, WW, x - 1, y - 1)) uf_union_c(l, p, p - W - 1);
       if (y + 1 < H && cbit(cb, WW, x - 1, y + 1)) uf_union_c(l, p, p + W - 1);
-    } else {
-      if (cbit(cb, WW, x, y - 1)) uf_union_c(l, p, p - W);
-      if (x > 0 && cbit(cb, WW, x - 1, y - 1)) uf_union_c(l, p, p - W - 1);
-      if (x + 1 < W && cbit(cb, WW, x + 1, y - 1)) uf_union_c(l, p, p - W + 1);
+      continue;
+    }
+    const size_t h = k - nv;
+    const int y = (int)(h / WW + 1) * FTH, w = (int)(h % WW);
+    const uint32_t cur = cb[(size_t)y * WW + w];
+    if (!cur) continue;
+    const uint32_t* up = cb + (size_t)(y - 1) * WW;
+    const uint32_t a = up[w], ap = w > 0 ? up[w - 1] : 0u, an = w + 1 < WW ? up[w + 1] : 0u;
+    const uint32_t ul = (a << 1) | (ap >> 31), ur = (a >> 1) | (an << 31);  // bit b: x-1 / x+1 above
+    for (uint32_t mm = cur & (a | ul | ur); mm; mm &= mm - 1) {
+      const int b = __ffs(mm) - 1;
+      const int p = y * W + 32 * w + b;
+      if ((a >> b) & 1u) uf_union_c(l, p, p - W);
+      if ((ul >> b) & 1u) uf_union_c(l, p, p - W - 1);
+      if ((ur >> b) & 1u) uf_union_c(l, p, p - W + 1);
     }
   }
 }
