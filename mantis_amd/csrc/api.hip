@@ -132,6 +132,8 @@ struct Ctx {
   uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
+  uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
+  size_t tstride = 0;
   int32_t* d_rowb = nullptr;  // run CCL row bases, rstride per frame
   size_t rstride = 0;
   size_t dstride = 0;
@@ -295,12 +297,16 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
                                        kMaxBorders);
   mark(c, "components");
   const size_t tb_lds = (size_t)dbits_wpw(Wp) * Hp * sizeof(uint32_t);
-  if (c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames)
+  if (c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames) {
     k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
                                                    c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders);
-  else
-    k_trace_borders<<<dim3(4, n), 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
-                                                  c->d_scratch, c->pool_cap, Wp, kMaxBorders);
+  } else {
+    const int wpw = dbits_wpw(Wp);
+    k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, 32 * wpw * sizeof(uint32_t), c->s>>>(c->d_dbits, c->dstride, c->d_tbits,
+                                                                                  c->tstride, wpw, Hp);
+    k_trace_borders<<<n, 64, 0, c->s>>>(c->d_tbits, c->tstride, c->d_borders, c->d_st, c->d_bcount, c->d_scratch,
+                                        c->pool_cap, Wp, kMaxBorders);
+  }
   mark(c, "border_trace");
   // small batches (latency): 1024 threads per frame; large ones: 256, so the
   // per-frame blocks fit beside other contexts' kernels on a CU
@@ -522,6 +528,14 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
       c->h_res[f].status = MANTIS_ERR_CAPACITY;
     }
   }
+  if (const char* fs = getenv("MANTIS_FRAME_STATS")) {  // diagnostics: one line per frame
+    if (FILE* fp = fopen(fs, "a")) {
+      for (int f = 0; f < n; f++)
+        fprintf(fp, "%d %d %d %d %d %d\n", c->h_st[f].n_runs, c->h_st[f].n_borders, c->h_st[f].n_points,
+                c->h_st[f].trace_steps_max, c->h_st[f].trace_steps_sum, c->h_st[f].n_chunks);
+      fclose(fp);
+    }
+  }
   if (used * per != *c->h_gtotal) { c->err = "internal: gaussian stream accounting mismatch"; return MANTIS_ERR_DEVICE; }
   c->rng_state = c->h_states[used];
   return MANTIS_OK;
@@ -641,6 +655,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
+  c->tstride = tbits_words(dbits_wpw(c->Wmax + 2), c->Hmax + 2);
+  chk(dalloc(c, &c->d_tbits, (size_t)F * c->tstride));
   c->rstride = (size_t)c->Hmax + 3;
   chk(dalloc(c, &c->d_rowb, (size_t)F * c->rstride));
   chk(dalloc(c, &c->d_mask, c->plane));
@@ -698,7 +714,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->counted) g_live_ctx[c->cfg.device & 63].fetch_sub(1);
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_rowb,
+  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)

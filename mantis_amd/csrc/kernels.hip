@@ -1237,23 +1237,103 @@ struct RawQuad {
   int32_t parent, hole, key;
 };
 
-// 1. follow every border once (one work-item per border, many frames in
-// flight): points into 64-point chunks handed out by a per-frame counter.
-// The walks are serial chains of dependent neighbourhood reads; running them
-// in small blocks with the bit plane in L2 (instead of one 1024-thread block
-// per frame holding the plane in LDS) lets every CU interleave the walks of
-// many frames.
-__global__ __launch_bounds__(256) void k_trace_borders(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                       const Border* __restrict__ borders, FrameState* st,
-                                                       int32_t* __restrict__ counts, int32_t* __restrict__ scratch,
-                                                       int pool_cap, int Wp, int border_cap) {
+// The detector bit plane again in 32 x 32-pixel tiles, one 128-byte line per
+// tile (32 rows of one word column): a border walk moving vertically stays in
+// the lines it already holds instead of touching a new row-major line (and, with
+// thousands of frames walking at once, an HBM round trip) per step.
+__device__ __host__ inline size_t tbits_words(int wpw, int Hp) { return (size_t)wpw * ((Hp + 31) & ~31); }
+__global__ __launch_bounds__(256) void k_tile_bits(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                   uint32_t* __restrict__ tbits, size_t tstride, int wpw, int Hp) {
+  extern __shared__ uint32_t tl_band[];  // 32 rows x wpw words
+  const int f = blockIdx.y, by = blockIdx.x, t = threadIdx.x;
+  const uint32_t* src = dbits + (size_t)f * dstride + (size_t)by * 32 * wpw;
+  const int nrow = min(32, Hp - by * 32);
+  for (int i = t; i < 32 * wpw; i += 256) tl_band[i] = i < nrow * wpw ? src[i] : 0u;
+  __syncthreads();
+  uint32_t* dst = tbits + (size_t)f * tstride + (size_t)by * wpw * 32;
+  for (int o = t; o < 32 * wpw; o += 256) dst[o] = tl_band[(o & 31) * wpw + (o >> 5)];
+}
+struct BitsTiled {
+  const uint32_t* __restrict__ b;
+  int wpw;
+  __device__ uint32_t row3(int x, int y) const {
+    const uint32_t* q = b + ((size_t)(y >> 5) * wpw + ((x - 1) >> 5)) * 32 + (y & 31);
+    const uint64_t v = ((uint64_t)q[32] << 32) | q[0];
+    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  }
+  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
+};
+
+// trace_border_lut as a resumable walk (one step per call), so a lane whose
+// border closed can take the next one while its wave's long walks go on.
+struct Walk {
+  int x, y, s, px, py, prev_s, sx, sy, x1, y1, n, steps;
+};
+// the walk's first pixel and search; false: a single-point border (emitted)
+template <class NB, class EM>
+__device__ inline bool walk_start(const NB& nb, int sx, int sy, bool hole, EM& em, Walk& w) {
+  const uint32_t m = nb(sx, sy);
+  const int s_end0 = hole ? 0 : 4;
+  int s = s_end0;
+  do {
+    s = (s - 1) & 7;
+  } while (!((m >> s) & 1u) && s != s_end0);
+  w.px = sx - 1;
+  w.py = sy - 1;
+  w.n = 0;
+  w.steps = 0;
+  if (s == s_end0) {
+    em(w.px, w.py);
+    w.n = 1;
+    return false;
+  }
+  w.sx = w.x = sx;
+  w.sy = w.y = sy;
+  w.x1 = sx + fdx(s);
+  w.y1 = sy + fdy(s);
+  w.prev_s = s ^ 4;
+  w.s = s;
+  return true;
+}
+// one step of the follower; false once the border closed
+template <class NB, class EM>
+__device__ inline bool walk_step(const NB& nb, const uint8_t* lut, EM& em, Walk& w) {
+  const uint32_t p9 = nb.row3(w.x, w.y - 1) | (nb.row3(w.x, w.y) << 3) | (nb.row3(w.x, w.y + 1) << 6);
+  const int s = lut[(p9 << 3) | w.s];
+  if (s != w.prev_s) {
+    em(w.px, w.py);
+    w.n++;
+    w.prev_s = s;
+  }
+  const int dx = fdx(s), dy = fdy(s);
+  w.px += dx;
+  w.py += dy;
+  const int x4 = w.x + dx, y4 = w.y + dy;
+  if (x4 == w.sx && y4 == w.sy && w.x == w.x1 && w.y == w.y1) return false;
+  w.x = x4;
+  w.y = y4;
+  w.s = (s + 4) & 7;
+  w.steps++;
+  return true;
+}
+
+// 1. follow every border once: one wave per frame (the tiled bit plane in
+// L2), each lane walking one border at a time and refilled from the frame's
+// border list once a quarter of the wave is idle, so a frame costs about its
+// longest walk (the outer border of the grid lines, ~5-9k steps) instead of
+// the sum over static batches of each batch's longest. Points go to 64-point
+// chunks handed out by a per-frame counter.
+__global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict__ tbits, size_t tstride,
+                                                      const Border* __restrict__ borders, FrameState* st,
+                                                      int32_t* __restrict__ counts, int32_t* __restrict__ scratch,
+                                                      int pool_cap, int Wp, int border_cap) {
   __shared__ uint8_t next_lut[512 * 8];
-  const int f = blockIdx.y;
-  build_next_lut(next_lut, threadIdx.x, blockDim.x);
+  const int f = blockIdx.x, lane = threadIdx.x;
+  build_next_lut(next_lut, lane, 64);
   __syncthreads();
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
-  const uint32_t* B = dbits + (size_t)f * dstride;
+  const uint32_t* B = tbits + (size_t)f * tstride;
   const int wpw = dbits_wpw(Wp);
   const Border* bs = borders + (size_t)f * border_cap;
   int32_t* cnt = counts + (size_t)f * border_cap;
@@ -1262,12 +1342,42 @@ __global__ __launch_bounds__(256) void k_trace_borders(const uint32_t* __restric
   int32_t* chunks = sc;                        // [0, 2 pool_cap)
   int32_t* owner = sc + 2 * (size_t)pool_cap;  // [2 pool_cap, + max_chunks)
   int32_t* ordv = owner + max_chunks;
-  const BitsNB nbh{B, wpw};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
-    const Border b = bs[i];
-    ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, i, -1, 0, 0, false};
-    cnt[i] = trace_border_lut(nbh, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em, &st[f].trace_steps_max);
-    if (em.ovf) atomicOr(&st[f].overflow, 2);
+  const BitsTiled nbh{B, wpw};
+  int32_t* smax = &st[f].trace_steps_max;
+  ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
+  Walk w;
+  int i = -1;
+  bool act = false;
+  int next = 0;  // wave-uniform: the next border to hand out
+  const uint64_t below = (1ull << lane) - 1;
+  for (;;) {
+    const uint64_t idle = __ballot(!act);
+    const int nidle = __popcll(idle);
+    if (next < nb && (nidle >= 16 || nidle == 64)) {
+      if (!act) {
+        const int bi = next + __popcll(idle & below);
+        if (bi < nb) {
+          i = bi;
+          const Border b = bs[i];
+          em.border = i; em.cur = -1; em.k = 0; em.nch = 0; em.ovf = false;
+          act = walk_start(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em, w);
+          if (!act) {
+            cnt[i] = w.n;
+            if (em.ovf) atomicOr(&st[f].overflow, 2);
+          }
+        }
+      }
+      next += nidle;
+      continue;
+    }
+    if (nidle == 64) break;
+    if (act && !walk_step(nbh, next_lut, em, w)) {
+      act = false;
+      cnt[i] = w.n;
+      if (em.ovf) atomicOr(&st[f].overflow, 2);
+      atomicMax(smax, w.steps);
+      atomicAdd(&st[f].trace_steps_sum, w.steps);
+    }
   }
 }
 

@@ -101,6 +101,7 @@ struct FrameState {
   int32_t rpp_iters[2];  // AbsKernel calls of the first / candidate ObjPoses (k_objpose_q)
   int32_t trace_steps_max;  // longest border walk (steps) of k_trace_borders
   int32_t n_chunks;         // 64-point chunks handed out by k_trace_borders
+  int32_t trace_steps_sum;  // all border walks' steps of the frame
 };
 
 // Gauss–Newton rig refinement (gn_impl.hip): one camera's inv(T_base_cam)
