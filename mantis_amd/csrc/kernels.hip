@@ -1237,11 +1237,13 @@ struct RawQuad {
   int32_t parent, hole, key;
 };
 
-// The detector bit plane again in 32 x 32-pixel tiles, one 128-byte line per
-// tile (32 rows of one word column): a border walk moving vertically stays in
-// the lines it already holds instead of touching a new row-major line (and, with
-// thousands of frames walking at once, an HBM round trip) per step.
-__device__ __host__ inline size_t tbits_words(int wpw, int Hp) { return (size_t)wpw * ((Hp + 31) & ~31); }
+// The detector bit plane again for the walks: the 64-bit window (word w,
+// word w + 1) of every row and word, in tiles of 32 rows (256 bytes per word
+// column and tile), so a step reads one 8-byte word per row and a walk moving
+// vertically stays in the lines it already holds instead of touching a new
+// row-major line (with thousands of frames walking at once, an HBM round
+// trip) per step.
+__device__ __host__ inline size_t tbits_words(int wpw, int Hp) { return (size_t)2 * wpw * ((Hp + 31) & ~31); }
 __global__ __launch_bounds__(256) void k_tile_bits(const uint32_t* __restrict__ dbits, size_t dstride,
                                                    uint32_t* __restrict__ tbits, size_t tstride, int wpw, int Hp) {
   extern __shared__ uint32_t tl_band[];  // 32 rows x wpw words
@@ -1250,15 +1252,18 @@ __global__ __launch_bounds__(256) void k_tile_bits(const uint32_t* __restrict__ 
   const int nrow = min(32, Hp - by * 32);
   for (int i = t; i < 32 * wpw; i += 256) tl_band[i] = i < nrow * wpw ? src[i] : 0u;
   __syncthreads();
-  uint32_t* dst = tbits + (size_t)f * tstride + (size_t)by * wpw * 32;
-  for (int o = t; o < 32 * wpw; o += 256) dst[o] = tl_band[(o & 31) * wpw + (o >> 5)];
+  uint64_t* dst = (uint64_t*)(tbits + (size_t)f * tstride) + (size_t)by * wpw * 32;
+  for (int o = t; o < 32 * wpw; o += 256) {
+    const int r = o & 31, w = o >> 5;
+    const uint32_t lo = tl_band[r * wpw + w], hi = w + 1 < wpw ? tl_band[r * wpw + w + 1] : 0u;
+    dst[o] = (uint64_t)lo | ((uint64_t)hi << 32);
+  }
 }
 struct BitsTiled {
-  const uint32_t* __restrict__ b;
+  const uint64_t* __restrict__ b;
   int wpw;
   __device__ uint32_t row3(int x, int y) const {
-    const uint32_t* q = b + ((size_t)(y >> 5) * wpw + ((x - 1) >> 5)) * 32 + (y & 31);
-    const uint64_t v = ((uint64_t)q[32] << 32) | q[0];
+    const uint64_t v = b[((size_t)(y >> 5) * wpw + ((x - 1) >> 5)) * 32 + (y & 31)];
     return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
   }
   __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
@@ -1342,7 +1347,7 @@ __global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict
   int32_t* chunks = sc;                        // [0, 2 pool_cap)
   int32_t* owner = sc + 2 * (size_t)pool_cap;  // [2 pool_cap, + max_chunks)
   int32_t* ordv = owner + max_chunks;
-  const BitsTiled nbh{B, wpw};
+  const BitsTiled nbh{(const uint64_t*)B, wpw};
   int32_t* smax = &st[f].trace_steps_max;
   ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
   Walk w;
