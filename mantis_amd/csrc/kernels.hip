@@ -1270,10 +1270,17 @@ struct BitsTiled {
 };
 
 // trace_border_lut as a resumable walk (one step per call), so a lane whose
-// border closed can take the next one while its wave's long walks go on.
+// border closed can take the next one while its wave's long walks go on. A
+// step is a serial chain and its wave issues it for one or a few lanes, so it
+// is kept short: the position packed as x | y << 16 (one add moves it; the
+// emitted point is (x - 1, y - 1), as trace_border_lut's px, py), 32-bit byte
+// offsets into the tiled plane (scalar base + vector offset addressing).
 struct Walk {
-  int x, y, s, px, py, prev_s, sx, sy, x1, y1, n, steps;
+  uint32_t pos, spos, p1;  // current, start, and the start's last neighbour
+  int s, prev_s, n, steps;
 };
+__device__ inline uint32_t wpos(int x, int y) { return (uint32_t)x | ((uint32_t)y << 16); }
+__device__ inline uint32_t wdelta(int s) { return (uint32_t)(fdx(s) + (fdy(s) << 16)); }
 // the walk's first pixel and search; false: a single-point border (emitted)
 template <class NB, class EM>
 __device__ inline bool walk_start(const NB& nb, int sx, int sy, bool hole, EM& em, Walk& w) {
@@ -1283,40 +1290,44 @@ __device__ inline bool walk_start(const NB& nb, int sx, int sy, bool hole, EM& e
   do {
     s = (s - 1) & 7;
   } while (!((m >> s) & 1u) && s != s_end0);
-  w.px = sx - 1;
-  w.py = sy - 1;
   w.n = 0;
   w.steps = 0;
   if (s == s_end0) {
-    em(w.px, w.py);
+    em(sx - 1, sy - 1);
     w.n = 1;
     return false;
   }
-  w.sx = w.x = sx;
-  w.sy = w.y = sy;
-  w.x1 = sx + fdx(s);
-  w.y1 = sy + fdy(s);
+  w.spos = w.pos = wpos(sx, sy);
+  w.p1 = wpos(sx + fdx(s), sy + fdy(s));
   w.prev_s = s ^ 4;
   w.s = s;
   return true;
 }
-// one step of the follower; false once the border closed
-template <class NB, class EM>
-__device__ inline bool walk_step(const NB& nb, const uint8_t* lut, EM& em, Walk& w) {
-  const uint32_t p9 = nb.row3(w.x, w.y - 1) | (nb.row3(w.x, w.y) << 3) | (nb.row3(w.x, w.y + 1) << 6);
+// one step of the follower on the tiled plane (BitsTiled layout, wpw32 = 32 *
+// words per row); false once the border closed
+template <class EM>
+__device__ inline bool walk_step(const uint64_t* __restrict__ tb, int wpw32, const uint8_t* lut, EM& em, Walk& w) {
+  const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
+  const int xm = x - 1, col = xm & ~31, sh = xm & 31;
+  const char* base = (const char*)tb;
+  const int r = y & 31, t0 = (y >> 5) * wpw32 + col, om = t0 + r;
+  const uint32_t off[3] = {(uint32_t)(r == 0 ? t0 - wpw32 + 31 : om - 1), (uint32_t)om,
+                           (uint32_t)(r == 31 ? t0 + wpw32 : om + 1)};
+  uint32_t p9 = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint64_t v = *(const uint64_t*)(base + (off[k] << 3));
+    p9 |= ((uint32_t)(v >> sh) & 7u) << (3 * k);
+  }
   const int s = lut[(p9 << 3) | w.s];
   if (s != w.prev_s) {
-    em(w.px, w.py);
+    em(x - 1, y - 1);
     w.n++;
     w.prev_s = s;
   }
-  const int dx = fdx(s), dy = fdy(s);
-  w.px += dx;
-  w.py += dy;
-  const int x4 = w.x + dx, y4 = w.y + dy;
-  if (x4 == w.sx && y4 == w.sy && w.x == w.x1 && w.y == w.y1) return false;
-  w.x = x4;
-  w.y = y4;
+  const uint32_t np = w.pos + wdelta(s);
+  if (np == w.spos && w.pos == w.p1) return false;
+  w.pos = np;
   w.s = (s + 4) & 7;
   w.steps++;
   return true;
@@ -1376,7 +1387,7 @@ __global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict
       continue;
     }
     if (nidle == 64) break;
-    if (act && !walk_step(nbh, next_lut, em, w)) {
+    if (act && !walk_step(nbh.b, 32 * wpw, next_lut, em, w)) {
       act = false;
       cnt[i] = w.n;
       if (em.ovf) atomicOr(&st[f].overflow, 2);
