@@ -531,8 +531,8 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
   if (const char* fs = getenv("MANTIS_FRAME_STATS")) {  // diagnostics: one line per frame
     if (FILE* fp = fopen(fs, "a")) {
       for (int f = 0; f < n; f++)
-        fprintf(fp, "%d %d %d %d %d %d\n", c->h_st[f].n_runs, c->h_st[f].n_borders, c->h_st[f].n_points,
-                c->h_st[f].trace_steps_max, c->h_st[f].trace_steps_sum, c->h_st[f].n_chunks);
+        fprintf(fp, "%d %d %d %d %d %d %d\n", c->h_st[f].n_runs, c->h_st[f].n_borders, c->h_st[f].n_points,
+                c->h_st[f].trace_steps_max, c->h_st[f].trace_steps_sum, c->h_st[f].n_chunks, c->h_st[f].trace_ticks);
       fclose(fp);
     }
   }

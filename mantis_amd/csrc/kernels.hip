@@ -1343,6 +1343,7 @@ __global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict
                                                       const Border* __restrict__ borders, FrameState* st,
                                                       int32_t* __restrict__ counts, int32_t* __restrict__ scratch,
                                                       int pool_cap, int Wp, int border_cap) {
+  const uint64_t t_start = wall_clock64();
   __shared__ uint8_t next_lut[512 * 8];
   const int f = blockIdx.x, lane = threadIdx.x;
   build_next_lut(next_lut, lane, 64);
@@ -1395,6 +1396,7 @@ __global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict
       atomicAdd(&st[f].trace_steps_sum, w.steps);
     }
   }
+  if (lane == 0) st[f].trace_ticks = (int32_t)(wall_clock64() - t_start);
 }
 
 // Latency variant of k_trace_borders for small batches: one 1024-thread block

@@ -102,6 +102,7 @@ struct FrameState {
   int32_t trace_steps_max;  // longest border walk (steps) of k_trace_borders
   int32_t n_chunks;         // 64-point chunks handed out by k_trace_borders
   int32_t trace_steps_sum;  // all border walks' steps of the frame
+  int32_t trace_ticks;      // k_trace_borders wall-clock time of the frame (10 ns ticks)
 };
 
 // Gauss–Newton rig refinement (gn_impl.hip): one camera's inv(T_base_cam)
