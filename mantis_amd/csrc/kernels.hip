@@ -110,32 +110,28 @@ __device__ inline uint8_t gray_px(const uint8_t* p) {
 
 // 8-connected union-find of the candidates C (LDS bytes) of one FTW x FTH tile;
 // leaves every candidate's L at its component's minimum index (deterministic).
-// Candidates are sparse (thin NMS curves), so after the per-run init the
-// union and flatten passes walk a compacted candidate list (built with one
-// ballot and one LDS atomic per wave and step) instead of every pixel.
-__device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* count, int t) {
-  constexpr int SPR = FTW / FSEG;
+// Candidates are sparse (thin NMS curves): one ballot per 64 pixels gives the
+// candidate mask (kept in gm for the bit plane), a compacted candidate list
+// (one LDS atomic per wave and step), and each candidate's initial label, the
+// start of its run of consecutive candidates inside its FSEG-pixel segment (so
+// horizontal runs start linked). Only candidates' labels are ever read.
+__device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* count, uint64_t* gm, int t) {
   if (t == 0) *count = 0;
-  {
-    const int base = (t / SPR) * FTW + (t % SPR) * FSEG;
-    int run = base;
-    L[base] = base;
-#pragma unroll
-    for (int k = 1; k < FSEG; k++) {
-      const int i = base + k;
-      if (!(C[i] && C[i - 1])) run = i;
-      L[i] = run;
-    }
-  }
   __syncthreads();
   const int lane = t & 63;
   for (int i = t; i < FTW * FTH; i += 256) {
     const bool c = C[i] != 0;
     const uint64_t m = __ballot(c);
+    if (lane == 0) gm[i >> 6] = m;
     int base = 0;
     if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
     base = __shfl(base, 0);
-    if (c) list[base + __popcll(m & ((1ull << lane) - 1))] = (int16_t)i;
+    if (c) {
+      list[base + __popcll(m & ((1ull << lane) - 1))] = (int16_t)i;
+      const int sb = lane & ~(FSEG - 1);
+      const uint64_t z = ~m & ((1ull << lane) - 1) & ~((1ull << sb) - 1);  // non-candidates of the segment below
+      L[i] = (i - lane) + (z ? 64 - __clzll(z) : sb);
+    }
   }
   __syncthreads();
   const int n = *count;
@@ -256,8 +252,7 @@ __device__ inline void sobel4(const uint8_t* bl, int16_t* mag, int16_t* gx_s, in
 // allow dword loads, so the border rules (reflect/replicate/zero) drop out.
 template <bool IN>
 __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, int y0, int low, int high, int vec,
-                                     uint8_t* g, uint8_t* bl, int16_t* mag, int16_t* gxy, uint8_t* K, uint8_t* S,
-                                     int t) {
+                                     uint8_t* g, uint8_t* bl, int16_t* mag, int16_t* gxy, uint8_t* K, int t) {
   constexpr int BLH = FTH + 4;
   int16_t* gx_s = gxy;
   int16_t* gy_s = gxy + FTW * FTH;
@@ -390,7 +385,6 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
       }
     }
     K[i] = c;
-    S[i] = 0;
   }
   __syncthreads();
 }
@@ -418,7 +412,9 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   __shared__ __align__(16) uint8_t r1[R1];
   __shared__ __align__(16) uint8_t bl[BLH * FGW];
   __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];
-  __shared__ uint8_t K[FTW * FTH], S[FTW * FTH];
+  __shared__ uint8_t K[FTW * FTH];
+  __shared__ uint64_t gm[FTW * FTH / 64], sm[FTW * FTH / 64];  // candidate / strong-root masks
+  __shared__ int32_t gpre[FTW * FTH / 64];
   __shared__ int ncount;
   uint8_t* g = r1;
   int16_t* mag = (int16_t*)r1;
@@ -426,40 +422,33 @@ __global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ 
   int* L = (int*)gxy;
   const int t = threadIdx.x;
   const bool interior = vec && x0 >= 4 && x0 + FTW + 4 <= W && y0 >= 3 && y0 + FTH + 3 <= H;
-  if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, S, t);
-  else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, S, t);
-  const int ncand = tile_uf(K, L, list, &ncount, t);
+  if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, t);
+  else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, t);
+  if (t < FTW * FTH / 64) sm[t] = 0;
+  const int ncand = tile_uf(K, L, list, &ncount, gm, t);
   for (int k = t; k < ncand; k += 256) {
     const int i = list[k];
-    if (K[i] == 2) S[L[i]] = 1;
-  }
-  __syncthreads();
-  // bit planes: candidates, strong tile roots (4 words per tile row)
-  const int WW = bits::words(W);
-  const size_t ob = (size_t)f * bstride;
-  // (a wave covers 64 consecutive pixels of one tile row: two ballots give
-  // two words per plane; the candidate masks are kept for the root list)
-  __shared__ uint64_t gm[FTW * FTH / 64];
-  __shared__ int32_t gpre[FTW * FTH / 64];
-  for (int i = t; i < FTW * FTH; i += 256) {
-    const uint64_t cm = __ballot(K[i] != 0), rm = __ballot(S[i] != 0);
-    const int lane = t & 63;
-    if (lane == 0) gm[i >> 6] = cm;
-    if ((lane & 31) == 0) {
-      const int y = y0 + i / FTW, w = (x0 + i % FTW) >> 5;
-      if (y < H && w < WW) {
-        cbits[ob + (size_t)y * WW + w] = (uint32_t)(cm >> lane);
-        rbits[ob + (size_t)y * WW + w] = (uint32_t)(rm >> lane);
-      }
+    if (K[i] == 2) {
+      const int r = L[i];
+      atomicOr((unsigned long long*)&sm[r >> 6], 1ull << (r & 63));
     }
   }
-  // the candidates' tile roots, 2 B each, in raster order within the tile
-  // (croot: index = candidates before it = prefix over the 64-pixel masks);
-  // k_hyst_edge finds them again from the candidate bit plane. Sparse
-  // labels: tile roots (own index, strong flag cleared) and the tile-border
-  // candidates the seam unions start from.
+  // bit planes: candidates, strong tile roots (32-bit word j of the tile = row
+  // j / 4, quarter j % 4 = half j & 1 of the 64-pixel mask j / 2); the
+  // candidates' tile roots, 2 B each, in raster order within the tile (croot:
+  // index = candidates before it = prefix over the 64-pixel masks);
+  // k_hyst_edge finds them again from the candidate bit plane. Sparse labels:
+  // tile roots (own index, strong flag cleared) and the tile-border candidates
+  // the seam unions start from.
+  const int WW = bits::words(W);
+  const size_t ob = (size_t)f * bstride;
   __syncthreads();
   if (t < 64) {
+    const int y = y0 + (t >> 2), w = (x0 >> 5) + (t & 3);
+    if (y < H && w < WW) {
+      cbits[ob + (size_t)y * WW + w] = (uint32_t)(gm[t >> 1] >> (32 * (t & 1)));
+      rbits[ob + (size_t)y * WW + w] = (uint32_t)(sm[t >> 1] >> (32 * (t & 1)));
+    }
     constexpr int NGM = FTW * FTH / 64;
     const int c = t < NGM ? __popcll(gm[t]) : 0;
     int inc = c;
