@@ -365,22 +365,20 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
       const int cy = ly + 1, cx = lx + MO;
       const int m = mag[cy * MP + cx];
       if (m > low) {
+        // the three direction cases as selects (one pair of neighbour reads,
+        // no divergent branches): horizontal m > left && m >= right, vertical
+        // m > up && m >= down, diagonal m > both along the sign of gx * gy
         const int xs = gx_s[i], ys = gy_s[i];
         const int ax = abs(xs);
         const int ay = abs(ys) << SHIFT;
         const int tg22x = ax * TG22;
-        bool push;
-        if (ay < tg22x) {
-          push = m > mag[cy * MP + cx - 1] && m >= mag[cy * MP + cx + 1];
-        } else {
-          const int tg67x = tg22x + (ax << (SHIFT + 1));
-          if (ay > tg67x) {
-            push = m > mag[(cy - 1) * MP + cx] && m >= mag[(cy + 1) * MP + cx];
-          } else {
-            const int sg = (xs ^ ys) < 0 ? -1 : 1;
-            push = m > mag[(cy - 1) * MP + cx - sg] && m > mag[(cy + 1) * MP + cx + sg];
-          }
-        }
+        const int tg67x = tg22x + (ax << (SHIFT + 1));
+        const bool hor = ay < tg22x, ver = !hor && ay > tg67x, diag = !hor && !ver;
+        const int sg = (xs ^ ys) < 0 ? -1 : 1;
+        const int o = hor ? 1 : (ver ? MP : MP + sg);
+        const int c0 = cy * MP + cx;
+        const int a = mag[c0 - o], b = mag[c0 + o];
+        const bool push = m > a && (diag ? m > b : m >= b);
         if (push) c = (m > high) ? 2 : 1;
       }
     }
