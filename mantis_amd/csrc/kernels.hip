@@ -168,22 +168,36 @@ __device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* coun
 // [84,89,84] sums are exact, so 84(a+c) + 89b is the same number).
 constexpr int FG4 = FGW / 4;  // 4-pixel groups per interior row
 static_assert(FGW % 4 == 0 && FGH * FGW * 2 <= 2 * FTW * FTH * 2, "interior blur rows fit the gradient buffer");
-__device__ inline uint32_t byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; }
-// horizontal blur of gray rows 0 .. FGH-1 into hb (u16, FGH x FGW)
+// Packed 16-bit pairs (VOP3P v_pk_* arithmetic, two pixels per instruction):
+// for the 4-pixel group with bytes b1..b4 in wc, b0 = top byte of wp and b5 =
+// low byte of wn, the 3-tap operands of pixels (0,1) and (2,3) as u16 pairs
+// (l = left, m = centre, q = right; l23 = q01), built with v_perm_b32.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+struct Taps4 {
+  uint32_t l01, m01, q01, m23, q23;
+};
+__device__ inline Taps4 taps4(uint32_t wp, uint32_t wc, uint32_t wn) {
+  return {__builtin_amdgcn_perm(wc, wp, 0x0c040c03u), __builtin_amdgcn_perm(wc, wc, 0x0c010c00u),
+          __builtin_amdgcn_perm(wc, wc, 0x0c020c01u), __builtin_amdgcn_perm(wc, wc, 0x0c030c02u),
+          __builtin_amdgcn_perm(wn, wc, 0x0c040c03u)};
+}
+template <class V>
+__device__ inline V vpk(uint32_t v) { return __builtin_bit_cast(V, v); }
+template <class V>
+__device__ inline uint32_t upk(V v) { return __builtin_bit_cast(uint32_t, v); }
+// horizontal blur of gray rows 0 .. FGH-1 into hb (u16, FGH x FGW):
+// 84 (l + q) + 89 m <= 257 * 255 fits u16 exactly
 __device__ inline void hblur4(const uint8_t* g, uint16_t* hb, int t) {
   for (int u = t; u < FGH * FG4; u += 256) {
     const int ly = u / FG4, k = u - ly * FG4;
     const uint32_t* row = (const uint32_t*)(g + ly * FGW);
     const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
-    uint32_t b[6];
-    b[0] = wp >> 24;
-#pragma unroll
-    for (int j = 0; j < 4; j++) b[1 + j] = byte_of(wc, j);
-    b[5] = wn & 0xffu;
-    uint32_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) o[j] = 84u * (b[j] + b[j + 2]) + 89u * b[j + 1];
-    *(uint2*)(hb + ly * FGW + 4 * k) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
+    const Taps4 tp = taps4(wp, wc, wn);
+    const u16x2 c84 = {84, 84}, c89 = {89, 89};
+    const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
+    const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
+    *(uint2*)(hb + ly * FGW + 4 * k) = make_uint2(upk(o01), upk(o23));
   }
 }
 // vertical blur: bl rows 0 .. FTH+3 (image rows y0-2 ..) from hb rows ly .. ly+2
@@ -207,42 +221,36 @@ __device__ inline void vblur4(const uint16_t* hb, uint8_t* bl, int t) {
   }
 }
 // Sobel + L1 magnitude on rows 0 .. FTH+1 (image rows y0-1 ..), all columns;
-// gx / gy kept for the tile's own pixels (rows 1 .. FTH, columns 4 .. FTW+3)
+// gx / gy kept for the tile's own pixels (rows 1 .. FTH, columns 4 .. FTW+3).
+// Packed i16 pairs: |gx|, |gy| <= 1020, so every sum is exact in 16 bits.
 __device__ inline void sobel4(const uint8_t* bl, int16_t* mag, int16_t* gx_s, int16_t* gy_s, int t) {
   for (int u = t; u < (FTH + 2) * FG4; u += 256) {
     const int ly = u / FG4, k = u - ly * FG4;
-    int s[3][4], d[3][4];
+    s16x2 sm[3][2], df[3][2];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
       const uint32_t* row = (const uint32_t*)(bl + (ly + r) * FGW);
       const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
-      int b[6];
-      b[0] = (int)(wp >> 24);
-#pragma unroll
-      for (int j = 0; j < 4; j++) b[1 + j] = (int)byte_of(wc, j);
-      b[5] = (int)(wn & 0xffu);
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        s[r][j] = b[j] + 2 * b[j + 1] + b[j + 2];  // l + 2m + q
-        d[r][j] = b[j + 2] - b[j];                 // q - l
-      }
+      const Taps4 tp = taps4(wp, wc, wn);
+      const s16x2 l01 = vpk<s16x2>(tp.l01), m01 = vpk<s16x2>(tp.m01), q01 = vpk<s16x2>(tp.q01);
+      const s16x2 m23 = vpk<s16x2>(tp.m23), q23 = vpk<s16x2>(tp.q23);
+      sm[r][0] = l01 + (m01 << 1) + q01;  // l + 2m + q
+      sm[r][1] = q01 + (m23 << 1) + q23;
+      df[r][0] = q01 - l01;               // q - l
+      df[r][1] = q23 - q01;
     }
-    int m[4], gxv[4], gyv[4];
+    s16x2 m[2], gx[2], gy[2];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      gxv[j] = d[0][j] + 2 * d[1][j] + d[2][j];
-      gyv[j] = s[2][j] - s[0][j];
-      m[j] = abs(gxv[j]) + abs(gyv[j]);
+    for (int p = 0; p < 2; p++) {
+      gx[p] = df[0][p] + (df[1][p] << 1) + df[2][p];
+      gy[p] = sm[2][p] - sm[0][p];
+      m[p] = __builtin_elementwise_max(gx[p], -gx[p]) + __builtin_elementwise_max(gy[p], -gy[p]);
     }
-    *(uint2*)(mag + ly * FGW + 4 * k) =
-        make_uint2((uint32_t)(uint16_t)m[0] | ((uint32_t)(uint16_t)m[1] << 16),
-                   (uint32_t)(uint16_t)m[2] | ((uint32_t)(uint16_t)m[3] << 16));
+    *(uint2*)(mag + ly * FGW + 4 * k) = make_uint2(upk(m[0]), upk(m[1]));
     if (ly >= 1 && ly <= FTH && k >= 1 && k <= FTW / 4) {
       const int jj = (ly - 1) * FTW + 4 * (k - 1);
-      *(uint2*)(gx_s + jj) = make_uint2((uint32_t)(uint16_t)gxv[0] | ((uint32_t)(uint16_t)gxv[1] << 16),
-                                        (uint32_t)(uint16_t)gxv[2] | ((uint32_t)(uint16_t)gxv[3] << 16));
-      *(uint2*)(gy_s + jj) = make_uint2((uint32_t)(uint16_t)gyv[0] | ((uint32_t)(uint16_t)gyv[1] << 16),
-                                        (uint32_t)(uint16_t)gyv[2] | ((uint32_t)(uint16_t)gyv[3] << 16));
+      *(uint2*)(gx_s + jj) = make_uint2(upk(gx[0]), upk(gx[1]));
+      *(uint2*)(gy_s + jj) = make_uint2(upk(gy[0]), upk(gy[1]));
     }
   }
 }
