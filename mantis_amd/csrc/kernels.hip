@@ -107,6 +107,17 @@ __device__ inline int refl101(int i, int n) {  // BORDER_REFLECT_101
 __device__ inline uint8_t gray_px(const uint8_t* p) {
   return (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
 }
+// gray_px of the 4 pixels in three dwords (b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3)
+// with byte dot products: each coefficient = 256 hi + lo, both bytes, so
+// dot4(px, lo) + 256 dot4(px, hi) + 8192 is the same integer as gray_px's sum.
+__device__ inline uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
+  constexpr uint32_t LO = 0x0023914Cu, HI = 0x00132507u;  // (76, 145, 35), (7, 37, 19)
+  const uint32_t p1 = __builtin_amdgcn_perm(d1, d0, 0x0c050403u), p2 = __builtin_amdgcn_perm(d2, d1, 0x0c040302u);
+  const auto g = [](uint32_t p, uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_udot4(p, lo, (__builtin_amdgcn_udot4(p, hi, 0u, false) << 8) + 8192u, false) >> 14;
+  };
+  return g(d0, LO, HI) | (g(p1, LO, HI) << 8) | (g(p2, LO, HI) << 16) | (g(d2, LO << 8, HI << 8) << 24);
+}
 
 // 8-connected union-find of the candidates C (LDS bytes) of one FTW x FTH tile;
 // leaves every candidate's L at its component's minimum index (deterministic).
@@ -271,20 +282,12 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     uint8_t* o = g + ly * FGW + 4 * lg;
     if (IN) {
       const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
-      uint32_t d[3] = {q[0], q[1], q[2]};
-      const uint8_t* b = (const uint8_t*)d;
-      uint32_t w4 = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) w4 |= (uint32_t)gray_px(b + 3 * k) << (8 * k);
-      *(uint32_t*)o = w4;
+      *(uint32_t*)o = gray4(q[0], q[1], q[2]);
     } else if (y < 0 || y >= H) {
       o[0] = o[1] = o[2] = o[3] = 0;
     } else if (vec && xs >= 0 && xs + 3 < W) {
       const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
-      uint32_t d[3] = {q[0], q[1], q[2]};
-      const uint8_t* b = (const uint8_t*)d;
-#pragma unroll
-      for (int k = 0; k < 4; k++) o[k] = gray_px(b + 3 * k);
+      *(uint32_t*)o = gray4(q[0], q[1], q[2]);
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
