@@ -111,6 +111,44 @@ def test_contour_borders_match_find_contours(mantis, frames):
         assert cnt[1] == sum(len(c) for c in cs), f"points {cnt[1]} vs {sum(len(c) for c in cs)}"
 
 
+def test_throughput_border_walks_match_find_contours(landmark_map):
+    """The large-batch border walker (one wave per frame refilled from the
+    border list, 64-bit row windows in 32-row tiles) forced on single frames
+    (MANTIS_TRACE_LDS_FRAMES=0): borders and chain points against
+    findContours on blob-noise images whose padded sizes are not multiples of
+    32 (partial tiles, partial CCL bands) and on a real frame."""
+    import os
+
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(123)
+    imgs = []
+    for (w, h, cell) in [(333, 97, 2), (1000, 611, 6), (640, 480, 3), (1280, 720, 6)]:
+        base = (rng.random((h // cell + 2, w // cell + 2)) > 0.5).astype(np.float64) * 200 + 20
+        img = np.repeat(np.repeat(base, cell, 0), cell, 1)[:h, :w]
+        imgs.append(np.repeat(img[:, :, None], 3, 2).astype(np.uint8))
+    old = os.environ.get("MANTIS_TRACE_LDS_FRAMES")
+    os.environ["MANTIS_TRACE_LDS_FRAMES"] = "0"
+    try:
+        mt = M.Mantis(max_cams=2, max_width=1280, max_height=720)
+    finally:
+        if old is None:
+            del os.environ["MANTIS_TRACE_LDS_FRAMES"]
+        else:
+            os.environ["MANTIS_TRACE_LDS_FRAMES"] = old
+    try:
+        for img in imgs:
+            mt.detect_quads(M.make_image(img, K, D))
+            cnt = mt.frame_counters(0)
+            cs, holes = O.find_contours(O.detector_binary(O.canny(img)), 2)
+            assert cnt[8] == 0, f"overflow flags {cnt[8]}"
+            assert cnt[0] == len(cs), f"borders {cnt[0]} vs findContours {len(cs)}"
+            assert cnt[1] == sum(len(c) for c in cs), f"points {cnt[1]} vs {sum(len(c) for c in cs)}"
+    finally:
+        mt.close()
+
+
 def test_rpp_batch_matches_oracle(mantis):
     rng = np.random.default_rng(7)
     s = 0.16
