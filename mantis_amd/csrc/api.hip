@@ -10,6 +10,9 @@
 //   offsets into the gaussian stream (frames that reach the PF, in order)
 //   H2D gaussians -> scoring/PF/shift/yaw -> D2H results
 #include <hip/hip_runtime.h>
+#ifndef MK_FC_THREADS
+#define MK_FC_THREADS 256  // k_frame_contours threads per frame for large batches
+#endif
 
 #include <algorithm>
 #include <atomic>
@@ -310,7 +313,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   mark(c, "border_trace");
   // small batches (latency): 1024 threads per frame; large ones: 256, so the
   // per-frame blocks fit beside other contexts' kernels on a CU
-  k_frame_contours<<<n, n <= c->trace_lds_frames ? 1024 : 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
+  k_frame_contours<<<n, n <= c->trace_lds_frames ? 1024 : MK_FC_THREADS, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
                                          c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
                                          Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon,
                                          c->cfg.search_radius_multiplier);

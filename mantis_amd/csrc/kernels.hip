@@ -932,7 +932,10 @@ __device__ inline void run_row_union(const uint16_t* X, int bp, int np, int by, 
 // run id either way (both unions link the larger root under the smaller).
 // A band with more than RB_CAP runs does its in-band unions on the global
 // labels instead.
-constexpr int RB_ROWS = 32, RB_CAP = 4096;
+#ifndef MK_RB_ROWS
+#define MK_RB_ROWS 32
+#endif
+constexpr int RB_ROWS = MK_RB_ROWS, RB_CAP = 128 * MK_RB_ROWS;
 __global__ __launch_bounds__(256) void k_run_band(const int32_t* __restrict__ rowb, size_t rstride,
                                                   const uint16_t* __restrict__ rx, int32_t* lab, size_t plane, int Wp,
                                                   int Hp) {
