@@ -619,9 +619,6 @@ __global__ __launch_bounds__(256) void k_hyst_edge(const uint32_t* __restrict__ 
 // zero ring, WPW = ceil((W+2)/32) + 1 words per row (the spare word lets a
 // 64-bit window at any x be read without a bounds test).
 __device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
-__device__ inline uint32_t dbit(const uint32_t* B, int wpw, int x, int y) {
-  return (B[(size_t)y * wpw + (x >> 5)] >> (x & 31)) & 1u;
-}
 // ============================================================== morphology
 constexpr int MB_BH = 64;     // output rows per band
 constexpr int MB_HALO = 29;   // mask chain reach: M0 2 + (3+3+4+4+5+5) + 3
@@ -1028,18 +1025,6 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
 }
 
 // ============================================ per-frame contour -> quads
-// 8-neighbourhood of padded pixel (x, y) from the row-aligned bit plane
-// (LDS copy or global): three 64-bit windows starting at x - 1.
-struct BitsNB {
-  const uint32_t* __restrict__ b;
-  int wpw;
-  __device__ uint32_t row3(int x, int y) const {
-    const uint32_t* r = b + (size_t)y * wpw + ((x - 1) >> 5);
-    const uint64_t v = ((uint64_t)r[1] << 32) | r[0];
-    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
-  }
-  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
-};
 // direction code -> (dx + 1), (dy + 1), two bits per code (branch-free code_dx/code_dy)
 __device__ inline int fdx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }
 __device__ inline int fdy(int s) { return (int)((0xA901u >> (2 * s)) & 3u) - 1; }
