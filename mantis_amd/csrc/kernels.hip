@@ -620,7 +620,10 @@ __global__ __launch_bounds__(256) void k_hyst_edge(const uint32_t* __restrict__ 
 // 64-bit window at any x be read without a bounds test).
 __device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
 // ============================================================== morphology
-constexpr int MB_BH = 64;     // output rows per band
+#ifndef MK_MB_BH
+#define MK_MB_BH 48  // 3 x (48 + 2 x 29) rows x 40 words x 4 B = 51 KB: three bands per CU at 1280 px
+#endif
+constexpr int MB_BH = MK_MB_BH;  // output rows per band
 constexpr int MB_HALO = 29;   // mask chain reach: M0 2 + (3+3+4+4+5+5) + 3
 struct RowRange {
   int lo, hi;  // absolute rows [lo, hi) valid in a buffer
