@@ -142,6 +142,37 @@ mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
                                    mantis_result* out, mantis_cam_result* cam_out);
 
+/* Camera-sharded rig (BASELINE config 4: 8 cameras, one per GPU; SURVEY §8 e).
+ * Every rank of the communicator (mantis_comm_init) calls this with the same
+ * n_rigs / cams_per_rig and its own cameras: local_cams[r * n_local + j] is
+ * camera cam_index[j] (ascending) of rig r; each camera belongs to exactly one
+ * rank and n_local <= ceil(cams_per_rig / nranks). Exchanges (RCCL over xGMI):
+ * one ncclAllGather of the frames' particle-filter flags, so every frame
+ * draws the cv::RNG stream at the offset a sequential run over the rig's
+ * cameras in rig-major order would (Mantis3Params.h:87, PoseAdjustment.h:15-16);
+ * one ncclAllGather of the camera results for the rig fusion; with gn_enable one
+ * ncclAllReduce of every rig's J^T J / J^T r accumulators per Gauss-Newton
+ * iteration (each rank then solves the same 6x6 system). The multi-camera seam of
+ * the reference is the base->camera extrinsic chain of
+ * include/legacy/mantis/MonteCarlo.cpp:250-271. Every rank returns the same
+ * out[n_rigs]; cam_out (nullable) receives all n_rigs * cams_per_rig camera
+ * results in global order. With one rank this equals mantis_process_batch. */
+mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_cams, int32_t n_rigs, int32_t n_local,
+                                         const int32_t* cam_index, int32_t cams_per_rig, mantis_result* out,
+                                         mantis_cam_result* cam_out);
+
+/* Rig Gauss-Newton record of rig `rig` of the last batch (cfg.gn_enable):
+ * the fused pose the correspondences were formed with, the refined pose, the
+ * cost before / after, and this rank's correspondences as rows of
+ * [local camera index, u, v, X, Y, Z] (normalized undistorted point, world point). */
+typedef struct mantis_rig_gn_info {
+  double T_init[16];
+  double T_final[16];
+  double cost0, cost;
+  int32_t valid, iterations, n_obs, n_obs_local;
+} mantis_rig_gn_info;
+mantis_status mantis_get_rig_gn(void* ctx, int32_t rig, mantis_rig_gn_info* info, double* obs, int32_t cap);
+
 /* ------------------------------------------- stage entry points (parity) */
 /* gray -> GaussianBlur 3x3 -> Canny(50,150) (QuadDetection.h:209-212); out W*H bytes 0/255 */
 mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out);
@@ -192,6 +223,8 @@ mantis_status mantis_gn_solve(const double* acc28, double lambda, double* T_w_b,
 /* 128-byte ncclUniqueId; rank 0 creates it, the caller broadcasts it. */
 mantis_status mantis_comm_unique_id(void* id128);
 mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int32_t rank);
+/* the communicator's size and this context's rank (MANTIS_ERR_STATE without one) */
+mantis_status mantis_comm_info(void* ctx, int32_t* nranks, int32_t* rank);
 /* Camera-sharded rig: this rank contributes its cameras; the 28-double GN
  * accumulators are summed with one ncclAllReduce per iteration. */
 mantis_status mantis_gn_allreduce(void* ctx, double* acc28);

@@ -53,6 +53,12 @@ class MantisResult(C.Structure):
                 ("rng_state_after", C.c_uint64)]
 
 
+class MantisRigGnInfo(C.Structure):
+    _fields_ = [("T_init", C.c_double * 16), ("T_final", C.c_double * 16), ("cost0", C.c_double),
+                ("cost", C.c_double), ("valid", C.c_int32), ("iterations", C.c_int32), ("n_obs", C.c_int32),
+                ("n_obs_local", C.c_int32)]
+
+
 class SynthCamC(C.Structure):
     _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
                 ("k", C.c_double * 4), ("R_wc", C.c_double * 9), ("pos", C.c_double * 3),
@@ -115,6 +121,10 @@ _SIGS = {
     "mantis_gn_solve": (C.c_int, [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p]),
     "mantis_comm_unique_id": (C.c_int, [C.c_void_p]),
     "mantis_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
+    "mantis_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "mantis_process_rig_sharded": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_int32, C.c_int32, C.c_void_p,
+                                             C.c_int32, C.POINTER(MantisResult), C.POINTER(MantisCamResult)]),
+    "mantis_get_rig_gn": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(MantisRigGnInfo), C.c_void_p, C.c_int32]),
     "mantis_gn_allreduce": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mantis_score_argmin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
                                       C.c_int32, C.c_void_p, C.c_void_p]),
@@ -281,6 +291,33 @@ class Mantis:
         st = lib().mantis_process_batch(self.h, cams, rigs, n // rigs, out, cam_out)
         self._chk(st, "process_batch")
         return list(out), list(cam_out)
+
+    def process_sharded(self, images, rigs, cam_index, cams_per_rig):
+        """Camera-sharded rig call (mantis_process_rig_sharded): images are this
+        rank's cameras cam_index of each rig, rig-major. Returns (rig results,
+        every camera's result in global order)."""
+        n = len(images)
+        n_local = len(cam_index)
+        assert n == rigs * n_local
+        cams = (MantisImage * n)(*images)
+        idx = np.ascontiguousarray(cam_index, np.int32)
+        out = (MantisResult * rigs)()
+        cam_out = (MantisCamResult * (rigs * cams_per_rig))()
+        st = lib().mantis_process_rig_sharded(self.h, cams, rigs, n_local, idx.ctypes.data, cams_per_rig, out, cam_out)
+        self._chk(st, "process_rig_sharded")
+        return list(out), list(cam_out)
+
+    def comm_info(self):
+        nr, rk = C.c_int32(), C.c_int32()
+        self._chk(lib().mantis_comm_info(self.h, C.byref(nr), C.byref(rk)), "comm_info")
+        return nr.value, rk.value
+
+    def rig_gn(self, rig, cap=4096):
+        """(mantis_rig_gn_info, this rank's correspondences [cam, u, v, X, Y, Z])."""
+        info = MantisRigGnInfo()
+        obs = np.zeros((cap, 6))
+        self._chk(lib().mantis_get_rig_gn(self.h, rig, C.byref(info), obs.ctypes.data, cap), "get_rig_gn")
+        return info, obs[: min(cap, info.n_obs_local if info.valid else 0)].copy()
 
     def frame_counters(self, i):
         out = np.zeros(32, np.int32)

@@ -160,7 +160,9 @@ struct Ctx {
   GnCam* d_gncam = nullptr;
   RigGnIO* d_rigio = nullptr;
   double* d_gnobs = nullptr;
-  int gn_rigs = 0, gn_cpr = 0;  // batch frames allow aligned 3-dword BGR loads (W % 4 == 0, 4-byte bases)  // persistent-lane grid cap for k_objpose_q (0 = auto)
+  double* d_gnacc = nullptr;  // per-rig accumulator slots (kGnSlot doubles), all-reduced across camera shards
+  int gn_rigs = 0, gn_cpr = 0;
+  int gn_last_rigs = 0, gn_last_local = 0;  // shape of the last rig GN run (mantis_get_rig_gn)
   HypRec *d_gen = nullptr, *d_hyps = nullptr;
   FrameState* d_st = nullptr;
   ScoreState* d_sst = nullptr;  // scoring state between k_score_init / _pf / _final
@@ -184,7 +186,16 @@ struct Ctx {
   std::vector<void*> user_allocs;
   // multi-GPU
   void* comm = nullptr;  // ncclComm_t
+  int nranks = 1, rank = 0;
   double* d_gn28 = nullptr;
+  // camera-sharded rigs (mantis_process_rig_sharded): local frames' global
+  // indices, gathered (global index, PF flag) pairs, global PF flags, result records
+  int32_t *d_sh_gidx = nullptr, *d_sh_pf = nullptr, *d_sh_flags = nullptr;
+  int32_t* h_sh_flags = nullptr;
+  size_t sh_cap = 0;  // global frames the shard buffers hold
+  uint8_t *d_sh_rec = nullptr, *h_sh_rec = nullptr;
+  size_t sh_rec_bytes = 0;
+  int gauss_cap = 0;  // frames of gaussians h_gauss / d_gauss / h_states hold
 };
 
 void mark(Ctx* c, const char* name) {
@@ -362,15 +373,46 @@ mantis_status run_pose(Ctx* c, int n) {
   launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160);
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+// Camera-sharded rig call (mantis_process_rig_sharded): this rank's frames are
+// some cameras of each rig; the cv::RNG stream is consumed in global
+// (rig-major camera) order, as one sequential run over all cameras would.
+struct Shard {
+  int n_global;         // frames over all ranks (n_rigs * cams_per_rig)
+  int slots;            // (global index, PF flag) pairs each rank contributes
+  const int32_t* gidx;  // host: global frame index of each local frame
+};
+
+// Gaussian-stream offsets of the frames that reach the particle filter. One
+// rank: a prefix over the batch. Sharded: the frames' PF flags are gathered
+// from every rank (ncclAllGather of (global index, flag) pairs) and each local
+// frame takes the prefix at its global index.
+mantis_status gauss_offsets(Ctx* c, int n, const Shard* sh) {
   const int per = c->cfg.particles * c->cfg.iterations * 6;
-  k_gauss_offsets<<<1, 1024, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
+  if (!sh) {
+    k_gauss_offsets<<<1, 1024, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
+    HIP_OK(hipGetLastError());
+    return MANTIS_OK;
+  }
+  HIP_OK(hipMemcpyAsync(c->d_sh_gidx, sh->gidx, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->s));
+  int32_t* send = c->d_sh_pf;
+  int32_t* recv = c->d_sh_pf + 2 * (size_t)sh->slots;
+  k_shard_pf_pack<<<(sh->slots + 255) / 256, 256, 0, c->s>>>(c->d_st, c->d_sh_gidx, n, sh->slots, send);
+  ncclResult_t r = ncclAllGather(send, recv, 2 * (size_t)sh->slots, ncclInt32, (ncclComm_t)c->comm, c->s);
+  if (r != ncclSuccess) { c->err = std::string("ncclAllGather (PF flags): ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+  k_gauss_offsets_global<<<1, 1024, 0, c->s>>>(recv, sh->slots * c->nranks, c->d_sh_flags, sh->n_global, c->d_st,
+                                               c->d_sh_gidx, n, per, c->d_gtotal);
+  mark(c, "pf_exchange");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
 
 // Gaussian stream for up to n frames (frames that skip the PF draw nothing,
 // so the stream is contiguous and the device indexes it by prefix offsets).
-void gen_gauss(Ctx* c, int n) {
+void gen_gauss(Ctx* c, int n) {  // n <= c->gauss_cap
   const int per = c->cfg.particles * c->cfg.iterations * 6;
   uint64_t s = c->rng_state;
   c->h_states[0] = s;
@@ -381,9 +423,9 @@ void gen_gauss(Ctx* c, int n) {
   }
 }
 
-mantis_status run_score(Ctx* c, int n) {
+mantis_status run_score(Ctx* c, int n, int n_gauss) {
   const int per = c->cfg.particles * c->cfg.iterations * 6;
-  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s));
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
   k_score_init<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
@@ -453,7 +495,7 @@ void quat_to_mat4(const double* q, const double* p, double* T) {
 
 // Rig pose from per-camera results (reference-parity mode: no GN): the
 // published camera with the lowest error, mapped through T_base_cam.
-void fuse_rig(const mantis_image* cams, const mantis_cam_result* cr, int nc, mantis_result* out) {
+void fuse_rig(const double* Tbc, const mantis_cam_result* cr, int nc, mantis_result* out) {
   std::memset(out, 0, sizeof(*out));
   int best = -1;
   int npub = 0, nscored = 0, nq = 0;
@@ -480,7 +522,7 @@ void fuse_rig(const mantis_image* cams, const mantis_cam_result* cr, int nc, man
   }
   double Twc[16], Tbc_inv[16], Twb[16];
   quat_to_mat4(cr[best].orientation_xyzw, cr[best].position, Twc);
-  mat4_inv_rigid(cams[best].T_base_cam, Tbc_inv);
+  mat4_inv_rigid(Tbc + 16 * (size_t)best, Tbc_inv);
   mat4_mul(Twc, Tbc_inv, Twb);
   double R[9];
   for (int i = 0; i < 3; i++)
@@ -494,9 +536,35 @@ void fuse_rig(const mantis_image* cams, const mantis_cam_result* cr, int nc, man
   out->min_yaw_diff = cr[best].min_yaw_diff;
 }
 
-mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
+template <class T>
+mantis_status dalloc(Ctx* c, T** p, size_t count);
+template <class T>
+mantis_status halloc(Ctx* c, T** p, size_t count);
+
+// gaussian buffers for n frames (a sharded call draws for every rig camera)
+mantis_status ensure_gauss(Ctx* c, int n) {
+  if (n <= c->gauss_cap) return MANTIS_OK;
+  const int per = c->cfg.particles * c->cfg.iterations * 6;
+  HIP_OK(hipStreamSynchronize(c->s));
+  (void)hipFree(c->d_gauss);
+  (void)hipHostFree(c->h_gauss);
+  (void)hipHostFree(c->h_states);
+  c->d_gauss = nullptr;
+  c->h_gauss = nullptr;
+  c->h_states = nullptr;
+  c->gauss_cap = 0;
+  if (dalloc(c, &c->d_gauss, (size_t)n * per) || halloc(c, &c->h_gauss, (size_t)n * per) ||
+      halloc(c, &c->h_states, (size_t)n + 1))
+    return MANTIS_ERR_OOM;
+  c->gauss_cap = n;
+  return MANTIS_OK;
+}
+
+mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shard* sh = nullptr) {
   if (!c->d_lm) { c->err = "map not set (mantis_set_map)"; return MANTIS_ERR_STATE; }
   if (n <= 0 || n > c->F) { c->err = "frame count exceeds max_cams"; return MANTIS_ERR_ARG; }
+  const int ng = sh ? sh->n_global : n;
+  if (mantis_status e = ensure_gauss(c, ng)) return e;
   // The gaussian stream depends only on the RNG state, so a host thread draws
   // it while the device runs the image stages and RPP (the pinned buffer is
   // not in use: the previous call synchronised).
@@ -504,24 +572,28 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n) {
     std::thread t;
     ~Joiner() { if (t.joinable()) t.join(); }
   } gauss;
-  gauss.t = std::thread([c, n] { gen_gauss(c, n); });
+  gauss.t = std::thread([c, ng] { gen_gauss(c, ng); });
   int W, H;
   mantis_status st = stage_frames(c, cams, n, W, H);
   if (st != MANTIS_OK) return st;
   if ((st = run_image_stages(c, n, W, H)) != MANTIS_OK) return st;
   if ((st = run_contours(c, n, W, H)) != MANTIS_OK) return st;
   if ((st = run_pose(c, n)) != MANTIS_OK) return st;
+  if ((st = gauss_offsets(c, n, sh)) != MANTIS_OK) return st;
   gauss.t.join();
-  if ((st = run_score(c, n)) != MANTIS_OK) return st;
+  if ((st = run_score(c, n, ng)) != MANTIS_OK) return st;
   HIP_OK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(mantis_cam_result) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipMemcpyAsync(c->h_gtotal, c->d_gtotal, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
+  if (sh) HIP_OK(hipMemcpyAsync(c->h_sh_flags, c->d_sh_flags, sizeof(int32_t) * ng, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   finish_profile(c);
   const int per = c->cfg.particles * c->cfg.iterations * 6;
   int used = 0;
+  if (sh)
+    for (int f = 0; f < ng; f++) used += c->h_sh_flags[f] ? 1 : 0;
   for (int f = 0; f < n; f++) {
-    if (c->h_st[f].reaches_pf) used++;
+    if (!sh && c->h_st[f].reaches_pf) used++;
     if (c->h_st[f].overflow) {
       std::ostringstream os;
       os << "frame " << f << ": workspace capacity exceeded (flags " << c->h_st[f].overflow << ", borders "
@@ -559,6 +631,13 @@ mantis_status halloc(Ctx* c, T** p, size_t count) {
     return MANTIS_ERR_OOM;
   }
   return MANTIS_OK;
+}
+
+// T_base_cam of each camera, 16 doubles per camera
+std::vector<double> gather_tbc(const mantis_image* cams, int n) {
+  std::vector<double> T(16 * (size_t)n);
+  for (int i = 0; i < n; i++) std::memcpy(&T[16 * (size_t)i], cams[i].T_base_cam, sizeof(double) * 16);
+  return T;
 }
 
 thread_local std::string g_create_err;
@@ -685,6 +764,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_dbg, (size_t)F));
   chk(dalloc(c, &c->d_res, (size_t)F));
   chk(dalloc(c, &c->d_gauss, (size_t)F * per));
+  c->gauss_cap = F;
   chk(dalloc(c, &c->d_gtotal, 1));
   chk(halloc(c, &c->h_gauss, (size_t)F * per));
   chk(halloc(c, &c->h_states, (size_t)F + 1));
@@ -719,11 +799,11 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
-                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
+                   c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc, c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
     if (p) (void)hipFree(p);
   for (void* p : c->user_allocs) (void)hipFree(p);
-  void* hptrs[] = {c->h_gauss, c->h_states, c->h_res, c->h_st, c->h_gtotal, c->h_frames};
+  void* hptrs[] = {c->h_gauss, c->h_states, c->h_res, c->h_st, c->h_gtotal, c->h_frames, c->h_sh_flags, c->h_sh_rec};
   for (void* p : hptrs)
     if (p) (void)hipHostFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -797,7 +877,8 @@ mantis_status mantis_rng_set(void* ctx, uint64_t state) {
 }
 
 namespace {
-mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, mantis_result* out);  // gn_impl.hip
+mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, mantis_result* out,
+                         bool use_comm);  // gn_impl.hip
 }
 
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
@@ -808,24 +889,126 @@ mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t 
   const int n = n_rigs * cams_per_rig;
   mantis_status st = process_frames(c, cams, n);
   if (st != MANTIS_OK) return st;
-  const int per = c->cfg.particles * c->cfg.iterations * 6;
-  (void)per;
+  const std::vector<double> Tbc = gather_tbc(cams, n);
   int k = 0;
   for (int r = 0; r < n_rigs; r++) {
     const mantis_cam_result* cr = c->h_res + (size_t)r * cams_per_rig;
     if (out) {
-      fuse_rig(cams + (size_t)r * cams_per_rig, cr, cams_per_rig, &out[r]);
+      fuse_rig(&Tbc[16 * (size_t)r * cams_per_rig], cr, cams_per_rig, &out[r]);
       for (int i = 0; i < cams_per_rig; i++) k += c->h_st[r * cams_per_rig + i].reaches_pf;
       out[r].rng_state_after = c->h_states[k];
     }
   }
   if (out && c->cfg.gn_enable) {
-    st = run_rig_gn(c, cams, n_rigs, cams_per_rig, out);
+    st = run_rig_gn(c, Tbc.data(), n_rigs, cams_per_rig, out, false);
     if (st != MANTIS_OK) return st;
   }
   if (cam_out) std::memcpy(cam_out, c->h_res, sizeof(mantis_cam_result) * n);
   for (int f = 0; f < n; f++)
     if (c->h_res[f].status != 0) return MANTIS_ERR_CAPACITY;
+  return MANTIS_OK;
+}
+
+namespace {
+// one camera's result as exchanged between the ranks of a sharded rig
+struct ShardRec {
+  mantis_cam_result res;
+  double Tbc[16];
+  int32_t gidx, pad;
+};
+}  // namespace
+
+mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_cams, int32_t n_rigs, int32_t n_local,
+                                         const int32_t* cam_index, int32_t cams_per_rig, mantis_result* out,
+                                         mantis_cam_result* cam_out) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !local_cams || !cam_index || !out || n_rigs <= 0 || n_local <= 0 || cams_per_rig <= 0)
+    return MANTIS_ERR_ARG;
+  if (!c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
+  const int nl_max = (cams_per_rig + c->nranks - 1) / c->nranks;
+  if (n_local * c->nranks < cams_per_rig && c->nranks == 1) {
+    c->err = "sharded rig: a one-rank communicator must hold every camera";
+    return MANTIS_ERR_ARG;
+  }
+  if (n_local > nl_max) {
+    c->err = "sharded rig: at most ceil(cams_per_rig / nranks) cameras per rank";
+    return MANTIS_ERR_ARG;
+  }
+  for (int j = 0; j < n_local; j++)
+    if (cam_index[j] < 0 || cam_index[j] >= cams_per_rig || (j > 0 && cam_index[j] <= cam_index[j - 1])) {
+      c->err = "sharded rig: cam_index must be ascending indices in [0, cams_per_rig)";
+      return MANTIS_ERR_ARG;
+    }
+  const int n = n_rigs * n_local, ng = n_rigs * cams_per_rig, slots = n_rigs * nl_max;
+  // exchange buffers: (index, flag) pairs and result records, send + nranks x recv
+  if ((size_t)ng > c->sh_cap || (size_t)slots * (c->nranks + 1) * sizeof(ShardRec) > c->sh_rec_bytes) {
+    HIP_OK(hipStreamSynchronize(c->s));
+    void* d[] = {c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec};
+    for (void* p : d) (void)hipFree(p);
+    void* h[] = {c->h_sh_flags, c->h_sh_rec};
+    for (void* p : h) (void)hipHostFree(p);
+    c->d_sh_gidx = c->d_sh_pf = c->d_sh_flags = c->h_sh_flags = nullptr;
+    c->d_sh_rec = c->h_sh_rec = nullptr;
+    c->sh_cap = c->sh_rec_bytes = 0;
+    const size_t rec_bytes = (size_t)slots * (c->nranks + 1) * sizeof(ShardRec);
+    if (dalloc(c, &c->d_sh_gidx, (size_t)ng) || dalloc(c, &c->d_sh_pf, (size_t)2 * ng * (c->nranks + 1)) ||
+        dalloc(c, &c->d_sh_flags, (size_t)2 * ng) || halloc(c, &c->h_sh_flags, (size_t)2 * ng) ||
+        dalloc(c, &c->d_sh_rec, rec_bytes) || halloc(c, &c->h_sh_rec, rec_bytes))
+      return MANTIS_ERR_OOM;
+    c->sh_cap = ng;
+    c->sh_rec_bytes = rec_bytes;
+  }
+  std::vector<int32_t> gidx(n);
+  for (int r = 0; r < n_rigs; r++)
+    for (int j = 0; j < n_local; j++) gidx[(size_t)r * n_local + j] = r * cams_per_rig + cam_index[j];
+  Shard sh{ng, slots, gidx.data()};
+  mantis_status st = process_frames(c, local_cams, n, &sh);
+  if (st != MANTIS_OK) return st;
+  // gather every camera's result (one ncclAllGather of fixed-size records)
+  ShardRec* send = (ShardRec*)c->h_sh_rec;
+  for (int s = 0; s < slots; s++) {
+    std::memset(&send[s], 0, sizeof(ShardRec));
+    send[s].gidx = -1;
+    if (s < n) {
+      send[s].res = c->h_res[s];
+      std::memcpy(send[s].Tbc, local_cams[s].T_base_cam, sizeof(double) * 16);
+      send[s].gidx = gidx[s];
+    }
+  }
+  const size_t sbytes = (size_t)slots * sizeof(ShardRec);
+  HIP_OK(hipMemcpyAsync(c->d_sh_rec, send, sbytes, hipMemcpyHostToDevice, c->s));
+  ncclResult_t r = ncclAllGather(c->d_sh_rec, c->d_sh_rec + sbytes, sbytes, ncclUint8, (ncclComm_t)c->comm, c->s);
+  if (r != ncclSuccess) { c->err = std::string("ncclAllGather (camera results): ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+  HIP_OK(hipMemcpyAsync(c->h_sh_rec + sbytes, c->d_sh_rec + sbytes, sbytes * c->nranks, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  const ShardRec* recv = (const ShardRec*)(c->h_sh_rec + sbytes);
+  std::vector<mantis_cam_result> all(ng);
+  std::vector<double> Tall(16 * (size_t)ng);
+  std::vector<int> seen(ng, 0);
+  for (int i = 0; i < slots * c->nranks; i++) {
+    const int g = recv[i].gidx;
+    if (g < 0) continue;
+    if (g >= ng || seen[g]++) { c->err = "sharded rig: a camera is owned by two ranks"; return MANTIS_ERR_ARG; }
+    all[g] = recv[i].res;
+    std::memcpy(&Tall[16 * (size_t)g], recv[i].Tbc, sizeof(double) * 16);
+  }
+  for (int g = 0; g < ng; g++)
+    if (!seen[g]) { c->err = "sharded rig: a camera is owned by no rank"; return MANTIS_ERR_ARG; }
+  int k = 0;
+  for (int rr = 0; rr < n_rigs; rr++) {
+    fuse_rig(&Tall[16 * (size_t)rr * cams_per_rig], &all[(size_t)rr * cams_per_rig], cams_per_rig, &out[rr]);
+    for (int i = 0; i < cams_per_rig; i++) k += c->h_sh_flags[rr * cams_per_rig + i] ? 1 : 0;
+    out[rr].rng_state_after = c->h_states[k];
+  }
+  if (c->cfg.gn_enable) {
+    const std::vector<double> Tbc = gather_tbc(local_cams, n);
+    st = run_rig_gn(c, Tbc.data(), n_rigs, n_local, out, true);
+    if (st != MANTIS_OK) return st;
+  }
+  if (cam_out) std::memcpy(cam_out, all.data(), sizeof(mantis_cam_result) * ng);
+  for (int g = 0; g < ng; g++)
+    if (all[g].status != 0) return MANTIS_ERR_CAPACITY;
   return MANTIS_OK;
 }
 

@@ -105,9 +105,8 @@ mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint
   HIP_OK(hipGetLastError());
   int nr = 1;
   if (use_comm) {
-    int cnt = 0;
-    ncclCommCount((ncclComm_t)c->comm, &cnt);
-    if (cnt > 63) { c->err = "argmin exchange supports up to 63 ranks"; return MANTIS_ERR_ARG; }
+    const int cnt = c->nranks;  // checked against ncclCommCount in mantis_comm_init
+    if (cnt < 1 || cnt > 63) { c->err = "argmin exchange supports 1..63 ranks"; return MANTIS_ERR_ARG; }
     nr = cnt;
     ncclResult_t r = ncclAllGather(c->d_pairs, c->d_pairs + 2, 2, ncclFloat64, (ncclComm_t)c->comm, c->s);
     if (r != ncclSuccess) { c->err = std::string("ncclAllGather: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }

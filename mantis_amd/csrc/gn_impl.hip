@@ -185,30 +185,43 @@ __device__ inline bool gn_quad_obs(const FrameDesc& fd, const QuadRec& q, const 
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_rig_gn(const FrameDesc* __restrict__ frames, const FrameState* __restrict__ st,
-                                                const QuadRec* __restrict__ quads, const GnCam* __restrict__ gncam,
-                                                RigGnIO* io, int cams_per_rig, double* __restrict__ obs_all,
-                                                int obs_cap, int iterations, double half, double spacing) {
-  __shared__ double red[4][16][16];
-  __shared__ double T[16], acc28[28];
+// The rig GN runs as: k_rig_gn_obs (correspondences, once, with the fused
+// pose) then, per iteration, k_rig_gn_acc (one block per rig builds M^T M with
+// MFMA into a kGnSlot accumulator slot) -> [ncclAllReduce of every rig's slot
+// when the rig's cameras are sharded over ranks] -> k_rig_gn_step (one lane
+// per rig: Cholesky solve, SE(3) update, convergence flag). The single-GPU
+// path is the same sequence without the all-reduce, so a camera-sharded run on
+// a one-rank communicator is bit-identical to it, and with several ranks every
+// rank solves the same summed system (no broadcast). The reference's
+// multi-camera seam is the base->camera extrinsic chain of
+// include/legacy/mantis/MonteCarlo.cpp:250-271 (T_w_c = T_w_b T_b_c).
+
+// one rig, one block of 256: the accepted correspondences of this rank's
+// cameras in item order (camera, quad), compacted by a block scan
+__global__ __launch_bounds__(256) void k_rig_gn_obs(const FrameDesc* __restrict__ frames,
+                                                    const FrameState* __restrict__ st,
+                                                    const QuadRec* __restrict__ quads,
+                                                    const GnCam* __restrict__ gncam, RigGnIO* io, int cams_local,
+                                                    double* __restrict__ obs_all, int obs_cap, double half,
+                                                    double spacing) {
+  __shared__ double T[16];
   __shared__ int32_t scan[256];
-  __shared__ int32_t nobs_s, done;
-  const int rig = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  __shared__ int32_t nobs_s;
+  const int rig = blockIdx.x, t = threadIdx.x;
   RigGnIO& R = io[rig];
   if (!R.valid) return;
   if (t < 16) T[t] = R.Twb[t];
   __syncthreads();
-  const GnCam* cams = gncam + (size_t)rig * cams_per_rig;
+  const GnCam* cams = gncam + (size_t)rig * cams_local;
   double* obs = obs_all + (size_t)rig * obs_cap * 6;
-  const int n_items = cams_per_rig * kMaxQuads;
-  // pass 1: count accepted corners of this thread's item range; pass 2: write them in item order
+  const int n_items = cams_local * kMaxQuads;
+  const int per = (n_items + 255) / 256;
+  // pass 1: count accepted quads of this thread's item range; pass 2: write them in item order
   for (int pass = 0; pass < 2; pass++) {
-    int cntv = 0, pos = 0;
-    if (pass == 1) pos = scan[t];
-    const int per = (n_items + 255) / 256;
+    int pos = pass == 1 ? scan[t] : 0, cntv = 0;
     for (int it = t * per; it < n_items && it < (t + 1) * per; it++) {
       const int c = it / kMaxQuads, q = it % kMaxQuads;
-      const int f = rig * cams_per_rig + c;
+      const int f = rig * cams_local + c;
       if (q >= st[f].n_quads) continue;
       // camera pose in the world from the base pose: T_wc = T_wb inv(T_cb)
       double Rbc[9], tbc[3], Rwc[9], Cw[3];
@@ -237,73 +250,116 @@ __global__ __launch_bounds__(256) void k_rig_gn(const FrameDesc* __restrict__ fr
         int run = 0;
         for (int i = 0; i < 256; i++) { const int v = scan[i]; scan[i] = run; run += v; }
         nobs_s = run < obs_cap ? run : obs_cap;
-        done = 0;
       }
       __syncthreads();
     }
   }
   __syncthreads();
-  const int n_obs = nobs_s;
-  if (n_obs < 6) {
-    if (t == 0) { R.n_obs = n_obs; R.iterations = 0; }
+  if (t < 16) R.T0[t] = T[t];
+  if (t == 0) {
+    R.n_obs_local = nobs_s;
+    R.n_obs = 0;
+    R.iterations = 0;
+    R.done = 0;
+    R.cost0 = R.cost = 0;
+  }
+}
+
+// one rig, one block of 256: M^T M of M = [J | r] over this rank's
+// correspondences about the current pose (4 waves, v_mfma_f64_16x16x4f64, 4
+// residual rows per instruction), summed over the waves in a fixed order
+__global__ __launch_bounds__(256) void k_rig_gn_acc(const GnCam* __restrict__ gncam, const RigGnIO* __restrict__ io,
+                                                    int cams_local, const double* __restrict__ obs_all, int obs_cap,
+                                                    double* __restrict__ acc_all) {
+  __shared__ double red[4][16][16];
+  const int rig = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const RigGnIO& R = io[rig];
+  double* out = acc_all + (size_t)rig * kGnSlot;
+  const int n_obs = R.n_obs_local;
+  if (!R.valid || R.done) {
+    if (t < kGnSlot) out[t] = 0.0;
     return;
   }
-  int it_done = 0;
-  for (int it = 0; it < iterations; it++) {
-    double Rt[9], tw[3];
-    for (int a = 0; a < 3; a++) {
-      for (int b = 0; b < 3; b++) Rt[3 * a + b] = T[4 * b + a];
-      tw[a] = T[4 * a + 3];
-    }
-    v4d acc = {0, 0, 0, 0};
-    const int rows = 2 * n_obs;
-    const int kk = lane >> 4, m = lane & 15;
-    for (int base = wave * 4; base < rows; base += 16) {
-      const double v = gn_entry(Rt, tw, cams, obs, n_obs, base + kk, m);
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
-    }
-    for (int r = 0; r < 4; r++) red[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
-    __syncthreads();
-    if (t == 0) {
-      int n = 0;
-      for (int a = 0; a < 6; a++)
-        for (int b = a; b < 6; b++) acc28[n++] = red[0][a][b] + red[1][a][b] + red[2][a][b] + red[3][a][b];
-      for (int a = 0; a < 6; a++) acc28[21 + a] = red[0][a][6] + red[1][a][6] + red[2][a][6] + red[3][a][6];
-      acc28[27] = red[0][6][6] + red[1][6][6] + red[2][6][6] + red[3][6][6];
-      if (it == 0) R.cost0 = acc28[27];
-      R.cost = acc28[27];
-      double Tn[16], d6[6];
-      for (int e = 0; e < 16; e++) Tn[e] = T[e];
-      if (!gn_solve6(acc28, 1e-9, Tn, d6)) {
-        done = 1;
-      } else {
-        for (int e = 0; e < 16; e++) T[e] = Tn[e];
-        double dn = 0;
-        for (int e = 0; e < 6; e++) dn += d6[e] * d6[e];
-        if (dn < 1e-24) done = 1;
-      }
-    }
-    __syncthreads();
-    it_done = it + 1;
-    if (done) break;
+  const GnCam* cams = gncam + (size_t)rig * cams_local;
+  const double* obs = obs_all + (size_t)rig * obs_cap * 6;
+  double Rt[9], tw[3];
+  for (int a = 0; a < 3; a++) {
+    for (int b = 0; b < 3; b++) Rt[3 * a + b] = R.Twb[4 * b + a];
+    tw[a] = R.Twb[4 * a + 3];
   }
-  if (t < 16) R.Twb[t] = T[t];
-  if (t == 0) { R.iterations = it_done; R.n_obs = n_obs; }
+  v4d acc = {0, 0, 0, 0};
+  const int rows = 2 * n_obs;
+  const int kk = lane >> 4, m = lane & 15;
+  for (int base = wave * 4; base < rows; base += 16) {
+    const double v = gn_entry(Rt, tw, cams, obs, n_obs, base + kk, m);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+  }
+  for (int r = 0; r < 4; r++) red[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
+  __syncthreads();
+  if (t < kGnSlot) {
+    double v = 0.0;
+    if (t < 21) {  // upper triangle, row-major
+      int a = 0, k = t;
+      while (k >= 6 - a) { k -= 6 - a; a++; }
+      const int b = a + k;
+      v = red[0][a][b] + red[1][a][b] + red[2][a][b] + red[3][a][b];
+    } else if (t < 27) {
+      const int a = t - 21;
+      v = red[0][a][6] + red[1][a][6] + red[2][a][6] + red[3][a][6];
+    } else if (t == 27) {
+      v = red[0][6][6] + red[1][6][6] + red[2][6][6] + red[3][6][6];
+    } else if (t == 28) {
+      v = (double)n_obs;
+    }
+    out[t] = v;
+  }
+}
+
+// one lane per rig: the summed system -> Cholesky solve -> T_w_b Exp(delta)
+__global__ __launch_bounds__(64) void k_rig_gn_step(RigGnIO* io, const double* __restrict__ acc_all, int n_rigs,
+                                                    int it) {
+  const int rig = blockIdx.x * 64 + threadIdx.x;
+  if (rig >= n_rigs) return;
+  RigGnIO& R = io[rig];
+  if (!R.valid || R.done) return;
+  const double* acc = acc_all + (size_t)rig * kGnSlot;
+  if (it == 0) {
+    R.n_obs = (int)acc[28];
+    if (R.n_obs < 6) {  // too few correspondences over the rig: keep the fused pose
+      R.done = 1;
+      return;
+    }
+    R.cost0 = acc[27];
+  }
+  R.cost = acc[27];
+  double Tn[16], d6[6];
+  for (int e = 0; e < 16; e++) Tn[e] = R.Twb[e];
+  if (!gn_solve6(acc, 1e-9, Tn, d6)) {
+    R.done = 1;
+  } else {
+    for (int e = 0; e < 16; e++) R.Twb[e] = Tn[e];
+    double dn = 0;
+    for (int e = 0; e < 6; e++) dn += d6[e] * d6[e];
+    if (dn < 1e-24) R.done = 1;
+  }
+  R.iterations = it + 1;
 }
 
 }  // namespace mk
 
 namespace {
-// cfg.gn_enable: refine every rig's fused base pose on the device (k_rig_gn);
-// per-camera inv(T_base_cam) and the fused poses go up, refined poses come back.
-mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, mantis_result* out) {
-  const int n = n_rigs * cpr;
-  const int obs_cap = cpr * kMaxQuads;
+// cfg.gn_enable: refine every rig's fused base pose on the device. Tbc holds
+// T_base_cam of this rank's cameras, rig-major (n_rigs x cams_local x 16); the
+// frames of the last pipeline batch are those cameras in the same order. With
+// a communicator (camera-sharded rigs) the accumulators are summed over ranks.
+mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, mantis_result* out, bool use_comm) {
+  const int n = n_rigs * cams_local;
+  const int obs_cap = cams_local * kMaxQuads;
   std::vector<GnCam> gc(n);
   std::vector<RigGnIO> io(n_rigs);
   for (int f = 0; f < n; f++) {
     double inv[16];
-    mat4_inv_rigid(cams[f].T_base_cam, inv);
+    mat4_inv_rigid(Tbc + 16 * (size_t)f, inv);
     for (int a = 0; a < 3; a++) {
       for (int b = 0; b < 3; b++) gc[f].R_cb[3 * a + b] = inv[4 * a + b];
       gc[f].t_cb[a] = inv[4 * a + 3];
@@ -317,31 +373,42 @@ mantis_status run_rig_gn(Ctx* c, const mantis_image* cams, int n_rigs, int cpr, 
       io[r].valid = 1;
     }
   }
-  if (c->gn_rigs < n_rigs || c->gn_cpr != cpr) {
-    (void)hipFree(c->d_gncam);
-    (void)hipFree(c->d_rigio);
-    (void)hipFree(c->d_gnobs);
+  if (c->gn_rigs < n_rigs || c->gn_cpr != cams_local) {
+    void* old[] = {c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc};
+    for (void* p : old) (void)hipFree(p);
     c->d_gncam = nullptr;
     c->d_rigio = nullptr;
     c->d_gnobs = nullptr;
+    c->d_gnacc = nullptr;
     c->gn_rigs = 0;
     if (dalloc(c, &c->d_gncam, (size_t)n) || dalloc(c, &c->d_rigio, (size_t)n_rigs) ||
-        dalloc(c, &c->d_gnobs, (size_t)n_rigs * obs_cap * 6))
+        dalloc(c, &c->d_gnobs, (size_t)n_rigs * obs_cap * 6) || dalloc(c, &c->d_gnacc, (size_t)n_rigs * kGnSlot))
       return MANTIS_ERR_OOM;
     c->gn_rigs = n_rigs;
-    c->gn_cpr = cpr;
+    c->gn_cpr = cams_local;
   }
   HIP_OK(hipMemcpyAsync(c->d_gncam, gc.data(), sizeof(GnCam) * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(c->d_rigio, io.data(), sizeof(RigGnIO) * n_rigs, hipMemcpyHostToDevice, c->s));
   const double spacing = c->cfg.grid_spacing, half = 4.5 * spacing;  // lines at -1.44 + 0.32 k, k = 0..9
   mark(c, "start");
-  k_rig_gn<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cpr, c->d_gnobs,
-                                      obs_cap, c->cfg.gn_iterations, half, spacing);
+  k_rig_gn_obs<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cams_local,
+                                          c->d_gnobs, obs_cap, half, spacing);
+  for (int it = 0; it < c->cfg.gn_iterations; it++) {
+    k_rig_gn_acc<<<n_rigs, 256, 0, c->s>>>(c->d_gncam, c->d_rigio, cams_local, c->d_gnobs, obs_cap, c->d_gnacc);
+    if (use_comm) {
+      ncclResult_t r = ncclAllReduce(c->d_gnacc, c->d_gnacc, (size_t)n_rigs * kGnSlot, ncclFloat64, ncclSum,
+                                     (ncclComm_t)c->comm, c->s);
+      if (r != ncclSuccess) { c->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+    }
+    k_rig_gn_step<<<(n_rigs + 63) / 64, 64, 0, c->s>>>(c->d_rigio, c->d_gnacc, n_rigs, it);
+  }
   mark(c, "rig_gn");
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(io.data(), c->d_rigio, sizeof(RigGnIO) * n_rigs, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   finish_profile(c, true);
+  c->gn_last_rigs = n_rigs;
+  c->gn_last_local = cams_local;
   for (int r = 0; r < n_rigs; r++) {
     if (!io[r].valid || io[r].iterations <= 0) continue;
     double R[9];
@@ -418,9 +485,57 @@ mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int
   std::memcpy(&id, id128, sizeof(id));
   ncclComm_t comm;
   HIP_OK(hipSetDevice(c->cfg.device));
+  if (c->comm) {  // re-initialisation replaces the previous communicator
+    HIP_OK(hipStreamSynchronize(c->s));
+    (void)ncclCommDestroy((ncclComm_t)c->comm);
+    c->comm = nullptr;
+    c->nranks = 1;
+    c->rank = 0;
+  }
   ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
   if (r != ncclSuccess) { c->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+  int cnt = 0, me = -1;
+  if (ncclCommCount(comm, &cnt) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess || cnt != nranks ||
+      me != rank) {
+    (void)ncclCommDestroy(comm);
+    c->err = "ncclCommCount/UserRank disagree with the requested rank layout";
+    return MANTIS_ERR_COMM;
+  }
   c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_comm_info(void* ctx, int32_t* nranks, int32_t* rank) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !nranks || !rank) return MANTIS_ERR_ARG;
+  if (!c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
+  *nranks = c->nranks;
+  *rank = c->rank;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_get_rig_gn(void* ctx, int32_t rig, mantis_rig_gn_info* info, double* obs, int32_t cap) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !info || rig < 0 || cap < 0 || (cap > 0 && !obs)) return MANTIS_ERR_ARG;
+  if (rig >= c->gn_last_rigs || !c->d_rigio) { c->err = "no rig GN result for that rig (gn_enable, last batch)"; return MANTIS_ERR_STATE; }
+  RigGnIO io;
+  HIP_OK(hipMemcpyAsync(&io, c->d_rigio + rig, sizeof(io), hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  std::memcpy(info->T_init, io.T0, sizeof(io.T0));
+  std::memcpy(info->T_final, io.Twb, sizeof(io.Twb));
+  info->cost0 = io.cost0;
+  info->cost = io.cost;
+  info->valid = io.valid;
+  info->iterations = io.iterations;
+  info->n_obs = io.n_obs;
+  info->n_obs_local = io.n_obs_local;
+  const int k = std::min(cap, io.valid ? io.n_obs_local : 0);
+  const size_t obs_cap = (size_t)c->gn_last_local * kMaxQuads;
+  if (k > 0)
+    HIP_OK(hipMemcpy(obs, c->d_gnobs + (size_t)rig * obs_cap * 6, sizeof(double) * 6 * k, hipMemcpyDeviceToHost));
   return MANTIS_OK;
 }
 

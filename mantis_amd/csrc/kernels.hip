@@ -2041,6 +2041,56 @@ __global__ __launch_bounds__(1024) void k_gauss_offsets(FrameState* st, int nf, 
   if (t == 1023) *total = base + incl;
 }
 
+// Camera-sharded rigs: this rank's (global frame index, reaches-PF flag) pairs,
+// padded to `slots` with (-1, 0) so every rank contributes the same count.
+__global__ __launch_bounds__(256) void k_shard_pf_pack(const FrameState* __restrict__ st,
+                                                       const int32_t* __restrict__ gidx, int n_local, int slots,
+                                                       int32_t* __restrict__ pairs) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= slots) return;
+  pairs[2 * s] = s < n_local ? gidx[s] : -1;
+  pairs[2 * s + 1] = s < n_local ? (st[s].reaches_pf ? 1 : 0) : 0;
+}
+
+// The gathered pairs of every rank -> flags[0, ng) in global frame order, the
+// exclusive prefix of flags * per_frame in flags[ng, 2 ng), and each local
+// frame's gaussian offset at its global index (one block).
+__global__ __launch_bounds__(1024) void k_gauss_offsets_global(const int32_t* __restrict__ pairs, int npairs,
+                                                               int32_t* flags, int ng, FrameState* st,
+                                                               const int32_t* __restrict__ gidx, int n_local,
+                                                               int per_frame, int32_t* total) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int i = t; i < ng; i += 1024) flags[i] = 0;
+  __syncthreads();
+  for (int i = t; i < npairs; i += 1024) {
+    const int g = pairs[2 * i];
+    if (g >= 0 && g < ng) flags[g] = pairs[2 * i + 1];
+  }
+  __syncthreads();
+  const int chunk = (ng + 1023) / 1024;
+  const int f0 = min(ng, t * chunk), f1 = min(ng, f0 + chunk);
+  int mine = 0;
+  for (int f = f0; f < f1; f++) mine += flags[f] ? per_frame : 0;
+  int incl = mine;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wave; w++) base += wsum[w];
+  int acc = base + incl - mine;
+  for (int f = f0; f < f1; f++) {
+    flags[ng + f] = acc;
+    if (flags[f]) acc += per_frame;
+  }
+  if (t == 1023) *total = base + incl;
+  __syncthreads();
+  for (int f = t; f < n_local; f += 1024) st[f].gauss_offset = flags[ng + gidx[f]];
+}
+
 // ============================================================== scoring
 struct Landmarks {
   const double* xyz;  // n x 3 (white, red, green in map order)

@@ -110,11 +110,18 @@ struct GnCam {
   double R_cb[9];
   double t_cb[3];
 };
-// per-rig input/output of k_rig_gn: base pose in, refined pose out
+// per-rig state of the rig GN kernels: base pose in, refined pose out.
+// n_obs_local = this rank's correspondences (k_rig_gn_obs); n_obs = the whole
+// rig's (summed with the accumulators); done = converged / failed / too few.
 struct RigGnIO {
   double Twb[16];
+  double T0[16];  // the fused pose the correspondences were formed with
   double cost0, cost;
-  int32_t valid, iterations, n_obs, pad;
+  int32_t valid, iterations, n_obs, done;
+  int32_t n_obs_local, pad[3];
 };
+// per-rig accumulator slot of the rig GN: upper-triangle J^T J (21), J^T r (6),
+// r^T r (1), correspondence count (1), padding — summed across camera shards
+constexpr int kGnSlot = 32;
 
 }  // namespace mk

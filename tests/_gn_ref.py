@@ -78,3 +78,76 @@ def synth_rig_obs(rng, T_w_b, T_b_c, n_per_cam=24, noise=1e-3):
             u = pc[:2] / pc[2] + rng.normal(size=2) * noise
             obs.append([c, u[0], u[1], X[0], X[1], X[2]])
     return np.array(obs)
+
+
+def quad_cell_obs(corners, undistort, Rwc, Cw, half=1.44, spacing=0.32):
+    """FP64 restatement of gn_quad_obs (mantis_amd/csrc/gn_impl.hip): the
+    crossing of the quad's undistorted diagonals, back-projected with the
+    camera pose onto the floor z = 0 and snapped to the nearest cell centre
+    (accepted within 0.1 m). corners: 4 x 2 pixel ints; undistort(px) -> 4 x 2
+    normalized. Returns (u, v, X, Y, 0) or None."""
+    uv = undistort(np.asarray(corners, np.float64).reshape(4, 2))
+    u, v = uv[:, 0], uv[:, 1]
+    d1x, d1y, d2x, d2y = u[2] - u[0], v[2] - v[0], u[3] - u[1], v[3] - v[1]
+    den = d1x * d2y - d1y * d2x
+    if abs(den) < 1e-12:
+        return None
+    a = ((u[1] - u[0]) * d2y - (v[1] - v[0]) * d2x) / den
+    if not (0 < a < 1):
+        return None
+    uc, vc = u[0] + a * d1x, v[0] + a * d1y
+    dw = Rwc @ np.array([uc, vc, 1.0])
+    if not dw[2] < -1e-9:
+        return None
+    tt = -Cw[2] / dw[2]
+    if not tt > 0:
+        return None
+    X, Y = Cw[0] + tt * dw[0], Cw[1] + tt * dw[1]
+    c0 = -half + 0.5 * spacing
+    kx, ky = np.rint((X - c0) / spacing), np.rint((Y - c0) / spacing)
+    lim = np.rint(2 * half / spacing) - 1
+    if kx < 0 or ky < 0 or kx > lim or ky > lim:
+        return None
+    gx, gy = c0 + spacing * kx, c0 + spacing * ky
+    if abs(X - gx) > 0.1 or abs(Y - gy) > 0.1:
+        return None
+    return np.array([uc, vc, gx, gy, 0.0])
+
+
+def rig_gn_reference(T0, T_b_c, cam_quads, undistorters, iterations, lam=1e-9, half=1.44, spacing=0.32):
+    """FP64 restatement of the pipeline's rig Gauss-Newton (k_rig_gn_obs /
+    _acc / _step): correspondences formed once with the fused pose T0 in
+    (camera, quad) order, then up to `iterations` solves of the summed normal
+    equations, stopping when the step is below 1e-12 or the system is not
+    positive definite; fewer than 6 correspondences keep T0.
+    Returns (obs rows [cam, u, v, X, Y, Z], T, iterations, cost0, cost)."""
+    obs = []
+    for c, quads in enumerate(cam_quads):
+        Twc = T0 @ T_b_c[c]
+        for q in quads:
+            o = quad_cell_obs(np.asarray(q).reshape(4, 2), undistorters[c], Twc[:3, :3], Twc[:3, 3], half, spacing)
+            if o is not None:
+                obs.append(np.concatenate([[c], o]))
+    obs = np.array(obs).reshape(-1, 6)
+    T = np.array(T0, np.float64)
+    if len(obs) < 6:
+        return obs, T, 0, 0.0, 0.0
+    cost0 = cost = None
+    it_done = 0
+    for it in range(iterations):
+        acc = gn_accumulate(T, T_b_c, obs)
+        if it == 0:
+            cost0 = acc[27]
+        cost = acc[27]
+        it_done = it + 1
+        A = np.zeros((6, 6))
+        A[np.triu_indices(6)] = acc[:21]
+        A = A + np.triu(A, 1).T + lam * np.eye(6)
+        try:
+            np.linalg.cholesky(A)
+        except np.linalg.LinAlgError:
+            break
+        T, x = gn_solve(acc, lam, T)
+        if float(x @ x) < 1e-24:
+            break
+    return obs, T, it_done, cost0, cost

@@ -173,9 +173,12 @@ def test_dense_config5_argmin(m720, landmark_map):
 
 def test_rig_gn_refines_pose(landmark_map):
     """cfg.gn_enable (SURVEY a-21, config 3): the batched rig Gauss-Newton
-    (quad corners -> grid intersections, MFMA J^T J / J^T r, 6x6 Cholesky)
-    moves the fused base pose towards the synthetic ground truth and is
-    reproducible run to run; with GN off the result is the reference fusion."""
+    (one correspondence per quad: the crossing of its undistorted diagonals ->
+    the grid cell centre it images; MFMA J^T J / J^T r, 6x6 Cholesky) equals
+    its FP64 restatement (correspondences and pose to 1e-9), moves the fused
+    base pose towards the synthetic ground truth and is reproducible run to
+    run; with GN off the result is the reference fusion."""
+    from test_gpu_multi import check_rig_gn_against_restatement
     import mantis_amd as M
 
     K, D = synth.intrinsics()
@@ -202,6 +205,7 @@ def test_rig_gn_refines_pose(landmark_map):
             again = m.process(imgs, rigs=n_rigs)[0]
             for a, b in zip(res[gn], again):
                 assert list(a.position) == list(b.position) and list(a.orientation_xyzw) == list(b.orientation_xyzw)
+            assert check_rig_gn_against_restatement(m, ext, n_rigs, K, D, 8) >= 3
         m.close()
     e0, e1 = [], []
     for r in range(n_rigs):
