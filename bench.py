@@ -1,28 +1,47 @@
 #!/usr/bin/env python3
 """Benchmark: mantis3 rig poses/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2], the metric's "1280x720 4-cam batch"): rigs
-of 4 fisheye cameras at 1280x720 over the IARC-style grid, shared map
-(params/map.yaml, 720 landmarks); the full reference per-camera path
-(detector -> RPP -> clustering -> scoring -> particle filter -> shifts ->
-yaw -> publish gate) plus the rig fusion, batched `--rigs` rigs per step.
-A step = one mantis_process_batch over the batch; frames are synthetic,
-rendered once into HBM before timing (inputs resident in HBM).
+Workload (default, --config 3; BASELINE.json configs[2], the metric's
+"1280x720 4-cam batch"): rigs of 4 fisheye cameras at 1280x720 over the
+IARC-style grid, shared map (params/map.yaml, 720 landmarks); the full
+reference per-camera path (detector -> RPP -> clustering -> scoring ->
+particle filter -> shifts -> yaw -> publish gate) plus the rig fusion and the
+joint rig Gauss-Newton, batched `--rigs` rigs per step per GPU. Frames are
+synthetic, rendered into HBM before timing (inputs resident in HBM); a second
+leg passes the same frames as pageable host buffers (H2D inside the timed
+region) and is reported beside it as `host_ingest`.
 
-Multi-GPU: one process per GPU (torchrun); rigs are independent units, each
-rank processes its own batch (weak scaling, no collective on the data path);
-barrier + device sync bracket the timed region and the max time over ranks is
-reported. value = rig poses/s of the whole job.
+Other legs (same JSON contract, own metric names):
+  --config 4  BASELINE configs[3]: 8-camera 1920x1080 rigs, camera-sharded
+              across the ranks (mantis_process_rig_sharded: RCCL all-gathers
+              of the particle-filter flags and camera results, one RCCL
+              all-reduce of the J^T J / J^T r accumulators per GN iteration).
+              Strong scaling: every rank holds 8/N cameras of every rig.
+  --config 5  BASELINE configs[4]: 16,200-hypothesis dense grid at 1280x720
+              sharded across ranks (mantis_score_argmin, one RCCL all-gather
+              of (err, index) per frame). Strong scaling.
 
-Also reported: p50 single-rig latency (host submit -> result), the dominant
-kernel's roofline (HIP events on the library stream during the timed region)
-and the CPU oracle baseline timed on this host (rank 0, N=1 only).
+Multi-GPU: one process per GPU. Under torchrun (WORLD_SIZE in the env) this
+process is one rank. `--gpus N` without torchrun makes this process a
+launcher that never touches the GPU: it spawns N ranks of itself with
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and prints rank 0's line.
+Ranks use torch.distributed over gloo (host) for the barriers, the RCCL
+unique-id broadcast and the max-over-ranks time; the data path's collectives
+are the library's own RCCL calls. Config 3 rigs are independent units: each
+rank processes its own batch (weak scaling, no data-path collective).
+
+Also reported (config 3): p50 single-rig latency (host submit -> result,
+device-resident and host frames), the dominant kernel's roofline (HIP events
+on the library stream during the timed region), and the CPU oracle baseline
+timed on this host before the GPU is touched (rank 0, N=1 only): one core and
+all cores (one frame stream per thread).
 """
 import argparse
 import ctypes as C
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,11 +60,10 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector spec
 # (mk_rpp.h jacobi_noise_ff) skips the ~19 sweeps that only shrink the
 # rank-deficient row (the full reference sweep count is 4282 per iteration).
 FLOPS_PER_OBJPOSE_ITER = 1704
-W, H = 1280, 720
-CAMS = 4
 LANDMARKS = 720
 FLOPS_PER_PROJ = 51         # BASELINE.md roofline formulas
 FLOPS_PER_WINDOW = 200
+METRIC3 = "poses/sec + p50 per-frame latency, 1280x720 4-cam batch"
 
 
 def parse():
@@ -53,61 +71,234 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rigs", type=int, default=3072, help="rigs per step per GPU")
-    p.add_argument("--distinct", type=int, default=16, help="distinct rendered rigs (cycled)")
+    p.add_argument("--config", type=int, default=3, choices=(3, 4, 5))
+    p.add_argument("--rigs", type=int, default=None,
+                   help="rigs per step per GPU (config 3, default 3072) / rigs per step (config 4, default 128)")
+    p.add_argument("--frames", type=int, default=16, help="config 5: frames per step (16,200 hypotheses each)")
+    p.add_argument("--distinct", type=int, default=128, help="distinct rendered rigs (cycled through the batch)")
     p.add_argument("--contexts", type=int, default=3,
-                   help="library contexts per GPU, each driven by its own host thread (one ctx per thread, "
-                        "include/mantis.h); the step's rigs are split evenly between them")
+                   help="config 3: library contexts per GPU, each driven by its own host thread (one ctx per "
+                        "thread, include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
-    p.add_argument("--cpu-rigs", type=int, default=6, help="rigs timed on the CPU oracle (bounded sample)")
+    p.add_argument("--ingest-steps", type=int, default=1,
+                   help="config 3: timed steps of the host-ingest leg (pageable host frames); 0 = skip")
+    p.add_argument("--cpu-seconds", type=float, default=8.0,
+                   help="CPU baseline: seconds of oracle work per leg (1 core, all cores)")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="CPU baseline all-cores leg: at most this many threads (the box's CPU share per GPU)")
     p.add_argument("--hw-queues", type=int, default=4,
                    help="GPU_MAX_HW_QUEUES for this process, so the contexts' streams run on separate hardware queues")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--gn", type=int, default=1,
-                   help="joint rig Gauss-Newton after the per-camera pipeline (SURVEY §8 d config 3); 0 = reference-parity only")
+                   help="joint rig Gauss-Newton after the per-camera pipeline (SURVEY §8 d configs 3/4); "
+                        "0 = reference-parity only")
     p.add_argument("--gn-iterations", type=int, default=8)
-    p.add_argument("--max-contour-points", type=int, default=98304,
-                   help="per-frame contour point pool (720p frames use ~22k, max seen 28k; overflow is reported as an error)")
-    return p.parse_args()
+    p.add_argument("--max-contour-points", type=int, default=None,
+                   help="per-frame contour point pool, in 64-point chunks per border (default 98304 at 720p: ~22k "
+                        "points used, max seen 28k; 262144 at 1080p); overflow is an error")
+    a = p.parse_args()
+    if a.rigs is None:
+        a.rigs = 3072 if a.config == 3 else 128
+    if a.max_contour_points is None:
+        a.max_contour_points = 262144 if a.config == 4 else 98304
+    return a
 
 
-def main():
-    a = parse()
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, a.hw_queues))))  # before HIP initialises
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(a):
+    """`--gpus N` without torchrun: spawn N ranks of this script (this process
+    never touches the GPU), forward rank 0's JSON line; when a rank fails the
+    others are stopped and the launcher fails."""
+    import tempfile
+
+    port = _free_port()
+    procs, logs = [], []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        f = tempfile.TemporaryFile(mode="w+")
+        logs.append(f)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=f, stderr=subprocess.STDOUT, text=True))
+    codes = [None] * a.gpus
+    while any(c is None for c in codes):
+        time.sleep(0.2)
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    p.kill()
+                    codes[r] = p.wait()
+    outs = []
+    for f in logs:
+        f.seek(0)
+        outs.append(f.read())
+        f.close()
+    for r, o in enumerate(outs):
+        for ln in o.splitlines():
+            if r != 0 or not ln.startswith("{"):
+                print(f"[rank {r}] {ln}", file=sys.stderr)
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f"bench: rank(s) failed (rank, exit code): {bad}", file=sys.stderr)
+        return 1
+    lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
+    if not lines:
+        print("bench: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
+class Ranks:
+    """torch.distributed over gloo for the host-side bench plumbing (barrier,
+    unique-id broadcast, max time); a no-op at world size 1."""
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import datetime
+
+            import torch.distributed as tdist
+
+            tdist.init_process_group(backend="gloo", timeout=datetime.timedelta(seconds=300))
+            self.dist = tdist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.dist is None:
+            return x
         import torch
-        import torch.distributed as tdist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        tdist.init_process_group(backend=backend)
-        dist = tdist
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
 
-    import mantis_amd as M
+    def seen(self):
+        return self.dist.get_world_size() if self.dist is not None else 1
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def die(rk, msg):
+    print(f"bench rank {rk.rank}/{rk.world}: {msg}", file=sys.stderr, flush=True)
+    sys.exit(1)
+
+
+def make_ctx(M, rk, **cfg):
+    try:
+        return M.Mantis(M.default_config(device=rk.local, **cfg))
+    except M.MantisError as e:
+        die(rk, f"cannot create a library context on device {rk.local} ({e}); this needs an MI355X per rank")
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ------------------------------------------------------------- CPU baseline
+def cpu_baseline(a, W, H, cams_per_rig):
+    """The oracle (C++17 -O3 restatement of the reference path, test
+    infrastructure) on the same synthetic scene, timed on this host BEFORE the
+    GPU is touched: (1) one core, frames one at a time as the reference's
+    single spinner; (2) all cores: one independent frame stream per thread
+    (ctypes releases the GIL inside the oracle), aggregate rig poses/s."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import _oracle as O
     from mantis_amd import synth
 
     white, red, green = synth.load_map()
     K, D = synth.intrinsics(W, H)
+    rng = np.random.default_rng(1000)
+    ext = synth.rig_extrinsics(cams_per_rig)
+    rigs = []
+    for r in range(8):  # the first rigs of rank 0's bench frames (same poses and seeds)
+        Twb = synth.random_base_pose(rng)
+        frames = []
+        for c in range(cams_per_rig):
+            Twc = Twb @ ext[c]
+            frames.append(synth.render_host(synth.make_cam(Twc[:3, :3], Twc[:3, 3], W, H),
+                                            synth.frame_seed(3, r * cams_per_rig + c)))
+        rigs.append(frames)
+
+    def stream(k, budget):
+        orc = O.Oracle(white, red, green, seed=1)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            for fr in rigs[(k + n) % len(rigs)]:
+                orc.process(fr, K, D)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget and n >= 2:
+                return n, dt
+
+    n1, t1 = stream(0, a.cpu_seconds)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    P = max(1, min(a.cpu_threads, avail))
+    with ThreadPoolExecutor(max_workers=P) as ex:
+        t0 = time.perf_counter()
+        res = list(ex.map(lambda k: stream(k, a.cpu_seconds), range(P)))
+        tall = time.perf_counter() - t0
+    nall = sum(n for n, _ in res)
+    return {"value": round(nall / tall, 4), "unit": "rig poses/s", "cores": P, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": avail,
+            "single_core": {"value": round(n1 / t1, 4), "p50_rig_ms": round(t1 / n1 * 1e3, 1), "rigs": n1},
+            "sample": f"oracle/liboracle.so (C++17 -O3, full mantis3 callback per camera) on {len(rigs)} distinct "
+                      f"{cams_per_rig}x{W}x{H} rigs of the bench scene: {nall} rigs over {P} threads (one frame "
+                      f"stream each) in {tall:.1f} s; 1 core: {n1} rigs in {t1:.1f} s"}
+
+
+# -------------------------------------------------------------------- config 3
+def run_config3(a, rk, cpu):
+    import mantis_amd as M
+    from mantis_amd import synth
+
+    W, H, CAMS = 1280, 720, 4
+    white, red, green = synth.load_map()
+    K, D = synth.intrinsics(W, H)
     n_frames = a.rigs * CAMS
     nctx = max(1, min(a.contexts, a.rigs))
-    assert a.rigs % nctx == 0, "--rigs must be a multiple of --contexts"
+    if a.rigs % nctx:
+        die(rk, "--rigs must be a multiple of --contexts")
     rigs_ctx = a.rigs // nctx
     ctxs = []
     for _ in range(nctx):
-        mc = M.Mantis(M.default_config(device=local, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H,
-                                       gn_enable=a.gn, gn_iterations=a.gn_iterations,
-                                       max_contour_points=a.max_contour_points))
+        mc = make_ctx(M, rk, max_cams=rigs_ctx * CAMS, max_width=W, max_height=H, gn_enable=a.gn,
+                      gn_iterations=a.gn_iterations, max_contour_points=a.max_contour_points)
         mc.set_map(white, red, green)
         ctxs.append(mc)
     m = ctxs[0]
 
     # ---- synthetic rigs rendered into HBM once
-    rng = np.random.default_rng(1000 + rank)
+    rng = np.random.default_rng(1000 + rk.rank)
     ext = synth.rig_extrinsics(CAMS)
     cams, Tbc = [], []
     for r in range(a.distinct):
@@ -119,63 +310,45 @@ def main():
     nd = len(cams)
     fb = W * H * 3
     dev = m.device_alloc(nd * fb)
-    seeds = [synth.frame_seed(3, i + 100000 * rank) for i in range(nd)]
+    seeds = [synth.frame_seed(3, i + 100000 * rk.rank) for i in range(nd)]
     m.synth_render(cams, seeds, dev)
     m.synchronize()
-    imgs = []
-    for i in range(n_frames):
-        j = i % nd
-        imgs.append(M.make_image(None, K, D, T_base_cam=Tbc[j], device_ptr=dev + j * fb, width=W, height=H))
+    imgs = [M.make_image(None, K, D, T_base_cam=Tbc[i % nd], device_ptr=dev + (i % nd) * fb, width=W, height=H)
+            for i in range(n_frames)]
     per_ctx = [imgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS] for k in range(nctx)]
     from concurrent.futures import ThreadPoolExecutor
 
     pool = ThreadPoolExecutor(max_workers=nctx)
 
-    def run_step():
+    def run_step(parts):
         """One step: every context processes its share of the rigs, concurrently."""
-        futs = [pool.submit(ctxs[k].process, per_ctx[k], rigs_ctx) for k in range(nctx)]
+        futs = [pool.submit(ctxs[k].process, parts[k], rigs_ctx) for k in range(nctx)]
         outs = [f.result() for f in futs]
-        rig = [r for o in outs for r in o[0]]
-        cam = [c for o in outs for c in o[1]]
-        return rig, cam
+        return [r for o in outs for r in o[0]], [c for o in outs for c in o[1]]
 
     def barrier_sync():
-        if dist is not None:
-            dist.barrier()
+        rk.barrier()
         for mc in ctxs:
             mc.synchronize()
 
-    # ---- warmup
     for _ in range(a.warmup):
-        run_step()
+        run_step(per_ctx)
 
-    # ---- timed region: stage events on the library stream
+    # ---- timed region: stage events on context 0's stream
     m.set_profiling(True)
-    stage_ms = {}
-    scored = 0
-    published = 0
+    stage_ms, scored, published = {}, 0, 0
     barrier_sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        rig, cam = run_step()
+        rig, cam = run_step(per_ctx)
         for name, ms in m.kernel_times():
             stage_ms[name] = stage_ms.get(name, 0.0) + ms
         scored += sum(c.n_scored for c in cam)
         published += sum(r.publish for r in rig)
     barrier_sync()
-    elapsed = time.perf_counter() - t0
+    elapsed = rk.max(time.perf_counter() - t0)
     m.set_profiling(False)
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        if torch.cuda.is_available():
-            t = t.cuda()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    poses = a.rigs * a.steps * world
-    value = poses / elapsed
+    value = a.rigs * a.steps * rk.world / elapsed
     ms_per_step = elapsed / a.steps * 1e3
 
     # ---- per-step work counts (every step processes the same frames, so the
@@ -195,7 +368,6 @@ def main():
 
     # ---- roofline of the dominant stage (per launch = per step on context 0)
     avg = {k: v / a.steps for k, v in stage_ms.items()}
-    # algorithmic bytes (HBM-bound stages) or FP64 flops (VALU-bound stages) per launch
     work = {
         # BGR read once; candidate and strong-root bit planes written
         "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
@@ -208,7 +380,6 @@ def main():
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
         "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),
-
         "score_pf_yaw": ("fp64", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
@@ -261,62 +432,254 @@ def main():
         roof["stages_ms_isolated"] = {k: round(v, 4) for k, v in sorted(iso.items(), key=lambda kv: -kv[1])}
     path_bytes = n_frames * (6 * W * H + 3 * (s_fast + s_slow))
 
-    # ---- p50 latency of one rig (host submit -> result on host)
-    lat = []
-    one = imgs[:CAMS]
-    for _ in range(a.latency_iters):
-        t1 = time.perf_counter()
-        m.process(one, rigs=1)
-        lat.append(time.perf_counter() - t1)
-    p50 = float(np.median(lat)) * 1e3
-
-    # ---- CPU baseline: the oracle (C++ -O2 restatement) on a bounded sample, 1 core
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        try:
-            import _oracle as O
-
-            orc = O.Oracle(white, red, green, seed=1)
-            host = [np.zeros((H, W, 3), np.uint8) for _ in range(a.cpu_rigs * CAMS)]
-            for i in range(len(host)):
-                m.d2h(host[i], dev + (i % nd) * fb)
+    # ---- p50 latency of one rig (host submit -> result on host), HBM frames
+    def p50_of(one):
+        lat = []
+        for _ in range(a.latency_iters):
             t1 = time.perf_counter()
-            for i in range(len(host)):
-                orc.process(host[i], K, D)
-            dt = time.perf_counter() - t1
-            cpu = {"value": round(a.cpu_rigs / dt, 4), "unit": "rig poses/s", "cores": 1, "kind": "port",
-                   "sample": f"{a.cpu_rigs} rigs x {CAMS} cams 1280x720 through oracle/liboracle.so "
-                             f"(full mantis3 callback per camera), {dt:.1f} s on 1 host core"}
-        except Exception as e:  # the oracle is optional on a box without it
-            cpu = {"value": None, "unit": "rig poses/s", "cores": 1, "kind": "port", "sample": f"unavailable: {e}"}
+            m.process(one, rigs=1)
+            lat.append(time.perf_counter() - t1)
+        return float(np.median(lat)) * 1e3
 
-    if rank == 0:
+    p50 = p50_of(imgs[:CAMS])
+
+    # ---- host-ingest leg: the same frames as pageable host BGR buffers (what
+    # a ROS drop-in hands over); the H2D staging is inside the timed region
+    ingest = None
+    host = [np.empty((H, W, 3), np.uint8) for _ in range(nd)]
+    for j in range(nd):
+        m.d2h(host[j], dev + j * fb)
+    himgs = [M.make_image(host[i % nd], K, D, T_base_cam=Tbc[i % nd]) for i in range(n_frames)]
+    p50_host = p50_of(himgs[:CAMS])
+    if a.ingest_steps > 0:
+        hper = [himgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS] for k in range(nctx)]
+        run_step(hper)  # one untimed pass over the host path
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(a.ingest_steps):
+            run_step(hper)
+        barrier_sync()
+        el = rk.max(time.perf_counter() - t0)
+        h2d_bytes = n_frames * fb * a.ingest_steps
+        ingest = {"value": round(a.rigs * a.ingest_steps * rk.world / el, 3), "unit": "rig poses/s",
+                  "ms_per_step": round(el / a.ingest_steps * 1e3, 3), "steps": a.ingest_steps,
+                  "h2d_GBps_per_gpu": round(h2d_bytes / el / 1e9, 2),
+                  "p50_latency_ms": round(p50_host, 3),
+                  "note": "frames passed as pageable host BGR buffers (mem_kind 0); staging H2D inside the timed "
+                          "region; never the headline value"}
+    del host, himgs
+
+    line = None
+    if rk.rank == 0:
         line = {
-            "metric": "poses/sec + p50 per-frame latency, 1280x720 4-cam batch",
-            "value": round(value, 3), "unit": "rig poses/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC3,
+            "value": round(value, 3), "unit": "rig poses/s", "n_gpus": rk.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic fisheye grid frames rendered in HBM (SURVEY §8d scene), map.yaml landmarks",
+            "data": f"synthetic fisheye grid frames rendered in HBM (SURVEY §8d scene, {a.distinct} distinct rigs "
+                    f"= {nd * fb / 1e9:.2f} GB cycled), map.yaml landmarks",
             "config": {"workload": "config3: 4-cam 1280x720 rig, shared map, full mantis3 path per camera"
-                                    + (" + joint rig Gauss-Newton" if a.gn else ""),
+                                   + (" + joint rig Gauss-Newton" if a.gn else ""),
                        "rigs_per_step_per_gpu": a.rigs, "cams_per_rig": CAMS, "frames_per_step_per_gpu": n_frames,
-                       "contexts_per_gpu": nctx,
-                       "resolution": [W, H], "landmarks": LANDMARKS, "parallelism": f"rig-data-parallel x{world}"},
+                       "contexts_per_gpu": nctx, "resolution": [W, H], "landmarks": LANDMARKS,
+                       "parallelism": f"rig-data-parallel x{rk.world}"},
+            "ranks_seen": rk.seen(),
             "p50_latency_ms": round(p50, 3),
             "camera_frames_per_s": round(value * CAMS, 2),
             "published_frac": round(published / max(1, a.rigs * a.steps), 4),
             "path_alg_GBps": round(path_bytes * a.steps / elapsed / 1e9, 3),
+            "host_ingest": ingest,
             "roofline": roof,
             "roofline_frontend": roof_front,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     pool.shutdown()
     for mc in ctxs:
         mc.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return line
+
+
+# -------------------------------------------------------------------- config 4
+def run_config4(a, rk):
+    """8-camera 1920x1080 rigs, camera c on rank c % N (mantis_process_rig_sharded)."""
+    import mantis_amd as M
+    from mantis_amd import rig as RG
+    from mantis_amd import synth
+
+    W, H, CAMS = 1920, 1080, 8
+    if rk.world > CAMS:
+        die(rk, "config 4 shards 8 cameras: at most 8 ranks")
+    K, D = synth.intrinsics(W, H)
+    mine = RG.shard_cameras(CAMS, rk.rank, rk.world)
+    nl = len(mine)
+    m = make_ctx(M, rk, max_cams=a.rigs * nl, max_width=W, max_height=H, gn_enable=a.gn,
+                 gn_iterations=a.gn_iterations, max_contour_points=a.max_contour_points)
+    m.set_map(*synth.load_map())
+    m.comm_init(rk.rank, rk.world, rk.dist)
+    nranks, _ = m.comm_info()
+    rng = np.random.default_rng(4000)  # the same rigs on every rank
+    ext = synth.rig_extrinsics(CAMS)
+    distinct = min(a.distinct, a.rigs)
+    cams, Tbc, seeds = [], [], []
+    for r in range(distinct):
+        Twb = synth.random_base_pose(rng)
+        for c in mine:
+            Twc = Twb @ ext[c]
+            cams.append(synth.make_cam(Twc[:3, :3], Twc[:3, 3], W, H))
+            Tbc.append(ext[c])
+            seeds.append(synth.frame_seed(4, r * CAMS + c))
+    fb = W * H * 3
+    dev = m.device_alloc(len(cams) * fb)
+    m.synth_render(cams, seeds, dev)
+    m.synchronize()
+    nd = len(cams)
+    imgs = [M.make_image(None, K, D, T_base_cam=Tbc[i % nd], device_ptr=dev + (i % nd) * fb, width=W, height=H)
+            for i in range(a.rigs * nl)]
+    for _ in range(a.warmup):
+        m.process_sharded(imgs, a.rigs, mine, CAMS)
+    m.set_profiling(True)
+    stage_ms, published, gn_its = {}, 0, 0
+    rk.barrier()
+    m.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        rr, _ = m.process_sharded(imgs, a.rigs, mine, CAMS)
+        for name, ms in m.kernel_times():
+            stage_ms[name] = stage_ms.get(name, 0.0) + ms
+        published += sum(r.publish for r in rr)
+        gn_its += sum(r.gn_iterations for r in rr)
+    m.synchronize()
+    rk.barrier()
+    elapsed = rk.max(time.perf_counter() - t0)
+    m.set_profiling(False)
+    lat = []
+    for _ in range(a.latency_iters):
+        rk.barrier()
+        t1 = time.perf_counter()
+        m.process_sharded(imgs[:nl], 1, mine, CAMS)
+        lat.append(rk.max(time.perf_counter() - t1))
+    line = None
+    if rk.rank == 0:
+        avg = {k: round(v / a.steps, 4) for k, v in sorted(stage_ms.items(), key=lambda kv: -kv[1])}
+        frames = a.rigs * nl
+        canny = avg.get("canny_nms")
+        roof = None
+        if canny:
+            alg = frames * (3 * W * H + W * H // 4)
+            ach = alg / (canny * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": "canny_nms", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "alg_bytes_per_launch": alg, "avg_launch_ms": canny, "stages_ms": avg}
+        line = {"metric": "8-cam 1920x1080 rig poses/s, camera-sharded (config 4)",
+                "value": round(a.rigs * a.steps / elapsed, 3), "unit": "rig poses/s", "n_gpus": rk.world,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic fisheye grid frames rendered in HBM, map.yaml landmarks",
+                "config": {"workload": "config4: 8-cam 1920x1080 rig, camera c on rank c % N, RCCL all-gathers of "
+                                       "PF flags and camera results, RCCL all-reduce of J^T J / J^T r per GN "
+                                       "iteration", "rigs_per_step": a.rigs, "cams_per_rank": nl,
+                           "resolution": [W, H], "parallelism": f"camera-sharded x{rk.world}"},
+                "rccl_ranks": nranks, "ranks_seen": rk.seen(),
+                "p50_latency_ms": round(float(np.median(lat)) * 1e3, 3),
+                "published_frac": round(published / max(1, a.rigs * a.steps), 4),
+                "gn_iterations_per_rig": round(gn_its / max(1, a.rigs * a.steps), 3),
+                "roofline": roof}
+    m.close()
+    return line
+
+
+# -------------------------------------------------------------------- config 5
+def run_config5(a, rk):
+    """16,200-hypothesis dense grid per frame, hypotheses sharded across ranks."""
+    import mantis_amd as M
+    from mantis_amd import dense, synth
+
+    W, H = 1280, 720
+    K, D = synth.intrinsics(W, H)
+    m = make_ctx(M, rk, max_cams=1, max_width=W, max_height=H)
+    m.set_map(*synth.load_map())
+    m.comm_init(rk.rank, rk.world, rk.dist)
+    nranks, _ = m.comm_info()
+    rng = np.random.default_rng(2024)
+    fb = W * H * 3
+    nf = max(1, a.frames)
+    dev = m.device_alloc(nf * fb)
+    work = []
+    for f in range(nf):
+        R, pos = synth.random_pose(rng)
+        m.synth_render([synth.make_cam(R, pos, W, H)], [synth.frame_seed(5, f)], dev + f * fb)
+        m.synchronize()
+        img = M.make_image(None, K, D, device_ptr=dev + f * fb, width=W, height=H)
+        _, mask = m.masks(img)
+        hyps = dense.config5_hypotheses(R, pos, np.random.default_rng(7 + f))
+        lo, hi = dense.shard_range(len(hyps), rk.rank, rk.world)
+        work.append((img, mask, np.ascontiguousarray(hyps[lo:hi]), lo, len(hyps)))
+
+    def step():
+        return [m.score_argmin(img, mine, lo, True, mask) for img, mask, mine, lo, _ in work]
+
+    for _ in range(a.warmup):
+        step()
+    m.set_profiling(True)
+    kt = 0.0
+    rk.barrier()
+    m.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        for img, mask, mine, lo, _ in work:
+            m.score_argmin(img, mine, lo, True, mask)
+            kt += dict(m.kernel_times()).get("score_dense", 0.0)
+    m.synchronize()
+    rk.barrier()
+    elapsed = rk.max(time.perf_counter() - t0)
+    best0 = step()[0]  # every rank takes part in the exchange
+    line = None
+    if rk.rank == 0:
+        n_h = sum(w[4] for w in work)
+        kavg = kt / (a.steps * nf)
+        flops = FLOPS_PER_PROJ * float(LANDMARKS) * len(work[0][2])
+        ach = flops / (kavg * 1e-3) / 1e12 if kavg > 0 else 0.0
+        line = {"metric": "dense hypothesis scoring (config 5), hypotheses/s",
+                "value": round(n_h * a.steps / elapsed, 1), "unit": "hypotheses/s", "n_gpus": rk.world,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic fisheye grid frames in HBM, map.yaml landmarks",
+                "config": {"workload": "config5: 1280x720, 81 shifts x 4 yaws x 50 perturbations per frame",
+                           "frames_per_step": nf, "hypotheses_per_frame": work[0][4], "landmarks": LANDMARKS,
+                           "parallelism": f"hypothesis-sharded x{rk.world}"},
+                "rccl_ranks": nranks, "ranks_seen": rk.seen(),
+                "best_frame0": list(best0),
+                "roofline": {"bound": "fp64_valu", "kernel": "k_score_api", "achieved": round(ach, 4),
+                             "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / FP64_PEAK_TFLOPS, 5),
+                             "traffic": None, "avg_launch_ms": round(kavg, 4), "alg_flops_per_launch": int(flops)}}
+    m.close()
+    return line
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(a)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world} (run under torchrun with --nproc-per-node "
+              f"{a.gpus}, or without torchrun to let bench.py spawn the ranks)", file=sys.stderr)
+        return 2
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, a.hw_queues))))  # before HIP initialises
+    cpu = None
+    if a.config == 3 and world == 1 and not a.no_cpu:
+        try:
+            cpu = cpu_baseline(a, 1280, 720, 4)  # before any GPU work: nothing else runs on the host cores
+        except Exception as e:  # the oracle is optional on a box without it
+            cpu = {"value": None, "unit": "rig poses/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    rk = Ranks()
+    line = {3: lambda: run_config3(a, rk, cpu), 4: lambda: run_config4(a, rk), 5: lambda: run_config5(a, rk)}[
+        a.config]()
+    if line is not None:
+        print(json.dumps(line), flush=True)
+    rk.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

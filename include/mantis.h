@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MANTIS_ABI_VERSION 1
+#define MANTIS_ABI_VERSION 2
 
 typedef enum mantis_status {
   MANTIS_OK = 0,
@@ -60,9 +60,11 @@ typedef struct mantis_config {
   double grid_spacing;          /* ~grid_spacing, 0.32 (:167) */
   int32_t particles, iterations;/* 50, 10 (PoseAdjustment.h:29) */
   int32_t gn_enable;            /* 0 = reference-parity mode (no GN refinement) */
-  int32_t gn_iterations;        /* rig GN iterations (<= 10) */
-  int32_t max_quads;            /* per-frame quad capacity (default 256) */
+  int32_t gn_iterations;        /* rig GN iterations (0..10) */
+  int32_t max_quads;            /* per-frame quad capacity: 256 (0 = default); other values are rejected */
   int32_t max_contour_points;   /* per-frame contour point pool (default 262144) */
+  int32_t quad_gn_iterations;   /* per-quad GN after RPP (4 corners <-> model square), 0 = off (parity) */
+  int32_t pad0;
 } mantis_config;
 
 typedef struct mantis_image {   /* sensor_msgs/Image (bgr8) + sensor_msgs/CameraInfo */
@@ -194,6 +196,18 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
  * -1 rotation check failed = the reference's exit(1)). */
 mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
                                double* t, double* errs, int32_t* rpp_status);
+
+/* Per-quad Gauss-Newton after RPP (new stage; legacy analogue
+ * cv::solvePnP ITERATIVE, include/legacy/mantis2/PoseEstimator.h:91-153): n
+ * problems of 4 normalized image points img_pts (n x 4 x 2) and model points
+ * obj_pts (n x 4 x 3); R (n x 9), t (n x 3) hold the starting pose (model ->
+ * camera, e.g. mantis_rpp_batch's) and receive the refined one. Up to
+ * `iterations` steps minimizing the normalized reprojection error; a step is
+ * kept only if the cost decreases. steps (n, nullable) = steps kept, costs
+ * (n x 2, nullable) = r^T r before / after. The same refinement runs inside
+ * the pipeline after RPP when cfg.quad_gn_iterations > 0. */
+mantis_status mantis_quad_gn(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
+                             double* t, int32_t iterations, int32_t* steps, double* costs);
 
 /* Dense scoring with an argmin (BASELINE config 5: 81 shifts x 4 yaws x 50
  * perturbations = 16,200 hypotheses, SURVEY §8 d/e): the fast evaluator

@@ -25,7 +25,8 @@ class MantisConfig(C.Structure):
                 ("canny_low", C.c_int32), ("polygon_epsilon", C.c_int32),
                 ("search_radius_multiplier", C.c_double), ("grid_spacing", C.c_double),
                 ("particles", C.c_int32), ("iterations", C.c_int32), ("gn_enable", C.c_int32),
-                ("gn_iterations", C.c_int32), ("max_quads", C.c_int32), ("max_contour_points", C.c_int32)]
+                ("gn_iterations", C.c_int32), ("max_quads", C.c_int32), ("max_contour_points", C.c_int32),
+                ("quad_gn_iterations", C.c_int32), ("pad0", C.c_int32)]
 
 
 class MantisImage(C.Structure):
@@ -105,6 +106,8 @@ _SIGS = {
                                           C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_rpp_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    "mantis_quad_gn": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
+                                 C.c_void_p, C.c_void_p]),
     "mantis_synth_render": (C.c_int, [C.c_void_p, C.POINTER(SynthCamC), C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "mantis_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -397,6 +400,19 @@ class Mantis:
         self._chk(lib().mantis_rpp_batch(self.h, img_pts.ctypes.data, obj_pts.ctypes.data, n, R.ctypes.data,
                                          t.ctypes.data, e.ctypes.data, s.ctypes.data), "rpp_batch")
         return R.reshape(n, 3, 3), t, e, s
+
+    def quad_gn(self, img_pts, obj_pts, R, t, iterations):
+        """Per-quad GN after RPP (mantis_quad_gn): (R, t, steps, costs)."""
+        img_pts = np.ascontiguousarray(img_pts, np.float64).reshape(-1, 4, 2)
+        obj_pts = np.ascontiguousarray(obj_pts, np.float64).reshape(-1, 4, 3)
+        n = len(img_pts)
+        R = np.ascontiguousarray(R, np.float64).reshape(n, 9).copy()
+        t = np.ascontiguousarray(t, np.float64).reshape(n, 3).copy()
+        steps = np.zeros(n, np.int32)
+        costs = np.zeros((n, 2))
+        self._chk(lib().mantis_quad_gn(self.h, img_pts.ctypes.data, obj_pts.ctypes.data, n, R.ctypes.data,
+                                       t.ctypes.data, iterations, steps.ctypes.data, costs.ctypes.data), "quad_gn")
+        return R.reshape(n, 3, 3), t, steps, costs
 
     # device buffers -------------------------------------------------------
     def device_alloc(self, nbytes):

@@ -352,7 +352,7 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
 }
 
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
-                       RppOut* out, FrameState* st, size_t ni, size_t expected_items) {
+                       RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads) {
   k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q, st);
   mark(c, "rpp_first");
   k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
@@ -360,7 +360,8 @@ void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, 
   mark(c, "rpp_2nd");
   k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st);
   mark(c, "rpp_cand");
-  k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out);
+  k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out, quads,
+                                                               quads ? c->cfg.quad_gn_iterations : 0);
   mark(c, "rpp_merge");
 }
 
@@ -370,7 +371,8 @@ mantis_status run_pose(Ctx* c, int n) {
   k_rpp_prep<<<gr, 256, 0, c->s>>>(c->d_quads, c->d_st, c->d_items, c->d_jobs0, c->d_rq, c->cfg.grid_spacing / 2);
   const size_t ni = (size_t)n * kMaxQuads * 2;
   mark(c, "rpp_prep");
-  launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160);
+  launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160,
+                    c->d_quads);
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
   HIP_OK(hipGetLastError());
@@ -666,6 +668,7 @@ void mantis_default_config(mantis_config* cfg) {
   cfg->gn_iterations = 10;
   cfg->max_quads = kMaxQuads;
   cfg->max_contour_points = 262144;
+  cfg->quad_gn_iterations = 0;
 }
 
 mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
@@ -680,9 +683,18 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     }
     cfg = *cfg_in;
   }
-  if (cfg.particles < 1 || cfg.particles > 96 || cfg.iterations < 0 || cfg.max_cams < 1 || cfg.max_width < 3 ||
-      cfg.max_height < 3) {
-    g_create_err = "invalid config";
+  if (cfg.max_quads == 0) cfg.max_quads = kMaxQuads;
+  // iterations bound: particles * iterations * 6 gaussians per frame must stay
+  // far inside int32 for the offset scan (k_gauss_offsets)
+  if (cfg.particles < 1 || cfg.particles > 96 || cfg.iterations < 0 || cfg.iterations > 1000 || cfg.max_cams < 1 ||
+      cfg.max_width < 3 || cfg.max_height < 3 || cfg.gn_iterations < 0 || cfg.gn_iterations > 10 ||
+      cfg.quad_gn_iterations < 0 || cfg.quad_gn_iterations > 20) {
+    g_create_err = "invalid config (particles 1..96, iterations 0..1000, gn_iterations 0..10, "
+                   "quad_gn_iterations 0..20, max_cams >= 1, image >= 3x3)";
+    return MANTIS_ERR_ARG;
+  }
+  if (cfg.max_quads != kMaxQuads) {
+    g_create_err = "max_quads: the per-frame quad capacity is fixed at 256 in this build";
     return MANTIS_ERR_ARG;
   }
   int ndev = 0;
@@ -1136,6 +1148,32 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
   return MANTIS_OK;
 }
 
+mantis_status mantis_quad_gn(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
+                             double* t, int32_t iterations, int32_t* steps, double* costs) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !img_pts || !obj_pts || n <= 0 || !R || !t || iterations < 0 || iterations > 100) return MANTIS_ERR_ARG;
+  double *d_ip, *d_op, *d_R, *d_t, *d_c;
+  int32_t* d_s;
+  if (dalloc(c, &d_ip, (size_t)8 * n) || dalloc(c, &d_op, (size_t)12 * n) || dalloc(c, &d_R, (size_t)9 * n) ||
+      dalloc(c, &d_t, (size_t)3 * n) || dalloc(c, &d_c, (size_t)2 * n) || dalloc(c, &d_s, (size_t)n))
+    return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 8 * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_R, R, sizeof(double) * 9 * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_t, t, sizeof(double) * 3 * n, hipMemcpyHostToDevice, c->s));
+  k_quad_gn<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_R, d_t, iterations, d_s, d_c);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(R, d_R, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(t, d_t, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, c->s));
+  if (steps) HIP_OK(hipMemcpyAsync(steps, d_s, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->s));
+  if (costs) HIP_OK(hipMemcpyAsync(costs, d_c, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  void* ps[] = {d_ip, d_op, d_R, d_t, d_c, d_s};
+  for (void* p : ps) (void)hipFree(p);
+  return MANTIS_OK;
+}
+
 mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
                                double* t, double* errs, int32_t* rpp_status) {
   Ctx* c = (Ctx*)ctx;
@@ -1157,7 +1195,7 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
   mark(c, "start");
   k_rpp_prep_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it, d_j0, d_q);
   mark(c, "rpp_prep");
-  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, nullptr, (size_t)n, (size_t)n);
+  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, nullptr, (size_t)n, (size_t)n, nullptr);
   HIP_OK(hipGetLastError());
   std::vector<RppOut> h(n);
   HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));

@@ -1,53 +1,17 @@
 // Gauss–Newton rig refinement (new stage) and the RCCL
 // exchange of its accumulators for camera-sharded rigs (§8 e). Included by
-// api.hip (shares its Ctx).
-//
-// Residuals: r = pi(p) - u with p = inv(T_b_c) inv(T_w_b) X the world point
-// X in camera c, u the observed normalized (undistorted) image point and
-// pi(p) = (p_x/p_z, p_y/p_z). Right perturbation T_w_b <- T_w_b Exp(delta),
-// delta = (rho, phi): dp/d(delta) = R_cb [ -I | [q]x ], q = inv(T_w_b) X.
-// The 28 accumulated doubles are the upper triangle of J^T J (21), J^T r (6)
-// and r^T r (1): with M = [J | r] (rows = residual components) all of them
-// are entries of M^T M, which one wave builds with v_mfma_f64_16x16x4_f64,
-// 4 residual rows per instruction.
+// api.hip (shares its Ctx). The residual rows, the 6x6 solve and the
+// correspondences are in mk_gn.h (shared with the host build of the tests);
+// here M^T M of M = [J | r] is built by one wave per rig with
+// v_mfma_f64_16x16x4_f64, 4 residual rows per instruction.
 #include <rccl/rccl.h>
+
+#include "mk_gn.h"
 
 namespace mk {
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-
-// value of M[row][col] (col 0..5 = J, 6 = r, else 0) for one residual row
-__device__ inline double gn_entry(const double* Rwb_t, const double* twb, const GnCam* cams, const double* obs,
-                                  int n_obs, int row, int col) {
-  if (col > 6) return 0.0;
-  int i = row >> 1, comp = row & 1;
-  if (i >= n_obs) return 0.0;
-  const double* o = obs + 6 * (size_t)i;
-  const GnCam& cm = cams[(int)o[0]];
-  // q = inv(T_w_b) X = R_wb^T (X - t_wb)
-  double d[3] = {o[3] - twb[0], o[4] - twb[1], o[5] - twb[2]};
-  double q[3];
-  for (int a = 0; a < 3; a++) q[a] = Rwb_t[3 * a] * d[0] + Rwb_t[3 * a + 1] * d[1] + Rwb_t[3 * a + 2] * d[2];
-  double p[3];
-  for (int a = 0; a < 3; a++)
-    p[a] = cm.R_cb[3 * a] * q[0] + cm.R_cb[3 * a + 1] * q[1] + cm.R_cb[3 * a + 2] * q[2] + cm.t_cb[a];
-  double iz = 1.0 / p[2];
-  if (col == 6) return (comp == 0 ? p[0] : p[1]) * iz - (comp == 0 ? o[1] : o[2]);
-  // dpi/dp row
-  double g[3];
-  if (comp == 0) { g[0] = iz; g[1] = 0; g[2] = -p[0] * iz * iz; }
-  else { g[0] = 0; g[1] = iz; g[2] = -p[1] * iz * iz; }
-  // h = g^T R_cb (1x3)
-  double h[3];
-  for (int b = 0; b < 3; b++) h[b] = g[0] * cm.R_cb[b] + g[1] * cm.R_cb[3 + b] + g[2] * cm.R_cb[6 + b];
-  if (col < 3) return -h[col];
-  // h [q]x column: [q]x = [[0,-qz,qy],[qz,0,-qx],[-qy,qx,0]]
-  int k = col - 3;
-  if (k == 0) return h[1] * q[2] - h[2] * q[1];
-  if (k == 1) return -h[0] * q[2] + h[2] * q[0];
-  return h[0] * q[1] - h[1] * q[0];
-}
 
 __global__ __launch_bounds__(256) void k_gn_accum(const double* __restrict__ Twb, const GnCam* __restrict__ cams,
                                                   const double* __restrict__ obs, int n_obs, double* __restrict__ out28) {
@@ -80,110 +44,11 @@ __global__ __launch_bounds__(256) void k_gn_accum(const double* __restrict__ Twb
   }
 }
 
-// (J^T J + lambda I) delta = -J^T r from the 28 accumulators by Cholesky, then
-// T_w_b <- T_w_b Exp(delta) (right perturbation: translation delta[0..2],
-// rotation vector delta[3..5] through Rodrigues). Returns false when the
-// normal matrix is not positive definite (too few observations). Shared by
-// mantis_gn_solve (host) and the batched rig kernel.
-MK_HD bool gn_solve6(const double* acc28, double lambda, double* T_w_b, double* delta6) {
-  double A[6][6], b[6];
-  int n = 0;
-  for (int i = 0; i < 6; i++)
-    for (int j = i; j < 6; j++) { A[i][j] = A[j][i] = acc28[n++]; }
-  for (int i = 0; i < 6; i++) { A[i][i] += lambda; b[i] = -acc28[21 + i]; }
-  double L[6][6];
-  for (int i = 0; i < 6; i++)
-    for (int j = 0; j < 6; j++) L[i][j] = 0;
-  for (int i = 0; i < 6; i++)
-    for (int j = 0; j <= i; j++) {
-      double s = A[i][j];
-      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
-      if (i == j) {
-        if (!(s > 0)) return false;
-        L[i][i] = sqrt(s);
-      } else {
-        L[i][j] = s / L[j][j];
-      }
-    }
-  double y[6], x[6];
-  for (int i = 0; i < 6; i++) {
-    double s = b[i];
-    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
-    y[i] = s / L[i][i];
-  }
-  for (int i = 5; i >= 0; i--) {
-    double s = y[i];
-    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
-    x[i] = s / L[i][i];
-  }
-  if (delta6)
-    for (int i = 0; i < 6; i++) delta6[i] = x[i];
-  const double* w = x + 3;
-  const double th = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-  const double K[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-  double a, bb;
-  if (th < 1e-12) { a = 1.0; bb = 0.5; }
-  else { a = sin(th) / th; bb = (1 - cos(th)) / (th * th); }
-  double dR[9];
-  for (int i = 0; i < 3; i++)
-    for (int j = 0; j < 3; j++) {
-      double s = 0;
-      for (int k = 0; k < 3; k++) s += K[i * 3 + k] * K[k * 3 + j];
-      dR[i * 3 + j] = (i == j ? 1.0 : 0.0) + a * K[i * 3 + j] + bb * s;
-    }
-  const double D[16] = {dR[0], dR[1], dR[2], x[0], dR[3], dR[4], dR[5], x[1], dR[6], dR[7], dR[8], x[2], 0, 0, 0, 1};
-  double r[16];
-  for (int i = 0; i < 4; i++)
-    for (int j = 0; j < 4; j++) {
-      double s = 0;
-      for (int k = 0; k < 4; k++) s += T_w_b[i * 4 + k] * D[k * 4 + j];
-      r[i * 4 + j] = s;
-    }
-  for (int i = 0; i < 16; i++) T_w_b[i] = r[i];
-  return true;
-}
-
 // ------------------------------------------------ batched rig GN (pipeline)
-// cfg.gn_enable: after the per-camera pipeline and the rig fusion, one block
-// per rig refines the base pose over all its cameras' quads. A detected quad
-// is the dark inside of one grid cell, so its centre is the cell centre; in
-// the undistorted normalized image (a perspective view) the centre of the
-// square is exactly where the quad's diagonals cross. Each quad gives that
-// point, back-projected with the fused pose onto the floor and snapped to the
-// nearest cell centre (-1.28 + 0.32 k of the map's grid; accepted within
-// 0.1 m). The list is compacted in item order (block scan), so the MFMA sums
-// are reproducible.
-
-__device__ inline bool gn_quad_obs(const FrameDesc& fd, const QuadRec& q, const double* Rwc, const double* Cw,
-                                   double half, double spacing, double* o) {
-  double u[4], v[4];
-  for (int k = 0; k < 4; k++) undistort(fd.cam, (double)q.c[2 * k], (double)q.c[2 * k + 1], &u[k], &v[k]);
-  // diagonals p0-p2 and p1-p3: p0 + a (p2 - p0) = p1 + b (p3 - p1)
-  const double d1x = u[2] - u[0], d1y = v[2] - v[0], d2x = u[3] - u[1], d2y = v[3] - v[1];
-  const double den = d1x * d2y - d1y * d2x;
-  if (fabs(den) < 1e-12) return false;
-  const double a = ((u[1] - u[0]) * d2y - (v[1] - v[0]) * d2x) / den;
-  if (!(a > 0 && a < 1)) return false;
-  const double uc = u[0] + a * d1x, vc = v[0] + a * d1y;
-  const double dw[3] = {Rwc[0] * uc + Rwc[1] * vc + Rwc[2], Rwc[3] * uc + Rwc[4] * vc + Rwc[5],
-                        Rwc[6] * uc + Rwc[7] * vc + Rwc[8]};
-  if (!(dw[2] < -1e-9)) return false;
-  const double tt = -Cw[2] / dw[2];
-  if (!(tt > 0)) return false;
-  const double X = Cw[0] + tt * dw[0], Y = Cw[1] + tt * dw[1];
-  const double c0 = -half + 0.5 * spacing;  // first cell centre
-  const double kx = rint((X - c0) / spacing), ky = rint((Y - c0) / spacing);
-  const double lim = rint(2 * half / spacing) - 1;
-  if (kx < 0 || ky < 0 || kx > lim || ky > lim) return false;
-  const double gx = c0 + spacing * kx, gy = c0 + spacing * ky;
-  if (fabs(X - gx) > 0.1 || fabs(Y - gy) > 0.1) return false;
-  o[1] = uc;
-  o[2] = vc;
-  o[3] = gx;
-  o[4] = gy;
-  o[5] = 0.0;
-  return true;
-}
+// cfg.gn_enable: after the per-camera pipeline and the rig fusion, the base
+// pose of every rig is refined over all its cameras' quads, one quad-centre
+// to cell-centre correspondence per quad (gn_quad_obs, mk_gn.h). The list is
+// compacted in item order (block scan), so the MFMA sums are reproducible.
 
 // The rig GN runs as: k_rig_gn_obs (correspondences, once, with the fused
 // pose) then, per iteration, k_rig_gn_acc (one block per rig builds M^T M with
@@ -235,7 +100,7 @@ __global__ __launch_bounds__(256) void k_rig_gn_obs(const FrameDesc* __restrict_
         Cw[a] = T[4 * a] * tbc[0] + T[4 * a + 1] * tbc[1] + T[4 * a + 2] * tbc[2] + T[4 * a + 3];
       }
       double o[6];
-      if (!gn_quad_obs(frames[f], quads[(size_t)f * kMaxQuads + q], Rwc, Cw, half, spacing, o)) continue;
+      if (!gn_quad_obs(frames[f].cam, quads[(size_t)f * kMaxQuads + q].c, Rwc, Cw, half, spacing, o)) continue;
       if (pass == 1 && pos < obs_cap) {
         o[0] = (double)c;
         for (int e = 0; e < 6; e++) obs[(size_t)pos * 6 + e] = o[e];

@@ -14,6 +14,7 @@ static int g_jacobi_ff = 1;
 #define MK_JACOBI_FF g_jacobi_ff
 #include "mk_bits.h"
 #include "mk_contour.h"
+#include "mk_gn.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
 #include "mk_sort.h"
@@ -186,6 +187,28 @@ void hc_distort(const double* xyz, int n, const double* K, const double* D, doub
 void hc_undistort(const double* px, int n, const double* K, const double* D, double* out) {
   mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
   for (int i = 0; i < n; i++) mk::undistort(cm, px[2 * i], px[2 * i + 1], out + 2 * i, out + 2 * i + 1);
+}
+
+// rig GN accumulators of n_obs observations [cam, u, v, X, Y, Z] about T_w_b
+// (camera c has extrinsic T_base_cam[16 c]): the same residual rows as the
+// device's MFMA accumulation (mk_gn.h gn_entry), summed in row order
+void hc_gn_accumulate(const double* Twb, const double* Tbc, int n_cams, const double* obs, int n_obs, double* acc28) {
+  std::vector<mk::GnCam> cams(n_cams);
+  for (int i = 0; i < n_cams; i++) {
+    const double* a = Tbc + 16 * i;
+    for (int r = 0; r < 3; r++) {
+      for (int k = 0; k < 3; k++) cams[i].R_cb[3 * r + k] = a[4 * k + r];
+      cams[i].t_cb[r] = -(a[r] * a[3] + a[4 + r] * a[7] + a[8 + r] * a[11]);
+    }
+  }
+  mk::gn_accumulate_seq(Twb, cams.data(), obs, n_obs, acc28);
+}
+
+// per-quad GN after RPP (mk_gn.h quad_gn_refine) on n problems
+void hc_quad_gn(int n, double* R, double* t, const double* img, const double* obj, int iters, int32_t* steps,
+                double* cost0, double* cost) {
+  for (int i = 0; i < n; i++)
+    steps[i] = mk::quad_gn_refine(R + 9 * i, t + 3 * i, img + 8 * i, obj + 12 * i, iters, cost0 + i, cost + i);
 }
 
 }  // extern "C"

@@ -22,6 +22,7 @@
 
 #include "mk_bits.h"
 #include "mk_contour.h"
+#include "mk_gn.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
 #include "mk_sort.h"
@@ -1835,11 +1836,26 @@ __global__ __launch_bounds__(64) void k_rpp_s1b(RppItem* __restrict__ items, con
   }
 }
 
+// RPP's answer per item; with quad_gn_its > 0 (pipeline items, quads given)
+// the pose is then refined by the per-quad GN on the quad's 4 undistorted
+// test points against the model square (mk_gn.h quad_gn_refine); RPP's
+// img_err stays the generateCentralHypotheses gate (HypothesisGeneration.h:80-85)
 __global__ __launch_bounds__(256) void k_rpp_merge(const RppItem* __restrict__ items, size_t n_items,
-                                                   const rpp::Refine* __restrict__ rf, RppOut* __restrict__ out) {
+                                                   const rpp::Refine* __restrict__ rf, RppOut* __restrict__ out,
+                                                   const QuadRec* __restrict__ quads, int quad_gn_its) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items || !items[i].active) return;
   rpp::Result r = rpp::merge(items[i].s, rf + i * rpp::kCand);
+  if (quads && quad_gn_its > 0 && r.error != 1) {
+    const QuadRec& Q = quads[i >> 1];  // item = (frame * kMaxQuads + quad) * 2 + orientation
+    double obj[12], c0, c1;
+    for (int k = 0; k < 4; k++) {
+      obj[3 * k] = items[i].P[k];
+      obj[3 * k + 1] = items[i].P[4 + k];
+      obj[3 * k + 2] = items[i].P[8 + k];
+    }
+    quad_gn_refine(r.R, r.t, Q.tp, obj, quad_gn_its, &c0, &c1);
+  }
   RppOut& R = out[i];
   for (int k = 0; k < 9; k++) R.R[k] = r.R[k];
   for (int k = 0; k < 3; k++) R.t[k] = r.t[k];
@@ -1848,6 +1864,24 @@ __global__ __launch_bounds__(256) void k_rpp_merge(const RppItem* __restrict__ i
   R.status = r.status;
   R.error = r.error;
   R.iterations = r.iterations;
+}
+
+// stage entry mantis_quad_gn: one lane per problem
+__global__ __launch_bounds__(256) void k_quad_gn(const double* __restrict__ img, const double* __restrict__ obj, int n,
+                                                 double* __restrict__ R, double* __restrict__ t, int its,
+                                                 int32_t* __restrict__ steps, double* __restrict__ costs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double Ri[9], ti[3], ip[8], op[12], c0, c1;
+  for (int k = 0; k < 9; k++) Ri[k] = R[9 * i + k];
+  for (int k = 0; k < 3; k++) ti[k] = t[3 * i + k];
+  for (int k = 0; k < 8; k++) ip[k] = img[8 * i + k];
+  for (int k = 0; k < 12; k++) op[k] = obj[12 * i + k];
+  steps[i] = quad_gn_refine(Ri, ti, ip, op, its, &c0, &c1);
+  for (int k = 0; k < 9; k++) R[9 * i + k] = Ri[k];
+  for (int k = 0; k < 3; k++) t[3 * i + k] = ti[k];
+  costs[2 * i] = c0;
+  costs[2 * i + 1] = c1;
 }
 
 // ===================================== hypotheses generation + clustering

@@ -151,3 +151,65 @@ def rig_gn_reference(T0, T_b_c, cam_quads, undistorters, iterations, lam=1e-9, h
         if float(x @ x) < 1e-24:
             break
     return obs, T, it_done, cost0, cost
+
+
+def quad_gn_reference(R, t, img, obj, iterations, lam=1e-9):
+    """FP64 restatement of the per-quad GN after RPP (mk_gn.h quad_gn_refine):
+    the pose R, t (model -> camera) of one quad refined on its 4 normalized
+    image points img (4 x 2) against the model points obj (4 x 3), as the
+    camera pose T = inv([R | t]) with identity extrinsics; a step is kept only
+    if the cost decreases; stops when the step norm^2 < 1e-24 or the normal
+    matrix is singular. Returns (R, t, steps, cost0, cost)."""
+    obs = np.hstack([np.zeros((4, 1)), np.asarray(img, np.float64).reshape(4, 2),
+                     np.asarray(obj, np.float64).reshape(4, 3)])
+    ext = [np.eye(4)]
+    Tcw = np.eye(4)
+    Tcw[:3, :3] = np.asarray(R, np.float64).reshape(3, 3)
+    Tcw[:3, 3] = np.asarray(t, np.float64).reshape(3)
+    T = rigid_inv(Tcw)
+    acc = gn_accumulate(T, ext, obs)
+    cost0 = acc[27]
+    steps = 0
+    for _ in range(iterations):
+        A = np.zeros((6, 6))
+        A[np.triu_indices(6)] = acc[:21]
+        A = A + np.triu(A, 1).T + lam * np.eye(6)
+        try:
+            np.linalg.cholesky(A)
+        except np.linalg.LinAlgError:
+            break
+        Tn, x = gn_solve(acc, lam, T)
+        acc_n = gn_accumulate(Tn, ext, obs)
+        if not acc_n[27] <= acc[27]:
+            break
+        T, acc = Tn, acc_n
+        steps += 1
+        if float(x @ x) < 1e-24:
+            break
+    Tc = rigid_inv(T)
+    return Tc[:3, :3], Tc[:3, 3], steps, cost0, acc[27]
+
+
+def quad_problems(rng, n, noise=2e-3, pose_noise=0.02, half=0.16):
+    """n synthetic per-quad problems: the model square +-half seen by a random
+    camera 0.8..2.5 m away, noisy normalized corners, and a perturbed start
+    pose. Returns (img n x 4 x 2, obj n x 4 x 3, R0 n x 3 x 3, t0 n x 3,
+    R_true, t_true)."""
+    obj = np.array([[half, half, 0], [-half, half, 0], [-half, -half, 0], [half, -half, 0]], np.float64)
+    imgs, R0s, t0s, Rts, tts = [], [], [], [], []
+    for _ in range(n):
+        a = rng.normal(size=3) * 0.4
+        Rt = exp_se3_right(np.eye(4), np.concatenate([[0, 0, 0], a]))[:3, :3]
+        Rt = Rt @ np.diag([1.0, -1.0, -1.0])  # camera looks down at the plane
+        tt = np.array([rng.uniform(-0.3, 0.3), rng.uniform(-0.3, 0.3), rng.uniform(0.8, 2.5)])
+        pc = (Rt @ obj.T).T + tt
+        imgs.append(pc[:, :2] / pc[:, 2:3] + rng.normal(size=(4, 2)) * noise)
+        Tp = exp_se3_right(rigid_inv(np.vstack([np.hstack([Rt, tt[:, None]]), [0, 0, 0, 1]])),
+                           rng.normal(size=6) * pose_noise)
+        Tc = rigid_inv(Tp)
+        R0s.append(Tc[:3, :3])
+        t0s.append(Tc[:3, 3])
+        Rts.append(Rt)
+        tts.append(tt)
+    return (np.array(imgs), np.repeat(obj[None], n, 0), np.array(R0s), np.array(t0s), np.array(Rts),
+            np.array(tts))

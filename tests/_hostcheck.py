@@ -30,6 +30,9 @@ def lib():
         L.hc_distort.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.hc_undistort.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.hc_masks_bits.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.hc_gn_accumulate.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+        L.hc_quad_gn.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                 C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -125,3 +128,28 @@ def masks_bits(canny_img):
     mask = np.zeros((h, w), np.uint8)
     lib().hc_masks_bits(e.ctypes.data, w, h, det.ctypes.data, mask.ctypes.data)
     return det, mask
+
+
+def gn_accumulate(T_w_b, T_b_c, obs):
+    """mk_gn.h residual rows (the device's) summed in row order: 28 doubles."""
+    T = np.ascontiguousarray(T_w_b, np.float64)
+    E = np.ascontiguousarray(np.asarray(T_b_c, np.float64).reshape(-1, 16))
+    o = np.ascontiguousarray(np.asarray(obs, np.float64).reshape(-1, 6))
+    acc = np.zeros(28)
+    lib().hc_gn_accumulate(T.ctypes.data, E.ctypes.data, len(E), o.ctypes.data, len(o), acc.ctypes.data)
+    return acc
+
+
+def quad_gn(R, t, img, obj, iters):
+    """mk_gn.h quad_gn_refine on n problems: (R, t, steps, cost0, cost)."""
+    R = np.ascontiguousarray(R, np.float64).reshape(-1, 9).copy()
+    t = np.ascontiguousarray(t, np.float64).reshape(-1, 3).copy()
+    img = np.ascontiguousarray(img, np.float64).reshape(-1, 8)
+    obj = np.ascontiguousarray(obj, np.float64).reshape(-1, 12)
+    n = len(R)
+    steps = np.zeros(n, np.int32)
+    c0 = np.zeros(n)
+    c1 = np.zeros(n)
+    lib().hc_quad_gn(n, R.ctypes.data, t.ctypes.data, img.ctypes.data, obj.ctypes.data, iters, steps.ctypes.data,
+                     c0.ctypes.data, c1.ctypes.data)
+    return R.reshape(n, 3, 3), t, steps, c0, c1

@@ -1,9 +1,17 @@
 """N>1 paths on CPU with torch.distributed over gloo (world size 2).
 
-* Rig GN sharded by camera: each rank accumulates its cameras' 28 doubles,
-  the all-reduce sums them, every rank solves the same 6x6 system — the final
-  pose is identical on both ranks and equal to the single-process result.
+* Rig GN sharded by camera: each rank accumulates its cameras' 28 doubles
+  with the library's own residual rows (mk_gn.h, host build through
+  tests/_hostcheck.py), the all-reduce sums them, every rank solves the same
+  6x6 system with the library's mantis_gn_solve — the final pose is identical
+  on both ranks, equal to the single-process result, and the accumulators
+  agree with the numpy restatement (tests/_gn_ref.py).
 * bench.py's weak-scaling reduction: the MAX of the per-rank times is used.
+* Config 5's argmin exchange: the library's mantis_argmin_pick over the
+  all-gathered (err, index) pairs.
+* bench.py --gpus 2 without torchrun spawns two ranks of itself, which get as
+  far as creating the library context (no GPU here) and fail with a clear
+  message.
 """
 import os
 import socket
@@ -14,6 +22,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import _gn_ref as G
+import _hostcheck as HC
 
 
 def _free_port():
@@ -50,7 +59,7 @@ def _worker(rank, world, port, out):
     local = obs[np.isin(obs[:, 0].astype(int), mine)]
 
     def accumulate(T):
-        return G.gn_accumulate(T, ext, local) if len(local) else np.zeros(28)
+        return HC.gn_accumulate(T, ext, local) if len(local) else np.zeros(28)
 
     def allreduce(acc):
         t = torch.from_numpy(acc)
@@ -72,7 +81,9 @@ def test_camera_sharded_gn_world2():
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     T_true, T0, ext, obs = _scene()
-    T1, costs1 = rig.gn_refine(T0, lambda T: G.gn_accumulate(T, ext, obs), None, iterations=6)
+    T1, costs1 = rig.gn_refine(T0, lambda T: HC.gn_accumulate(T, ext, obs), None, iterations=6)
+    np.testing.assert_allclose(HC.gn_accumulate(T0, ext, obs), G.gn_accumulate(T0, ext, obs), rtol=1e-12,
+                               atol=1e-15)
     Ta, ca, ma, sa = out[0]
     Tb, cb, mb, sb = out[1]
     assert sa == [0, 2] and sb == [1, 3]
@@ -137,3 +148,21 @@ def test_argmin_pick_rules():
     assert spans[0] == (0, 2025) and spans[-1] == (14175, 16200)
     assert all(spans[i][1] == spans[i + 1][0] for i in range(7))
     assert dense.shard_range(5, 3, 4) == (4, 5) and dense.shard_range(2, 3, 4) == (2, 2)
+
+
+def test_bench_launcher_spawns_ranks():
+    """`bench.py --gpus 2` (no torchrun): the launcher never touches the GPU,
+    starts 2 ranks that rendezvous over gloo and stop at context creation."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-cpu"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1
+    for k in range(2):
+        assert f"bench rank {k}/2: cannot create a library context on device {k}" in r.stderr, r.stderr
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       env=dict(env, WORLD_SIZE="1"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

@@ -281,3 +281,58 @@ def test_ros_wire_callbacks_match_process(landmark_map):
     finally:
         a.close()
         b.close()
+
+
+def test_quad_gn_stage_and_pipeline(m720, landmark_map):
+    """Per-quad GN after RPP (SURVEY a-21: 4 corners <-> model square, N = 4
+    per quad): the device stage entry (mantis_quad_gn, k_quad_gn) against the
+    FP64 restatement (tests/_gn_ref.quad_gn_reference) and the host build of
+    the same code, on synthetic problems and chained after mantis_rpp_batch;
+    in the pipeline (cfg.quad_gn_iterations) the RPP poses of the hypotheses
+    are refined and the frame still goes through to a published pose.
+    Tolerance 1e-8: see test_host_logic.test_quad_gn_host_build_matches_restatement."""
+    import _hostcheck as HC
+    import mantis_amd as M
+
+    rng = np.random.default_rng(21)
+    img, obj, R0, t0, Rt, tt = G.quad_problems(rng, 256)
+    R, t, steps, costs = m720.quad_gn(img, obj, R0, t0, 8)
+    Rh, th, sh, c0h, c1h = HC.quad_gn(R0, t0, img, obj, 8)
+    np.testing.assert_allclose(R, Rh, atol=1e-8, rtol=0)
+    np.testing.assert_allclose(t, th, atol=1e-8, rtol=0)
+    np.testing.assert_allclose(costs[:, 0], c0h, rtol=1e-12)
+    assert np.all(costs[:, 1] <= costs[:, 0])
+    for i in range(0, 256, 8):
+        Rr, tr, _, c0r, _ = G.quad_gn_reference(R0[i], t0[i], img[i], obj[i], 8)
+        np.testing.assert_allclose(R[i], Rr, atol=1e-8, rtol=0)
+        np.testing.assert_allclose(t[i], tr, atol=1e-8, rtol=0)
+    # RPP -> GN chain on the same corners
+    Rp, tp, e, st = m720.rpp(img, obj)
+    ok = st >= 0
+    R2, t2, s2, c2 = m720.quad_gn(img[ok], obj[ok], Rp[ok], tp[ok], 8)
+    assert np.all(c2[:, 1] <= c2[:, 0] * (1 + 1e-12))
+    for i in np.flatnonzero(ok)[:16]:
+        j = int(np.sum(ok[:i]))
+        Rr, tr, _, _, _ = G.quad_gn_reference(Rp[i], tp[i], img[i], obj[i], 8)
+        np.testing.assert_allclose(t2[j], tr, atol=1e-8, rtol=0)
+    # in the pipeline
+    K, D = synth.intrinsics()
+    R_wc, pos = synth.random_pose(np.random.default_rng(5))
+    fr = synth.render_host(synth.make_cam(R_wc, pos), synth.frame_seed(2, 77))
+    im = M.make_image(fr, K, D)
+    out = {}
+    for its in (0, 6):
+        m = M.Mantis(M.default_config(max_cams=1, quad_gn_iterations=its))
+        m.set_map(*landmark_map)
+        m.rng_state = 1
+        rig, cams = m.process([im])
+        d = m.frame_debug(0)
+        out[its] = (cams[0], d.n_hyps, np.array(d.hyp_c2w)[: d.n_hyps].copy())
+        m.close()
+    (c0_, n0, h0), (c6, n6, h6) = out[0], out[6]
+    assert n0 > 0 and n6 > 0
+    assert c6.status == 0 and c6.reason in (0, 3)
+    # refined hypotheses stay next to the RPP ones (same quads, same clusters)
+    if n0 == n6:
+        assert np.max(np.abs(h6[:, 9:] - h0[:, 9:])) < 0.05
+        assert np.any(h6 != h0)
