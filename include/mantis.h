@@ -64,7 +64,8 @@ typedef struct mantis_config {
   int32_t max_quads;            /* per-frame quad capacity: 256 (0 = default); other values are rejected */
   int32_t max_contour_points;   /* per-frame contour point pool (default 262144) */
   int32_t quad_gn_iterations;   /* per-quad GN after RPP (4 corners <-> model square), 0 = off (parity) */
-  int32_t pad0;
+  int32_t rig_weighting;        /* rig fusion: 0 = lowest-error published camera (default);
+                                   1 = legacy MonteCarlo weighting (see mantis_get_rig_weights) */
 } mantis_config;
 
 typedef struct mantis_image {   /* sensor_msgs/Image (bgr8) + sensor_msgs/CameraInfo */
@@ -174,6 +175,27 @@ typedef struct mantis_rig_gn_info {
   int32_t valid, iterations, n_obs, n_obs_local;
 } mantis_rig_gn_info;
 mantis_status mantis_get_rig_gn(void* ctx, int32_t rig, mantis_rig_gn_info* info, double* obs, int32_t cap);
+
+/* Rig weighting (cfg.rig_weighting = 1): the legacy particle
+ * weight MonteCarlo::computeWeight / computeCameraError
+ * (include/legacy/mantis/MonteCarlo.cpp:183-241) made to work with every
+ * camera of the rig (the reference's "TODO make work with both cameras",
+ * :250-271). Candidate k = the base pose implied by published camera k
+ * (T_w_b = T_w_c inv(T_base_cam)); camera c scores it with
+ * computeCameraError: every landmark projected into c (no z test, the float
+ * pixel strictly inside (0, cols) x (0, rows), cvRound), the squared BGR
+ * distance to its set's colour (white / red / green targets, mantis3's
+ * palette Mantis3Params.h:40-42), error = sum / n, or 1e17 / n when n < 10.
+ * The legacy undistortImage + pinhole projection is replaced by mantis3's
+ * fisheye projection of the original frame (distortPixel, Mantis3Types.h:
+ * 125-136). Weight = mean over the rig's cameras; the lowest weight wins
+ * (first on ties) and is the rig's srv weight. Camera-sharded rigs sum the
+ * per-camera (error sum, count) slots with one ncclAllReduce (exact integers).
+ * Record of rig `rig` of the last batch: weights[C] (DBL_MAX = not a
+ * candidate), c2w[C x C x 12] (world->camera of candidate k in camera c,
+ * nullable) and sums[C x C x 2] (sum, count; nullable); C = cams_per_rig. */
+mantis_status mantis_get_rig_weights(void* ctx, int32_t rig, double* weights, double* c2w, double* sums,
+                                     int32_t* chosen);
 
 /* ------------------------------------------- stage entry points (parity) */
 /* gray -> GaussianBlur 3x3 -> Canny(50,150) (QuadDetection.h:209-212); out W*H bytes 0/255 */

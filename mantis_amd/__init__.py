@@ -26,7 +26,7 @@ class MantisConfig(C.Structure):
                 ("search_radius_multiplier", C.c_double), ("grid_spacing", C.c_double),
                 ("particles", C.c_int32), ("iterations", C.c_int32), ("gn_enable", C.c_int32),
                 ("gn_iterations", C.c_int32), ("max_quads", C.c_int32), ("max_contour_points", C.c_int32),
-                ("quad_gn_iterations", C.c_int32), ("pad0", C.c_int32)]
+                ("quad_gn_iterations", C.c_int32), ("rig_weighting", C.c_int32)]
 
 
 class MantisImage(C.Structure):
@@ -108,6 +108,8 @@ _SIGS = {
                                    C.c_void_p, C.c_void_p]),
     "mantis_quad_gn": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
                                  C.c_void_p, C.c_void_p]),
+    "mantis_get_rig_weights": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.POINTER(C.c_int32)]),
     "mantis_synth_render": (C.c_int, [C.c_void_p, C.POINTER(SynthCamC), C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "mantis_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -400,6 +402,18 @@ class Mantis:
         self._chk(lib().mantis_rpp_batch(self.h, img_pts.ctypes.data, obj_pts.ctypes.data, n, R.ctypes.data,
                                          t.ctypes.data, e.ctypes.data, s.ctypes.data), "rpp_batch")
         return R.reshape(n, 3, 3), t, e, s
+
+    def rig_weights(self, rig, cams_per_rig):
+        """Legacy rig weighting record of rig `rig` (mantis_get_rig_weights):
+        (weights[C], c2w[C, C, 12], sums[C, C, 2], chosen candidate or -1)."""
+        Cn = cams_per_rig
+        w = np.zeros(Cn)
+        c2w = np.zeros((Cn, Cn, 12))
+        sums = np.zeros((Cn, Cn, 2))
+        ch = C.c_int32()
+        self._chk(lib().mantis_get_rig_weights(self.h, rig, w.ctypes.data, c2w.ctypes.data, sums.ctypes.data,
+                                               C.byref(ch)), "get_rig_weights")
+        return w, c2w, sums, ch.value
 
     def quad_gn(self, img_pts, obj_pts, R, t, iterations):
         """Per-quad GN after RPP (mantis_quad_gn): (R, t, steps, costs)."""

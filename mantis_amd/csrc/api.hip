@@ -196,6 +196,14 @@ struct Ctx {
   uint8_t *d_sh_rec = nullptr, *h_sh_rec = nullptr;
   size_t sh_rec_bytes = 0;
   int gauss_cap = 0;  // frames of gaussians h_gauss / d_gauss / h_states hold
+  // legacy rig weighting (cfg.rig_weighting): jobs, (sum, count) per job, the
+  // last batch's record per rig (mantis_get_rig_weights)
+  RigWJob* d_rwjobs = nullptr;
+  double* d_rwout = nullptr;
+  size_t rw_cap = 0;
+  int rw_rigs = 0, rw_C = 0;
+  std::vector<double> rw_weights, rw_c2w, rw_sums;
+  std::vector<int32_t> rw_chosen;
 };
 
 void mark(Ctx* c, const char* name) {
@@ -669,6 +677,7 @@ void mantis_default_config(mantis_config* cfg) {
   cfg->max_quads = kMaxQuads;
   cfg->max_contour_points = 262144;
   cfg->quad_gn_iterations = 0;
+  cfg->rig_weighting = 0;
 }
 
 mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
@@ -688,7 +697,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   // far inside int32 for the offset scan (k_gauss_offsets)
   if (cfg.particles < 1 || cfg.particles > 96 || cfg.iterations < 0 || cfg.iterations > 1000 || cfg.max_cams < 1 ||
       cfg.max_width < 3 || cfg.max_height < 3 || cfg.gn_iterations < 0 || cfg.gn_iterations > 10 ||
-      cfg.quad_gn_iterations < 0 || cfg.quad_gn_iterations > 20) {
+      cfg.quad_gn_iterations < 0 || cfg.quad_gn_iterations > 20 || cfg.rig_weighting < 0 || cfg.rig_weighting > 1) {
     g_create_err = "invalid config (particles 1..96, iterations 0..1000, gn_iterations 0..10, "
                    "quad_gn_iterations 0..20, max_cams >= 1, image >= 3x3)";
     return MANTIS_ERR_ARG;
@@ -809,6 +818,8 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->counted) g_live_ctx[c->cfg.device & 63].fetch_sub(1);
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
+  if (c->d_rwjobs) (void)hipFree(c->d_rwjobs);
+  if (c->d_rwout) (void)hipFree(c->d_rwout);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc, c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
@@ -893,6 +904,126 @@ mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, 
                          bool use_comm);  // gn_impl.hip
 }
 
+namespace {
+// cfg.rig_weighting = 1: the legacy particle weight (MonteCarlo::computeWeight /
+// computeCameraError, include/legacy/mantis/MonteCarlo.cpp:183-241) over every
+// camera of the rig, for each published camera's base pose (include/mantis.h,
+// mantis_get_rig_weights). all / Tall: every camera's result and T_base_cam in
+// global order (rig-major); gidx: the global index of each local frame of the
+// last pipeline batch. With use_comm the (sum, count) slots of the local
+// cameras are summed over the ranks (exact integers in doubles).
+mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* all, const double* Tall,
+                          const int32_t* gidx, int n_local, bool use_comm, mantis_result* out) {
+  const size_t nslot = (size_t)n_rigs * C * C;
+  std::vector<double> Twb((size_t)n_rigs * C * 16);
+  std::vector<char> cand((size_t)n_rigs * C, 0);
+  for (int r = 0; r < n_rigs; r++)
+    for (int k = 0; k < C; k++) {
+      const mantis_cam_result& cr = all[(size_t)r * C + k];
+      if (!cr.publish) continue;
+      double Twc[16], Tinv[16];
+      quat_to_mat4(cr.orientation_xyzw, cr.position, Twc);
+      mat4_inv_rigid(Tall + 16 * ((size_t)r * C + k), Tinv);
+      mat4_mul(Twc, Tinv, &Twb[16 * ((size_t)r * C + k)]);
+      cand[(size_t)r * C + k] = 1;
+    }
+  c->rw_c2w.assign(nslot * 12, 0.0);
+  std::vector<RigWJob> jobs;
+  std::vector<size_t> slot_of;
+  for (int i = 0; i < n_local; i++) {
+    const int g = gidx ? gidx[i] : i;
+    const int r = g / C, cam = g % C;
+    for (int k = 0; k < C; k++) {
+      if (!cand[(size_t)r * C + k]) continue;
+      double Twc[16], Tcw[16];
+      mat4_mul(&Twb[16 * ((size_t)r * C + k)], Tall + 16 * (size_t)g, Twc);
+      mat4_inv_rigid(Twc, Tcw);
+      RigWJob J;
+      std::memset(&J, 0, sizeof(J));
+      for (int a = 0; a < 3; a++) {
+        for (int b = 0; b < 3; b++) J.c2w[3 * a + b] = Tcw[4 * a + b];
+        J.c2w[9 + a] = Tcw[4 * a + 3];
+      }
+      J.frame = i;
+      const size_t slot = ((size_t)r * C + k) * C + cam;
+      std::memcpy(&c->rw_c2w[12 * slot], J.c2w, sizeof(J.c2w));
+      jobs.push_back(J);
+      slot_of.push_back(slot);
+    }
+  }
+  const size_t nj = jobs.size();
+  const size_t need = std::max(nj, nslot);
+  if (need > c->rw_cap) {
+    HIP_OK(hipStreamSynchronize(c->s));
+    (void)hipFree(c->d_rwjobs);
+    (void)hipFree(c->d_rwout);
+    c->d_rwjobs = nullptr;
+    c->d_rwout = nullptr;
+    c->rw_cap = 0;
+    if (dalloc(c, &c->d_rwjobs, need) || dalloc(c, &c->d_rwout, 2 * need)) return MANTIS_ERR_OOM;
+    c->rw_cap = need;
+  }
+  std::vector<double> sums(2 * nslot, 0.0);
+  if (nj) {
+    HIP_OK(hipMemcpyAsync(c->d_rwjobs, jobs.data(), sizeof(RigWJob) * nj, hipMemcpyHostToDevice, c->s));
+    const RigWColors col{{255, 255, 255, 50, 85, 255, 50, 255, 85}};  // WHITE / RED / GREEN, Mantis3Params.h:40-42
+    Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+    k_rig_weight<<<(unsigned)((nj + 3) / 4), 256, 0, c->s>>>(c->d_frames, L, c->d_rwjobs, (int)nj, col, c->d_rwout);
+    HIP_OK(hipGetLastError());
+    std::vector<double> o(2 * nj);
+    HIP_OK(hipMemcpyAsync(o.data(), c->d_rwout, sizeof(double) * 2 * nj, hipMemcpyDeviceToHost, c->s));
+    HIP_OK(hipStreamSynchronize(c->s));
+    for (size_t j = 0; j < nj; j++) {
+      sums[2 * slot_of[j]] = o[2 * j];
+      sums[2 * slot_of[j] + 1] = o[2 * j + 1];
+    }
+  }
+  if (use_comm) {
+    HIP_OK(hipMemcpyAsync(c->d_rwout, sums.data(), sizeof(double) * 2 * nslot, hipMemcpyHostToDevice, c->s));
+    ncclResult_t rr = ncclAllReduce(c->d_rwout, c->d_rwout, 2 * nslot, ncclFloat64, ncclSum, (ncclComm_t)c->comm, c->s);
+    if (rr != ncclSuccess) { c->err = std::string("ncclAllReduce (rig weights): ") + ncclGetErrorString(rr); return MANTIS_ERR_COMM; }
+    HIP_OK(hipMemcpyAsync(sums.data(), c->d_rwout, sizeof(double) * 2 * nslot, hipMemcpyDeviceToHost, c->s));
+    HIP_OK(hipStreamSynchronize(c->s));
+  }
+  c->rw_rigs = n_rigs;
+  c->rw_C = C;
+  c->rw_sums = sums;
+  c->rw_weights.assign((size_t)n_rigs * C, DBL_MAX);
+  c->rw_chosen.assign(n_rigs, -1);
+  for (int r = 0; r < n_rigs; r++) {
+    int best = -1;
+    for (int k = 0; k < C; k++) {
+      if (!cand[(size_t)r * C + k]) continue;
+      double w = 0.0;
+      for (int cam = 0; cam < C; cam++) {
+        const size_t slot = ((size_t)r * C + k) * C + cam;
+        const double e = sums[2 * slot], n = sums[2 * slot + 1];
+        w += (n < 10 ? 1e17 : e) / n;  // computeCameraError :220-225 (n = 0 gives inf)
+      }
+      w /= (double)C;
+      c->rw_weights[(size_t)r * C + k] = w;
+      if (best < 0 || w < c->rw_weights[(size_t)r * C + best]) best = k;
+    }
+    c->rw_chosen[r] = best;
+    if (best < 0 || !out) continue;  // nothing published: keep the reference fusion's answer
+    const mantis_cam_result& cr = all[(size_t)r * C + best];
+    const double* T = &Twb[16 * ((size_t)r * C + best)];
+    double R[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) R[i * 3 + j] = T[i * 4 + j];
+    mk::Quat q = basis_to_quat(R);
+    out[r].orientation_xyzw[0] = q.x; out[r].orientation_xyzw[1] = q.y;
+    out[r].orientation_xyzw[2] = q.z; out[r].orientation_xyzw[3] = q.w;
+    for (int i = 0; i < 3; i++) out[r].position[i] = T[i * 4 + 3];
+    for (int i = 0; i < 36; i++) out[r].covariance[i] = cr.covariance[i];
+    out[r].weight = c->rw_weights[(size_t)r * C + best];
+    out[r].min_yaw_diff = cr.min_yaw_diff;
+    out[r].publish = 1;
+  }
+  return MANTIS_OK;
+}
+}  // namespace
+
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
                                    mantis_result* out, mantis_cam_result* cam_out) {
   Ctx* c = (Ctx*)ctx;
@@ -910,6 +1041,10 @@ mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t 
       for (int i = 0; i < cams_per_rig; i++) k += c->h_st[r * cams_per_rig + i].reaches_pf;
       out[r].rng_state_after = c->h_states[k];
     }
+  }
+  if (out && c->cfg.rig_weighting) {
+    st = weight_rigs(c, n_rigs, cams_per_rig, c->h_res, Tbc.data(), nullptr, n, false, out);
+    if (st != MANTIS_OK) return st;
   }
   if (out && c->cfg.gn_enable) {
     st = run_rig_gn(c, Tbc.data(), n_rigs, cams_per_rig, out, false);
@@ -1013,6 +1148,10 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
     for (int i = 0; i < cams_per_rig; i++) k += c->h_sh_flags[rr * cams_per_rig + i] ? 1 : 0;
     out[rr].rng_state_after = c->h_states[k];
   }
+  if (c->cfg.rig_weighting) {
+    st = weight_rigs(c, n_rigs, cams_per_rig, all.data(), Tall.data(), gidx.data(), n, true, out);
+    if (st != MANTIS_OK) return st;
+  }
   if (c->cfg.gn_enable) {
     const std::vector<double> Tbc = gather_tbc(local_cams, n);
     st = run_rig_gn(c, Tbc.data(), n_rigs, n_local, out, true);
@@ -1021,6 +1160,19 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
   if (cam_out) std::memcpy(cam_out, all.data(), sizeof(mantis_cam_result) * ng);
   for (int g = 0; g < ng; g++)
     if (all[g].status != 0) return MANTIS_ERR_CAPACITY;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_get_rig_weights(void* ctx, int32_t rig, double* weights, double* c2w, double* sums,
+                                     int32_t* chosen) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !weights || rig < 0) return MANTIS_ERR_ARG;
+  if (rig >= c->rw_rigs) { c->err = "no rig weighting record for that rig (cfg.rig_weighting, last batch)"; return MANTIS_ERR_STATE; }
+  const int C = c->rw_C;
+  std::memcpy(weights, &c->rw_weights[(size_t)rig * C], sizeof(double) * C);
+  if (c2w) std::memcpy(c2w, &c->rw_c2w[(size_t)rig * C * C * 12], sizeof(double) * C * C * 12);
+  if (sums) std::memcpy(sums, &c->rw_sums[(size_t)rig * C * C * 2], sizeof(double) * C * C * 2);
+  if (chosen) *chosen = c->rw_chosen[rig];
   return MANTIS_OK;
 }
 

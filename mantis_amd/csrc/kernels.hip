@@ -2740,6 +2740,65 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
   }
 }
 
+// ============================================ legacy rig weighting (f-4)
+// MonteCarlo::computeCameraError (include/legacy/mantis/MonteCarlo.cpp:183-226)
+// for one (candidate, camera) job per wave: every landmark projected (no z
+// test, as project2d :169-181), the pixel as a float strictly inside the
+// frame, cvRound, colorError (:283-286) to the landmark set's colour; integer
+// sum and count (exact, so the lane order does not matter). Pixels past the
+// end of the buffer (cvRound == cols / rows) read black, as the oracle's View.
+struct RigWJob {
+  double c2w[12];
+  int32_t frame, pad;
+};
+struct RigWColors {
+  int32_t c[9];  // B, G, R of white, red, green
+};
+__global__ __launch_bounds__(256) void k_rig_weight(const FrameDesc* __restrict__ frames, Landmarks lmk,
+                                                    const RigWJob* __restrict__ jobs, int n, RigWColors col,
+                                                    double* __restrict__ out2) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= n) return;
+  const RigWJob& J = jobs[j];
+  const FrameDesc fd = frames[J.frame];
+  Xf T;
+  for (int k = 0; k < 9; k++) T.R[k] = J.c2w[k];
+  for (int k = 0; k < 3; k++) T.t[k] = J.c2w[9 + k];
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  const long npx = (long)fd.w * fd.h;
+  long long s = 0;
+  int cnt = 0;
+  for (int l = lane; l < nl; l += 64) {
+    double rp[3], u, v;
+    xf_apply(T, lmk.xyz + 3 * l, rp);
+    distort(fd.cam, rp[0], rp[1], rp[2], &u, &v);
+    const float fu = (float)u, fv = (float)v;  // cv::Point2f out (:175-177)
+    if (!(fu > 0 && fu < (float)fd.w && fv > 0 && fv < (float)fd.h)) continue;
+    cnt++;
+    const int x = (int)rintf(fu), y = (int)rintf(fv);
+    const long lin = (long)y * fd.w + x;
+    const int set = l < lmk.nw ? 0 : (l < lmk.nw + lmk.nr ? 1 : 2);
+    int b = 0, g = 0, r = 0;
+    if (lin >= 0 && lin < npx) {
+      const uint32_t pv = load_bgr(fd.bgr, lin, npx);
+      b = (int)(pv & 0xffu);
+      g = (int)((pv >> 8) & 0xffu);
+      r = (int)((pv >> 16) & 0xffu);
+    }
+    const int e0 = b - col.c[3 * set], e1 = g - col.c[3 * set + 1], e2 = r - col.c[3 * set + 2];
+    s += e0 * e0 + e1 * e1 + e2 * e2;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    cnt += __shfl_xor(cnt, o);
+  }
+  if (lane == 0) {
+    out2[2 * j] = (double)s;
+    out2[2 * j + 1] = (double)cnt;
+  }
+}
+
 // ================================================ standalone scoring API
 __global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__ frames, const uint8_t* mask,
                                                    Landmarks lmk, const double* __restrict__ c2w, int n, int fast,

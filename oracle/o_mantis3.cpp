@@ -623,6 +623,39 @@ void orc_score(orc_ctx* c, const uint8_t* bgr, int32_t w, int32_t h, const doubl
     if (nproj) nproj[i] = np;
   }
 }
+// MonteCarlo::computeCameraError (include/legacy/mantis/MonteCarlo.cpp:183-226)
+// for n world->camera poses c2w (n x 12) on one frame: every landmark of the
+// three sets projected (project2d :169-181 has no z test) -- here with
+// mantis3's fisheye projection (distortPixel, Mantis3Types.h:125-136) of the
+// original frame instead of the legacy undistortImage + pinhole K -- the pixel
+// as cv::Point2f strictly inside (0, cols) x (0, rows), Mat::at<Vec3b>(Point2f)
+// = cvRound of the floats, colorError (:283-286) against the set's colour
+// (colors = B, G, R of white, red, green). sums[2i] = error sum, sums[2i+1] = count.
+void orc_camera_error(orc_ctx* c, const uint8_t* bgr, int32_t w, int32_t h, const double* K, const double* D,
+                      const double* c2w, int32_t n, const int32_t* colors, double* sums) {
+  Cam cm = make_cam(K, D);
+  View v{bgr, w, h};
+  const std::vector<Vec3>* sets[3] = {&c->map.white, &c->map.red, &c->map.green};
+  for (int i = 0; i < n; i++) {
+    Transform T = from12(c2w + 12 * i);
+    double error = 0;
+    int cnt = 0;
+    for (int s = 0; s < 3; s++)
+      for (const Vec3& X : *sets[s]) {
+        double u, vv;
+        distort_cam(cm, T(X), u, vv);
+        const float fx = (float)u, fy = (float)vv;
+        if (fx > 0 && fx < w && fy > 0 && fy < h) {
+          int b, g, r;
+          v.px((int)std::nearbyint(fx), (int)std::nearbyint(fy), b, g, r);
+          error += (double)color_err(b, g, r, colors[3 * s], colors[3 * s + 1], colors[3 * s + 2]);
+          cnt++;
+        }
+      }
+    sums[2 * i] = error;
+    sums[2 * i + 1] = cnt;
+  }
+}
 void orc_distort(const double* xyz, int32_t n, const double* K, const double* D, double* px) {
   Cam cm = make_cam(K, D);
   for (int i = 0; i < n; i++) distort_cam(cm, Vec3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]), px[2 * i], px[2 * i + 1]);

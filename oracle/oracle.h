@@ -75,6 +75,8 @@ int32_t orc_parse_coordinates(const char* s, double* xyz, int32_t max_pts);
  * against a BGR image (the cleaned image for fast scoring). */
 void orc_score(orc_ctx* c, const uint8_t* bgr, int32_t w, int32_t h, const double* K, const double* D,
                const double* c2w, int32_t n, int32_t fast, double* err, int32_t* nproj);
+void orc_camera_error(orc_ctx* c, const uint8_t* bgr, int32_t w, int32_t h, const double* K, const double* D,
+                      const double* c2w, int32_t n, const int32_t* colors, double* sums);
 void orc_distort(const double* xyz_cam, int32_t n, const double* K, const double* D, double* px);
 void orc_undistort(const double* px, int32_t n, const double* K, const double* D, double* out);
 

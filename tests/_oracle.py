@@ -65,6 +65,8 @@ def lib():
         L.orc_gaussians.restype = C.c_uint64
         L.orc_gaussians.argtypes = [C.c_uint64, C.c_int32, C.c_void_p]
         L.orc_approx_poly.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_int32, C.c_void_p]
+        L.orc_camera_error.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
         L.orc_score.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                 C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         _lib = L
@@ -256,6 +258,19 @@ class Oracle:
         dbg = OrcFrameDebug()
         lib().orc_process_frame(self.ctx, bgr.ctypes.data, w, h, 3 * w, K.ctypes.data, D.ctypes.data, C.byref(dbg))
         return dbg
+
+    def camera_error(self, bgr, K, D, c2w, colors=(255, 255, 255, 50, 85, 255, 50, 255, 85)):
+        """Legacy MonteCarlo::computeCameraError raw sums: (error sum, count) per pose."""
+        h, w = bgr.shape[:2]
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        K = np.ascontiguousarray(K, np.float64).reshape(9)
+        D = np.ascontiguousarray(D, np.float64).reshape(4)
+        c2w = np.ascontiguousarray(c2w, np.float64).reshape(-1, 12)
+        col = np.ascontiguousarray(colors, np.int32)
+        sums = np.zeros((len(c2w), 2))
+        lib().orc_camera_error(self.ctx, bgr.ctypes.data, w, h, K.ctypes.data, D.ctypes.data, c2w.ctypes.data,
+                               len(c2w), col.ctypes.data, sums.ctypes.data)
+        return sums
 
     def score(self, bgr, K, D, c2w, fast=True):
         h, w = bgr.shape[:2]

@@ -336,3 +336,89 @@ def test_quad_gn_stage_and_pipeline(m720, landmark_map):
     if n0 == n6:
         assert np.max(np.abs(h6[:, 9:] - h0[:, 9:])) < 0.05
         assert np.any(h6 != h0)
+
+
+def _quat_mat_xyzw(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def test_rig_weighting_legacy_montecarlo(landmark_map):
+    """cfg.rig_weighting = 1 (SURVEY f-4): every published camera's base pose
+    is weighted over all 4 cameras of the rig with the legacy
+    MonteCarlo::computeCameraError (MonteCarlo.cpp:183-226): the per-camera
+    (error sum, count) of every (candidate, camera) job equals the oracle's
+    restatement bit for bit, the weights are the per-camera errors' mean, the
+    lowest weight wins and its base pose is the rig answer; a one-rank
+    camera-sharded call (RCCL all-reduce of the slots) gives the same."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    ext = synth.rig_extrinsics(4)
+    rng = np.random.default_rng(33)
+    n_rigs = 4
+    imgs, frames = [], []
+    for r in range(n_rigs):
+        Twb = synth.random_base_pose(rng)
+        for c in range(4):
+            Twc = Twb @ ext[c]
+            fr = synth.render_host(synth.make_cam(Twc[:3, :3], Twc[:3, 3]), synth.frame_seed(8, 10 * r + c))
+            frames.append(fr)
+            imgs.append(M.make_image(fr, K, D, T_base_cam=ext[c]))
+    cfg = dict(max_cams=4 * n_rigs, max_width=1280, max_height=720)
+    m0 = M.Mantis(M.default_config(**cfg))
+    m0.set_map(*landmark_map)
+    base, cams0 = m0.process(imgs, rigs=n_rigs)
+    m0.close()
+    m = M.Mantis(M.default_config(rig_weighting=1, **cfg))
+    m.set_map(*landmark_map)
+    rig, cams = m.process(imgs, rigs=n_rigs)
+    for a, b in zip(cams0, cams):
+        assert bytes(a) == bytes(b)  # the per-camera path is untouched
+    orc = O.Oracle(*landmark_map, seed=1)
+    checked = 0
+    for r in range(n_rigs):
+        w, c2w, sums, chosen = m.rig_weights(r, 4)
+        cr = cams[4 * r: 4 * r + 4]
+        pub = [k for k in range(4) if cr[k].publish]
+        assert [k for k in range(4) if w[k] < np.finfo(np.float64).max] == pub
+        if not pub:
+            assert chosen == -1
+            assert bytes(rig[r]) == bytes(base[r])
+            continue
+        for k in pub:
+            Twc = np.eye(4)
+            Twc[:3, :3] = _quat_mat_xyzw(cr[k].orientation_xyzw)
+            Twc[:3, 3] = cr[k].position
+            Twb = Twc @ np.linalg.inv(ext[k])
+            tot = 0.0
+            for c in range(4):
+                Tcw = np.linalg.inv(Twb @ ext[c])
+                np.testing.assert_allclose(c2w[k, c], np.concatenate([Tcw[:3, :3].reshape(9), Tcw[:3, 3]]),
+                                           atol=1e-12, rtol=0)
+                o = orc.camera_error(frames[4 * r + c], K, D, c2w[k, c])
+                assert np.array_equal(o[0], sums[k, c]), (r, k, c, o, sums[k, c])
+                e, n = sums[k, c]
+                tot += (1e17 if n < 10 else e) / n
+            assert tot / 4 == w[k]
+        assert chosen == min(pub, key=lambda k: (w[k], k))
+        assert rig[r].weight == w[chosen] and rig[r].publish == 1
+        Twc = np.eye(4)
+        Twc[:3, :3] = _quat_mat_xyzw(cr[chosen].orientation_xyzw)
+        Twc[:3, 3] = cr[chosen].position
+        np.testing.assert_allclose(rig[r].position, (Twc @ np.linalg.inv(ext[chosen]))[:3, 3], atol=1e-9)
+        checked += 1
+    assert checked >= 2
+    ms = M.Mantis(M.default_config(rig_weighting=1, **cfg))
+    ms.set_map(*landmark_map)
+    ms.comm_init(0, 1)
+    rs, _ = ms.process_sharded(imgs, n_rigs, [0, 1, 2, 3], 4)
+    for a, b in zip(rig, rs):
+        assert bytes(a) == bytes(b)
+    for r in range(n_rigs):
+        a, b = m.rig_weights(r, 4), ms.rig_weights(r, 4)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+    m.close()
+    ms.close()
