@@ -137,9 +137,19 @@ mantis_status mantis_rng_set(void* ctx, uint64_t state);
 /* ------------------------------------------------------------ hot path */
 /* One rig pose from n_cams synchronized cameras (n_cams = 1 is exactly the
  * reference callback quadDetection, src/mantis3.cpp:68-135). cam_out may be
- * NULL; otherwise it receives n_cams per-camera results. */
+ * NULL; otherwise it receives n_cams per-camera results. motion (nullable) is
+ * the mantisService delta_pos / delta_quat ("applied to each particle before
+ * reevaluating", srv/mantisService.srv:4-8): the context keeps the last
+ * published rig pose as the service's particle; with a motion and that prior,
+ * T_prior * Transform(delta_quat, delta_pos) joins the rig candidates and all
+ * are re-evaluated with the legacy weighting (mantis_get_rig_weights, last
+ * candidate slot). Without a prior, or with |delta_quat|^2 < 0.5 (an unset
+ * message), the call is the reference callback. */
 mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams, const mantis_motion* motion,
                              mantis_result* out, mantis_cam_result* cam_out);
+/* the motion prior (last published rig pose, T_w_b row-major 4x4): set (NULL clears) / get */
+mantis_status mantis_set_prior_pose(void* ctx, const double* T_w_b);
+mantis_status mantis_get_prior_pose(void* ctx, double* T_w_b, int32_t* has_prior);
 /* n_rigs rigs of cams_per_rig cameras in one batched pass (throughput path):
  * cams[r * cams_per_rig + c]; frames are processed (and draw RNG) in that order. */
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
@@ -191,11 +201,32 @@ mantis_status mantis_get_rig_gn(void* ctx, int32_t rig, mantis_rig_gn_info* info
  * 125-136). Weight = mean over the rig's cameras; the lowest weight wins
  * (first on ties) and is the rig's srv weight. Camera-sharded rigs sum the
  * per-camera (error sum, count) slots with one ncclAllReduce (exact integers).
- * Record of rig `rig` of the last batch: weights[C] (DBL_MAX = not a
- * candidate), c2w[C x C x 12] (world->camera of candidate k in camera c,
- * nullable) and sums[C x C x 2] (sum, count; nullable); C = cams_per_rig. */
+ * Record of rig `rig` of the last batch, K = C + 1 candidate slots (C =
+ * cams_per_rig; slot C = the mantisService motion prediction, see
+ * mantis_process): weights[K] (DBL_MAX = not a candidate), c2w[K x C x 12]
+ * (world->camera of candidate k in camera c, this rank's cameras; nullable),
+ * sums[K x C x 2] (sum, count; nullable), chosen = winning slot or -1. */
 mantis_status mantis_get_rig_weights(void* ctx, int32_t rig, double* weights, double* c2w, double* sums,
                                      int32_t* chosen);
+
+/* Markov yaw filter (include/mantis3/Markov.{h,cpp}, MarkovModel,
+ * included but unused upstream): n_filters 360-bin yaw distributions in the
+ * context's HBM (one per camera stream or rig). w2c_R: hypothesis poses' w2c
+ * bases (row-major 3x3, one per filter / hypothesis); yaw bin = getRPY yaw in
+ * degrees wrapped to [0, 360). active (nullable): filter f is updated iff
+ * active[f] != 0. Results are bit-identical to oracle/o_markov.cpp. */
+/* MarkovModel(Hypothesis) (Markov.cpp:15-27): one-hot at the yaw bin, blurred (stddev 3) */
+mantis_status mantis_markov_init(void* ctx, int32_t n_filters, const double* w2c_R);
+/* senseFusion(Hypothesis) (:164-201): multiply by the measurement (stddev 3.5), normalize */
+mantis_status mantis_markov_sense(void* ctx, const double* w2c_R, const int32_t* active);
+/* convolve(dTheta, dt) (:227-258): shift by (int)dTheta*180/pi bins (dTheta truncated to whole
+ * radians first, as the reference), blur with stddev dt * 11.5 / 90 */
+mantis_status mantis_markov_convolve(void* ctx, const double* dtheta, const double* dt, const int32_t* active);
+/* updateHypothesis (:207-222) with filter `filter`: error[i] = error[i] * 1 / p[bin(w2c_R[i])] */
+mantis_status mantis_markov_weight(void* ctx, int32_t filter, const double* w2c_R, int32_t n, double* error);
+/* planes (n_filters x 360, nullable); yaw = getYaw (:265-275: p[argmax] * pi / 180, the reference's
+ * return value; nullable); argmax = first maximum bin (nullable) */
+mantis_status mantis_markov_get(void* ctx, double* planes, double* yaw, int32_t* argmax);
 
 /* ------------------------------------------- stage entry points (parity) */
 /* gray -> GaussianBlur 3x3 -> Canny(50,150) (QuadDetection.h:209-212); out W*H bytes 0/255 */

@@ -110,6 +110,13 @@ _SIGS = {
                                  C.c_void_p, C.c_void_p]),
     "mantis_get_rig_weights": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.POINTER(C.c_int32)]),
+    "mantis_markov_init": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p]),
+    "mantis_markov_sense": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mantis_markov_convolve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mantis_markov_weight": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]),
+    "mantis_markov_get": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mantis_set_prior_pose": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mantis_get_prior_pose": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int32)]),
     "mantis_synth_render": (C.c_int, [C.c_void_p, C.POINTER(SynthCamC), C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "mantis_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -297,6 +304,38 @@ class Mantis:
         self._chk(st, "process_batch")
         return list(out), list(cam_out)
 
+    def process_motion(self, images, delta_pos=None, delta_quat_xyzw=None):
+        """mantis_process (one rig) with an optional mantisService motion."""
+        n = len(images)
+        cams = (MantisImage * n)(*images)
+        out = MantisResult()
+        cam_out = (MantisCamResult * n)()
+        mo = None
+        if delta_pos is not None:
+            mo = MantisMotion()
+            for i in range(3):
+                mo.delta_pos[i] = delta_pos[i]
+            for i in range(4):
+                mo.delta_quat_xyzw[i] = delta_quat_xyzw[i]
+        st = lib().mantis_process(self.h, cams, n, None if mo is None else C.byref(mo), C.byref(out), cam_out)
+        self._chk(st, "process")
+        return out, list(cam_out)
+
+    @property
+    def prior_pose(self):
+        T = np.zeros((4, 4))
+        h = C.c_int32()
+        self._chk(lib().mantis_get_prior_pose(self.h, T.ctypes.data, C.byref(h)), "get_prior_pose")
+        return T if h.value else None
+
+    @prior_pose.setter
+    def prior_pose(self, T):
+        if T is None:
+            self._chk(lib().mantis_set_prior_pose(self.h, None), "set_prior_pose")
+        else:
+            T = np.ascontiguousarray(T, np.float64)
+            self._chk(lib().mantis_set_prior_pose(self.h, T.ctypes.data), "set_prior_pose")
+
     def process_sharded(self, images, rigs, cam_index, cams_per_rig):
         """Camera-sharded rig call (mantis_process_rig_sharded): images are this
         rank's cameras cam_index of each rig, rig-major. Returns (rig results,
@@ -405,15 +444,49 @@ class Mantis:
 
     def rig_weights(self, rig, cams_per_rig):
         """Legacy rig weighting record of rig `rig` (mantis_get_rig_weights):
-        (weights[C], c2w[C, C, 12], sums[C, C, 2], chosen candidate or -1)."""
+        (weights[C+1], c2w[C+1, C, 12], sums[C+1, C, 2], chosen slot or -1);
+        slot C = the mantisService motion prediction."""
         Cn = cams_per_rig
-        w = np.zeros(Cn)
-        c2w = np.zeros((Cn, Cn, 12))
-        sums = np.zeros((Cn, Cn, 2))
+        w = np.zeros(Cn + 1)
+        c2w = np.zeros((Cn + 1, Cn, 12))
+        sums = np.zeros((Cn + 1, Cn, 2))
         ch = C.c_int32()
         self._chk(lib().mantis_get_rig_weights(self.h, rig, w.ctypes.data, c2w.ctypes.data, sums.ctypes.data,
                                                C.byref(ch)), "get_rig_weights")
         return w, c2w, sums, ch.value
+
+    # Markov yaw filter (include/mantis3/Markov.cpp) ----------------------
+    def markov_init(self, w2c_R):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(-1, 9)
+        self._markov_n = len(R)
+        self._chk(lib().mantis_markov_init(self.h, len(R), R.ctypes.data), "markov_init")
+
+    def markov_sense(self, w2c_R, active=None):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(-1, 9)
+        a = None if active is None else np.ascontiguousarray(active, np.int32)
+        self._chk(lib().mantis_markov_sense(self.h, R.ctypes.data, None if a is None else a.ctypes.data),
+                  "markov_sense")
+
+    def markov_convolve(self, dtheta, dt, active=None):
+        th = np.ascontiguousarray(dtheta, np.float64)
+        d = np.ascontiguousarray(dt, np.float64)
+        a = None if active is None else np.ascontiguousarray(active, np.int32)
+        self._chk(lib().mantis_markov_convolve(self.h, th.ctypes.data, d.ctypes.data,
+                                               None if a is None else a.ctypes.data), "markov_convolve")
+
+    def markov_weight(self, f, w2c_R, error):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(-1, 9)
+        e = np.ascontiguousarray(error, np.float64).copy()
+        self._chk(lib().mantis_markov_weight(self.h, f, R.ctypes.data, len(R), e.ctypes.data), "markov_weight")
+        return e
+
+    def markov_get(self):
+        n = self._markov_n
+        planes = np.zeros((n, 360))
+        yaw = np.zeros(n)
+        am = np.zeros(n, np.int32)
+        self._chk(lib().mantis_markov_get(self.h, planes.ctypes.data, yaw.ctypes.data, am.ctypes.data), "markov_get")
+        return planes, yaw, am
 
     def quad_gn(self, img_pts, obj_pts, R, t, iterations):
         """Per-quad GN after RPP (mantis_quad_gn): (R, t, steps, costs)."""

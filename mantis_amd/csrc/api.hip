@@ -204,6 +204,13 @@ struct Ctx {
   int rw_rigs = 0, rw_C = 0;
   std::vector<double> rw_weights, rw_c2w, rw_sums;
   std::vector<int32_t> rw_chosen;
+  // mantisService motion (mantis_process with a mantis_motion): the last published rig pose
+  bool has_prior = false;
+  double prior_Twb[16];
+  // Markov yaw filters (markov_impl.hip): markov_n planes of 360 bins, per-filter operations
+  double* d_markov = nullptr;
+  MarkovOp* d_mops = nullptr;
+  int markov_n = 0;
 };
 
 void mark(Ctx* c, const char* name) {
@@ -819,6 +826,8 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
   if (c->d_rwjobs) (void)hipFree(c->d_rwjobs);
+  if (c->d_markov) (void)hipFree(c->d_markov);
+  if (c->d_mops) (void)hipFree(c->d_mops);
   if (c->d_rwout) (void)hipFree(c->d_rwout);
   void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
@@ -912,31 +921,40 @@ namespace {
 // global order (rig-major); gidx: the global index of each local frame of the
 // last pipeline batch. With use_comm the (sum, count) slots of the local
 // cameras are summed over the ranks (exact integers in doubles).
+// Candidate slots per rig: K = C + 1, the last one the mantisService motion
+// prediction pred_Twb[16 r] (nullable; mantis_process).
 mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* all, const double* Tall,
-                          const int32_t* gidx, int n_local, bool use_comm, mantis_result* out) {
-  const size_t nslot = (size_t)n_rigs * C * C;
-  std::vector<double> Twb((size_t)n_rigs * C * 16);
-  std::vector<char> cand((size_t)n_rigs * C, 0);
-  for (int r = 0; r < n_rigs; r++)
+                          const int32_t* gidx, int n_local, bool use_comm, mantis_result* out,
+                          const double* pred_Twb = nullptr) {
+  const int K = C + 1;
+  const size_t nslot = (size_t)n_rigs * K * C;
+  std::vector<double> Twb((size_t)n_rigs * K * 16);
+  std::vector<char> cand((size_t)n_rigs * K, 0);
+  for (int r = 0; r < n_rigs; r++) {
     for (int k = 0; k < C; k++) {
       const mantis_cam_result& cr = all[(size_t)r * C + k];
       if (!cr.publish) continue;
       double Twc[16], Tinv[16];
       quat_to_mat4(cr.orientation_xyzw, cr.position, Twc);
       mat4_inv_rigid(Tall + 16 * ((size_t)r * C + k), Tinv);
-      mat4_mul(Twc, Tinv, &Twb[16 * ((size_t)r * C + k)]);
-      cand[(size_t)r * C + k] = 1;
+      mat4_mul(Twc, Tinv, &Twb[16 * ((size_t)r * K + k)]);
+      cand[(size_t)r * K + k] = 1;
     }
-  c->rw_c2w.assign(nslot * 12, 0.0);
+    if (pred_Twb) {
+      std::memcpy(&Twb[16 * ((size_t)r * K + C)], pred_Twb + 16 * (size_t)r, sizeof(double) * 16);
+      cand[(size_t)r * K + C] = 1;
+    }
+  }
+  c->rw_c2w.assign(nslot * 12, 0.0);  // this rank's cameras only
   std::vector<RigWJob> jobs;
   std::vector<size_t> slot_of;
   for (int i = 0; i < n_local; i++) {
     const int g = gidx ? gidx[i] : i;
     const int r = g / C, cam = g % C;
-    for (int k = 0; k < C; k++) {
-      if (!cand[(size_t)r * C + k]) continue;
+    for (int k = 0; k < K; k++) {
+      if (!cand[(size_t)r * K + k]) continue;
       double Twc[16], Tcw[16];
-      mat4_mul(&Twb[16 * ((size_t)r * C + k)], Tall + 16 * (size_t)g, Twc);
+      mat4_mul(&Twb[16 * ((size_t)r * K + k)], Tall + 16 * (size_t)g, Twc);
       mat4_inv_rigid(Twc, Tcw);
       RigWJob J;
       std::memset(&J, 0, sizeof(J));
@@ -945,7 +963,7 @@ mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* al
         J.c2w[9 + a] = Tcw[4 * a + 3];
       }
       J.frame = i;
-      const size_t slot = ((size_t)r * C + k) * C + cam;
+      const size_t slot = ((size_t)r * K + k) * C + cam;
       std::memcpy(&c->rw_c2w[12 * slot], J.c2w, sizeof(J.c2w));
       jobs.push_back(J);
       slot_of.push_back(slot);
@@ -988,26 +1006,25 @@ mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* al
   c->rw_rigs = n_rigs;
   c->rw_C = C;
   c->rw_sums = sums;
-  c->rw_weights.assign((size_t)n_rigs * C, DBL_MAX);
+  c->rw_weights.assign((size_t)n_rigs * K, DBL_MAX);
   c->rw_chosen.assign(n_rigs, -1);
   for (int r = 0; r < n_rigs; r++) {
     int best = -1;
-    for (int k = 0; k < C; k++) {
-      if (!cand[(size_t)r * C + k]) continue;
+    for (int k = 0; k < K; k++) {
+      if (!cand[(size_t)r * K + k]) continue;
       double w = 0.0;
       for (int cam = 0; cam < C; cam++) {
-        const size_t slot = ((size_t)r * C + k) * C + cam;
+        const size_t slot = ((size_t)r * K + k) * C + cam;
         const double e = sums[2 * slot], n = sums[2 * slot + 1];
         w += (n < 10 ? 1e17 : e) / n;  // computeCameraError :220-225 (n = 0 gives inf)
       }
       w /= (double)C;
-      c->rw_weights[(size_t)r * C + k] = w;
-      if (best < 0 || w < c->rw_weights[(size_t)r * C + best]) best = k;
+      c->rw_weights[(size_t)r * K + k] = w;
+      if (best < 0 || w < c->rw_weights[(size_t)r * K + best]) best = k;
     }
     c->rw_chosen[r] = best;
-    if (best < 0 || !out) continue;  // nothing published: keep the reference fusion's answer
-    const mantis_cam_result& cr = all[(size_t)r * C + best];
-    const double* T = &Twb[16 * ((size_t)r * C + best)];
+    if (best < 0 || !out) continue;  // nothing published, no prediction: keep the reference fusion's answer
+    const double* T = &Twb[16 * ((size_t)r * K + best)];
     double R[9];
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 3; j++) R[i * 3 + j] = T[i * 4 + j];
@@ -1015,19 +1032,35 @@ mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* al
     out[r].orientation_xyzw[0] = q.x; out[r].orientation_xyzw[1] = q.y;
     out[r].orientation_xyzw[2] = q.z; out[r].orientation_xyzw[3] = q.w;
     for (int i = 0; i < 3; i++) out[r].position[i] = T[i * 4 + 3];
-    for (int i = 0; i < 36; i++) out[r].covariance[i] = cr.covariance[i];
-    out[r].weight = c->rw_weights[(size_t)r * C + best];
-    out[r].min_yaw_diff = cr.min_yaw_diff;
-    out[r].publish = 1;
+    out[r].weight = c->rw_weights[(size_t)r * K + best];
+    if (best < C) {
+      const mantis_cam_result& cr = all[(size_t)r * C + best];
+      for (int i = 0; i < 36; i++) out[r].covariance[i] = cr.covariance[i];
+      out[r].min_yaw_diff = cr.min_yaw_diff;
+      out[r].publish = 1;
+    } else {  // the motion prediction: published only if a camera measured a pose this call
+      out[r].publish = out[r].n_cams_published > 0 ? 1 : 0;
+    }
   }
   return MANTIS_OK;
 }
 }  // namespace
 
+namespace {
+mantis_status process_batch_impl(Ctx* c, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
+                                 mantis_result* out, mantis_cam_result* cam_out, const double* pred_Twb);
+}
+
 mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
                                    mantis_result* out, mantis_cam_result* cam_out) {
   Ctx* c = (Ctx*)ctx;
   if (c) bind_device(c);
+  return process_batch_impl(c, cams, n_rigs, cams_per_rig, out, cam_out, nullptr);
+}
+
+namespace {
+mantis_status process_batch_impl(Ctx* c, const mantis_image* cams, int32_t n_rigs, int32_t cams_per_rig,
+                                 mantis_result* out, mantis_cam_result* cam_out, const double* pred_Twb) {
   if (!c || !cams || n_rigs <= 0 || cams_per_rig <= 0) return MANTIS_ERR_ARG;
   const int n = n_rigs * cams_per_rig;
   mantis_status st = process_frames(c, cams, n);
@@ -1042,8 +1075,8 @@ mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t 
       out[r].rng_state_after = c->h_states[k];
     }
   }
-  if (out && c->cfg.rig_weighting) {
-    st = weight_rigs(c, n_rigs, cams_per_rig, c->h_res, Tbc.data(), nullptr, n, false, out);
+  if (out && (c->cfg.rig_weighting || pred_Twb)) {
+    st = weight_rigs(c, n_rigs, cams_per_rig, c->h_res, Tbc.data(), nullptr, n, false, out, pred_Twb);
     if (st != MANTIS_OK) return st;
   }
   if (out && c->cfg.gn_enable) {
@@ -1055,6 +1088,7 @@ mantis_status mantis_process_batch(void* ctx, const mantis_image* cams, int32_t 
     if (c->h_res[f].status != 0) return MANTIS_ERR_CAPACITY;
   return MANTIS_OK;
 }
+}  // namespace
 
 namespace {
 // one camera's result as exchanged between the ranks of a sharded rig
@@ -1149,7 +1183,7 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
     out[rr].rng_state_after = c->h_states[k];
   }
   if (c->cfg.rig_weighting) {
-    st = weight_rigs(c, n_rigs, cams_per_rig, all.data(), Tall.data(), gidx.data(), n, true, out);
+    st = weight_rigs(c, n_rigs, cams_per_rig, all.data(), Tall.data(), gidx.data(), n, true, out, nullptr);
     if (st != MANTIS_OK) return st;
   }
   if (c->cfg.gn_enable) {
@@ -1168,18 +1202,61 @@ mantis_status mantis_get_rig_weights(void* ctx, int32_t rig, double* weights, do
   Ctx* c = (Ctx*)ctx;
   if (!c || !weights || rig < 0) return MANTIS_ERR_ARG;
   if (rig >= c->rw_rigs) { c->err = "no rig weighting record for that rig (cfg.rig_weighting, last batch)"; return MANTIS_ERR_STATE; }
-  const int C = c->rw_C;
-  std::memcpy(weights, &c->rw_weights[(size_t)rig * C], sizeof(double) * C);
-  if (c2w) std::memcpy(c2w, &c->rw_c2w[(size_t)rig * C * C * 12], sizeof(double) * C * C * 12);
-  if (sums) std::memcpy(sums, &c->rw_sums[(size_t)rig * C * C * 2], sizeof(double) * C * C * 2);
+  const int C = c->rw_C, K = C + 1;
+  std::memcpy(weights, &c->rw_weights[(size_t)rig * K], sizeof(double) * K);
+  if (c2w) std::memcpy(c2w, &c->rw_c2w[(size_t)rig * K * C * 12], sizeof(double) * K * C * 12);
+  if (sums) std::memcpy(sums, &c->rw_sums[(size_t)rig * K * C * 2], sizeof(double) * K * C * 2);
   if (chosen) *chosen = c->rw_chosen[rig];
   return MANTIS_OK;
 }
 
+// mantisService motion (srv/mantisService.srv:4-8: "applied to each particle
+// before reevaluating"; parsed into tf::Transform(delta_quat, delta_pos) by the
+// legacy server, include/legacy/mantis/MonteCarlo.cpp:273-276, and composed on
+// the right of a particle as runFilter does, :58). The mantis3 callback has no
+// particles across frames, so the context keeps the last published
+// rig pose as the one particle the service carries: with a motion and that
+// prior, the prediction T_prior * Delta joins the rig candidates and all are
+// re-evaluated with the legacy weighting (weight_rigs). A motion whose
+// quaternion has |q|^2 < 0.5 (an unset message: all zeros) counts as none.
 mantis_status mantis_process(void* ctx, const mantis_image* cams, int32_t n_cams, const mantis_motion* motion,
                              mantis_result* out, mantis_cam_result* cam_out) {
-  (void)motion;  // delta_pos/delta_quat: the mantis3 callback does not use them
-  return mantis_process_batch(ctx, cams, 1, n_cams, out, cam_out);
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c) return MANTIS_ERR_ARG;
+  double pred[16];
+  const double* pq = motion ? motion->delta_quat_xyzw : nullptr;
+  const bool use_motion = motion && out && c->has_prior &&
+                          pq[0] * pq[0] + pq[1] * pq[1] + pq[2] * pq[2] + pq[3] * pq[3] >= 0.5;
+  if (use_motion) {
+    double D[16];
+    quat_to_mat4(motion->delta_quat_xyzw, motion->delta_pos, D);
+    mat4_mul(c->prior_Twb, D, pred);
+  }
+  mantis_result tmp;
+  mantis_result* o = out ? out : &tmp;
+  const mantis_status st = process_batch_impl(c, cams, 1, n_cams, o, cam_out, use_motion ? pred : nullptr);
+  if (st == MANTIS_OK && o->publish) {
+    quat_to_mat4(o->orientation_xyzw, o->position, c->prior_Twb);
+    c->has_prior = true;
+  }
+  return st;
+}
+
+mantis_status mantis_set_prior_pose(void* ctx, const double* T_w_b) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return MANTIS_ERR_ARG;
+  c->has_prior = T_w_b != nullptr;
+  if (T_w_b) std::memcpy(c->prior_Twb, T_w_b, sizeof(c->prior_Twb));
+  return MANTIS_OK;
+}
+
+mantis_status mantis_get_prior_pose(void* ctx, double* T_w_b, int32_t* has_prior) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !T_w_b || !has_prior) return MANTIS_ERR_ARG;
+  *has_prior = c->has_prior ? 1 : 0;
+  std::memcpy(T_w_b, c->prior_Twb, sizeof(c->prior_Twb));
+  return MANTIS_OK;
 }
 
 mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes) {
@@ -1450,4 +1527,5 @@ mantis_status mantis_set_profiling(void* ctx, int32_t on) {
 
 #include "gn_impl.hip"
 #include "dense_impl.hip"
+#include "markov_impl.hip"
 #include "ros_wire.h"

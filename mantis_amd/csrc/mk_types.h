@@ -124,4 +124,17 @@ struct RigGnIO {
 // r^T r (1), correspondence count (1), padding — summed across camera shards
 constexpr int kGnSlot = 32;
 
+// Markov yaw filter operation (markov_impl.hip, include/mantis3/Markov.cpp)
+constexpr int kYawBins = 360;
+
+struct MarkovOp {
+  int32_t kind;  // -1 skip, 0 MarkovModel(Hypothesis), 1 senseFusion(Hypothesis), 2 convolve
+  int32_t bin;   // yaw bin (kinds 0, 1)
+  int32_t off;   // kind 2: aux[k] = p[(k + off) % 360] (Markov.cpp:230-248)
+  int32_t pad;
+  double den;    // stddev * sqrt(2 pi)
+  double E[181]; // exp(-((d * d) / (2 * stddev * stddev))), d = 0..180
+};
+
+
 }  // namespace mk

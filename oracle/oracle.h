@@ -87,6 +87,13 @@ int32_t orc_rpoly(const double* op, int32_t deg, double* zr, double* zi);
 void orc_svd(const double* A, int32_t m, int32_t n, double* w, double* u, double* vt);
 /* n cv::RNG gaussian(1.0) float draws from `state`; returns the state after */
 uint64_t orc_gaussians(uint64_t state, int32_t n, float* out);
+/* Markov yaw filter (include/mantis3/Markov.cpp, o_markov.cpp): 360-bin planes, R = w2c basis (9) */
+void orc_markov_init(const double* R, double* p);
+void orc_markov_sense(double* p, const double* R);
+void orc_markov_convolve(double* p, double dTheta, double dt);
+void orc_markov_weight(const double* p, const double* R, int32_t n, double* error);
+double orc_markov_yaw(const double* p, int32_t* argmax);
+int32_t orc_markov_bin(const double* R);
 /* std::sort(descending error) permutation as libstdc++ orders it */
 void orc_sort_desc(const double* err, int32_t n, int32_t* perm);
 

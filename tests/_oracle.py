@@ -67,6 +67,14 @@ def lib():
         L.orc_approx_poly.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_int32, C.c_void_p]
         L.orc_camera_error.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.orc_markov_init.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_markov_sense.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_markov_convolve.argtypes = [C.c_void_p, C.c_double, C.c_double]
+        L.orc_markov_weight.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.orc_markov_yaw.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_markov_yaw.restype = C.c_double
+        L.orc_markov_bin.argtypes = [C.c_void_p]
+        L.orc_markov_bin.restype = C.c_int32
         L.orc_score.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                 C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         _lib = L
@@ -223,6 +231,38 @@ def undistort(px, K, D):
     lib().orc_undistort(_p(px, C.c_double), C.c_int32(len(px)), _p(K, C.c_double), _p(D, C.c_double),
                         _p(out, C.c_double))
     return out
+
+
+class Markov:
+    """Oracle restatement of MarkovModel (oracle/o_markov.cpp), one plane."""
+
+    def __init__(self, w2c_R):
+        self.p = np.zeros(360)
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(9)
+        lib().orc_markov_init(R.ctypes.data, self.p.ctypes.data)
+
+    def sense(self, w2c_R):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(9)
+        lib().orc_markov_sense(self.p.ctypes.data, R.ctypes.data)
+
+    def convolve(self, dtheta, dt):
+        lib().orc_markov_convolve(self.p.ctypes.data, C.c_double(dtheta), C.c_double(dt))
+
+    def weight(self, w2c_R, error):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(-1, 9)
+        e = np.ascontiguousarray(error, np.float64).copy()
+        lib().orc_markov_weight(self.p.ctypes.data, R.ctypes.data, len(R), e.ctypes.data)
+        return e
+
+    def yaw(self):
+        am = C.c_int32()
+        y = lib().orc_markov_yaw(self.p.ctypes.data, C.byref(am))
+        return y, am.value
+
+    @staticmethod
+    def bin(w2c_R):
+        R = np.ascontiguousarray(w2c_R, np.float64).reshape(9)
+        return lib().orc_markov_bin(R.ctypes.data)
 
 
 class Oracle:

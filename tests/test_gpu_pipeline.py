@@ -383,7 +383,7 @@ def test_rig_weighting_legacy_montecarlo(landmark_map):
         w, c2w, sums, chosen = m.rig_weights(r, 4)
         cr = cams[4 * r: 4 * r + 4]
         pub = [k for k in range(4) if cr[k].publish]
-        assert [k for k in range(4) if w[k] < np.finfo(np.float64).max] == pub
+        assert [k for k in range(5) if w[k] < np.finfo(np.float64).max] == pub  # slot 4: no motion prediction
         if not pub:
             assert chosen == -1
             assert bytes(rig[r]) == bytes(base[r])
@@ -422,3 +422,76 @@ def test_rig_weighting_legacy_montecarlo(landmark_map):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
     m.close()
     ms.close()
+
+
+def test_service_motion_prediction(landmark_map):
+    """mantisService motion (srv/mantisService.srv:4-8, include/mantis.h
+    mantis_process): the context keeps the last published rig pose; with a
+    delta the prediction T_prior * Delta joins the rig candidates and is
+    re-evaluated with the legacy weighting -- its world->camera poses are the
+    composition, its per-camera sums equal the oracle's computeCameraError, and
+    the winner is the lowest weight. An unset motion (zero quaternion), or no
+    prior, leaves the reference callback's answer unchanged."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    ext = synth.rig_extrinsics(4)
+    rng = np.random.default_rng(44)
+    T0 = synth.random_base_pose(rng)
+    delta = np.eye(4)
+    delta[:3, :3] = synth.rot_z(0.03)
+    delta[:3, 3] = [0.05, -0.02, 0.0]
+    T1 = T0 @ delta
+    rigs = []
+    for r, T in enumerate((T0, T1)):
+        fr = [synth.render_host(synth.make_cam((T @ ext[c])[:3, :3], (T @ ext[c])[:3, 3]), synth.frame_seed(9, 10 * r + c))
+              for c in range(4)]
+        rigs.append((fr, [M.make_image(f, K, D, T_base_cam=ext[c]) for c, f in enumerate(fr)]))
+    m = M.Mantis(max_cams=4)
+    m.set_map(*landmark_map)
+    assert m.prior_pose is None
+    r0, _ = m.process_motion(rigs[0][1], [0.1, 0, 0], [0, 0, 0, 1])  # no prior yet: plain callback
+    if not r0.publish:
+        pytest.skip("first rig not published")
+    P = m.prior_pose
+    np.testing.assert_allclose(P[:3, 3], r0.position, atol=0)
+    # an unset motion is no motion
+    s = m.rng_state
+    a, ca = m.process_motion(rigs[1][1], [0, 0, 0], [0, 0, 0, 0])
+    m.prior_pose = P
+    m.rng_state = s
+    b, cb = m.process_motion(rigs[1][1])
+    assert bytes(a) == bytes(b)
+    # with the delta: the prediction is weighted with the cameras' candidates
+    m.prior_pose = P
+    m.rng_state = s
+    q = [0, 0, np.sin(0.015), np.cos(0.015)]
+    res, cams = m.process_motion(rigs[1][1], delta[:3, 3], q)
+    w, c2w, sums, chosen = m.rig_weights(0, 4)
+    assert w[4] < np.finfo(np.float64).max
+    Dm = np.eye(4)
+    Dm[:3, :3] = _quat_mat_xyzw(q)
+    Dm[:3, 3] = delta[:3, 3]
+    pred = P @ Dm
+    orc = O.Oracle(*landmark_map, seed=1)
+    tot = 0.0
+    for c in range(4):
+        Tcw = np.linalg.inv(pred @ ext[c])
+        np.testing.assert_allclose(c2w[4, c], np.concatenate([Tcw[:3, :3].reshape(9), Tcw[:3, 3]]), atol=1e-12)
+        o = orc.camera_error(rigs[1][0][c], K, D, c2w[4, c])
+        assert np.array_equal(o[0], sums[4, c])
+        e, n = sums[4, c]
+        tot += (1e17 if n < 10 else e) / n
+    assert tot / 4 == w[4]
+    valid = [k for k in range(5) if w[k] < np.finfo(np.float64).max]
+    assert chosen == min(valid, key=lambda k: (w[k], k))
+    assert res.weight == w[chosen]
+    if chosen == 4:
+        np.testing.assert_allclose(res.position, pred[:3, 3], atol=1e-12)
+    # the prediction is near the truth of the second rig
+    assert np.linalg.norm(pred[:3, 3] - T1[:3, 3]) < 0.1
+    m.prior_pose = None
+    m.rng_state = s
+    c_, _ = m.process_motion(rigs[1][1], delta[:3, 3], q)
+    assert bytes(c_) == bytes(b)
+    m.close()
