@@ -126,7 +126,7 @@ struct Ctx {
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
-  uint16_t* d_lroot = nullptr;  // Canny candidates' tile roots (k_canny_uf -> k_hyst_edge), then run starts
+  uint16_t* d_lroot = nullptr;  // hysteresis run extents (k_hyst_*), then contour run starts
   size_t lstride = 0;            // d_lroot entries per frame: max(plane, tiles x FTW x FTH)
   uint8_t *d_bgr = nullptr, *d_strong = nullptr, *d_edge = nullptr,
           *d_det = nullptr, *d_mask = nullptr;
@@ -286,18 +286,22 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   mark(c, "start");
   const size_t B = c->bstride;
   dim3 gf((W + FTW - 1) / FTW, (H + FTH - 1) / FTH, n);
-  k_canny_uf<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
-                                   c->d_b2, c->d_lroot, c->lstride, c->d_lab, c->d_strong, P, B);
+  k_canny<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
+                                c->d_b2, B);
   mark(c, "canny_nms");
-  const size_t nhseam = (size_t)((W - 1) / FTW) * H + (size_t)((H - 1) / FTH) * ((W + 31) / 32);
-  if (nhseam) k_hyst_seam<<<dim3((unsigned)((nhseam + 255) / 256), n), 256, 0, c->s>>>(c->d_b1, c->d_lab, W, H, P, B);
-  const size_t nw = (size_t)((W + 31) / 32) * H;
-  dim3 gw(blocks_for(nw), n);
-  k_hyst_mark<<<gw, 256, 0, c->s>>>(c->d_b2, c->d_lab, c->d_strong, W, H, P, B);
-  const int ntiles = (int)(gf.x * gf.y);
-  k_hyst_edge<<<dim3((ntiles + 3) / 4, n), 256, 0, c->s>>>(c->d_b1, c->d_lroot, c->lstride, c->d_lab, c->d_strong,
-                                                          c->d_eb, edge_bytes ? c->d_edge : nullptr, W, H, P, B,
-                                                          (int)gf.x, ntiles);
+  // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
+  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, P, c->rstride, P / 2};
+  dim3 gr4((H + 3) / 4, n);
+  k_hyst_count<<<gr4, 256, 0, c->s>>>(c->d_b1, B, hr, W, H);
+  k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, H);
+  k_hyst_runs<<<gr4, 256, 0, c->s>>>(c->d_b1, B, hr, W, H);
+  k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 2 * sizeof(uint32_t) * HB_ROWS * bits::words(W), c->s>>>(
+      c->d_b2, B, hr, c->d_eb, W, H);
+  const int nseam = (H - 1) / HB_ROWS;
+  if (nseam > 0) k_hyst_seam<<<dim3((nseam + 3) / 4, n), 256, 0, c->s>>>(hr, H);
+  k_hyst_mark<<<dim3(8, n), 256, 0, c->s>>>(hr, H);
+  k_hyst_fix<<<dim3(8, n), 256, 0, c->s>>>(hr, c->d_eb, B, W, H);
+  if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
   mark(c, "hysteresis");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   dim3 gm((H + MB_BH - 1) / MB_BH, n);
@@ -709,6 +713,10 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
                    "quad_gn_iterations 0..20, max_cams >= 1, image >= 3x3)";
     return MANTIS_ERR_ARG;
   }
+  if (cfg.max_width > 8190) {
+    g_create_err = "max_width: at most 8190 (the hysteresis bands hold a row's worst-case runs in LDS)";
+    return MANTIS_ERR_ARG;
+  }
   if (cfg.max_quads != kMaxQuads) {
     g_create_err = "max_quads: the per-frame quad capacity is fixed at 256 in this build";
     return MANTIS_ERR_ARG;
@@ -757,7 +765,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
   chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
   chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
-  c->lstride = std::max(c->plane, (size_t)((c->Wmax + FTW - 1) / FTW) * ((c->Hmax + FTH - 1) / FTH) * FTW * FTH);
+  c->lstride = (c->plane + 1) & ~(size_t)1;  // even: the hysteresis views it as u32 run extents
   chk(dalloc(c, &c->d_lroot, (size_t)F * c->lstride));
   chk(dalloc(c, &c->d_edge, c->plane));  // debug / single-frame byte planes (frame 0)
   chk(dalloc(c, &c->d_det, c->plane));

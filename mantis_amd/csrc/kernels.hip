@@ -31,6 +31,18 @@
 
 namespace mk {
 
+__device__ inline int wave_sum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ inline int wave_incl_scan(int v, int lane) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
 // ======================================================== union-find (CCL)
 // Concurrent union by index: roots are component minima, links point to
 // smaller indices only, so finds terminate and stale reads only cost retries.
@@ -79,21 +91,22 @@ __device__ inline void lds_union(int* L, int a, int b) {
 // BORDER_REFLECT_101) -> Sobel 3x3 (REPLICATE) -> L1 magnitude -> NMS
 // (QuadDetection.h:209-212, HypothesisEvaluation.h:323-327; one Canny serves
 // both) and cv::Canny's hysteresis stack walk, i.e. the 8-connected components
-// of the NMS candidates that hold a strong pixel. Two-level, with nothing
-// per-pixel written to HBM but bit planes:
-//   k_canny_uf   per 128x16 tile: BGR (vector loads) -> classes in LDS, LDS
-//                union-find of the candidates; writes the candidate bit plane,
-//                a bit plane of the tile roots whose component holds a strong
-//                pixel, and sparse labels (tile roots, tile-border candidates)
-//   k_hyst_seam  unions across tile seams (global, path halving)
-//   k_hyst_mark  strong tile roots mark their global root
-//   k_hyst_edge  per tile: the same LDS union-find again; edge = candidate
-//                whose global root is marked (bit plane, bytes on request)
+// of the NMS candidates that hold a strong pixel. Nothing per-pixel reaches HBM
+// but bit planes:
+//   k_canny      per 128x16 tile: BGR (vector loads) -> classes in LDS ->
+//                candidate and strong bit planes (one ballot per 64 pixels)
+//   k_hyst_count / k_run_scan / k_hyst_runs   candidate runs per row, their
+//                ids (raster order), extents
+//   k_hyst_band  8-connected run unions inside 32-row bands in LDS; the edge
+//                words of every band component with a strong pixel; lists of
+//                the components that reach a band seam
+//   k_hyst_seam  the same unions across band seams (global labels)
+//   k_hyst_mark  strong components at a seam mark their global root
+//   k_hyst_fix   weak components at a seam whose global root is marked: edges
 #ifndef MK_FTH
 #define MK_FTH 16
 #endif
 constexpr int FTW = 128, FTH = MK_FTH;         // front-end tile
-constexpr int FSEG = FTW * FTH / 256;          // pixels per thread-run in the tile union-find
 constexpr int FGW = FTW + 8, FGH = FTH + 6;    // gray tile: x0-4 .. x0+FTW+3 (4-aligned), y0-3 .. y0+FTH+2
 constexpr int FRW = FTW + 4;                   // blurred columns x0-2 .. x0+FTW+1
 constexpr int FMW = FTW + 2, FMH = FTH + 2;    // magnitude: x0-1 .. x0+FTW, y0-1 .. y0+FTH
@@ -118,57 +131,6 @@ __device__ inline uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
     return __builtin_amdgcn_udot4(p, lo, (__builtin_amdgcn_udot4(p, hi, 0u, false) << 8) + 8192u, false) >> 14;
   };
   return g(d0, LO, HI) | (g(p1, LO, HI) << 8) | (g(p2, LO, HI) << 16) | (g(d2, LO << 8, HI << 8) << 24);
-}
-
-// 8-connected union-find of the candidates C (LDS bytes) of one FTW x FTH tile;
-// leaves every candidate's L at its component's minimum index (deterministic).
-// Candidates are sparse (thin NMS curves): one ballot per 64 pixels gives the
-// candidate mask (kept in gm for the bit plane), a compacted candidate list
-// (one LDS atomic per wave and step), and each candidate's initial label, the
-// start of its run of consecutive candidates inside its FSEG-pixel segment (so
-// horizontal runs start linked). Only candidates' labels are ever read.
-__device__ inline int tile_uf(const uint8_t* C, int* L, int16_t* list, int* count, uint64_t* gm, int t) {
-  if (t == 0) *count = 0;
-  __syncthreads();
-  const int lane = t & 63;
-  for (int i = t; i < FTW * FTH; i += 256) {
-    const bool c = C[i] != 0;
-    const uint64_t m = __ballot(c);
-    if (lane == 0) gm[i >> 6] = m;
-    int base = 0;
-    if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
-    base = __shfl(base, 0);
-    if (c) {
-      list[base + __popcll(m & ((1ull << lane) - 1))] = (int16_t)i;
-      const int sb = lane & ~(FSEG - 1);
-      const uint64_t z = ~m & ((1ull << lane) - 1) & ~((1ull << sb) - 1);  // non-candidates of the segment below
-      L[i] = (i - lane) + (z ? 64 - __clzll(z) : sb);
-    }
-  }
-  __syncthreads();
-  const int n = *count;
-  for (int k = t; k < n; k += 256) {
-    const int i = list[k];
-    const int lx = i % FTW, ly = i / FTW;
-    const bool left = lx > 0 && C[i - 1];
-    if ((lx % FSEG) == 0 && left) lds_union(L, i, i - 1);
-    if (ly == 0) continue;
-    const bool up = C[i - FTW] != 0;
-    const bool upl = lx > 0 && C[i - FTW - 1];
-    if (up) {
-      if (!(left && upl)) lds_union(L, i, i - FTW);
-    } else {
-      if (upl && !left) lds_union(L, i, i - FTW - 1);
-      if (lx + 1 < FTW && C[i - FTW + 1]) lds_union(L, i, i - FTW + 1);
-    }
-  }
-  __syncthreads();
-  for (int k = t; k < n; k += 256) {
-    const int i = list[k];
-    L[i] = lds_find(L, i);
-  }
-  __syncthreads();
-  return n;
 }
 
 // Interior tiles, four horizontally adjacent pixels per work-item: every
@@ -267,12 +229,14 @@ __device__ inline void sobel4(const uint8_t* bl, int16_t* mag, int16_t* gx_s, in
   }
 }
 
-// The Canny stages of one tile into K (classes). IN: the tile and its halo
+// The Canny stages of one tile into the candidate / strong masks gm, sm (bit
+// i & 63 of word i >> 6 = tile pixel i, i = ly * FTW + lx). IN: the tile and its halo
 // (x0-4 .. x0+FTW+3, y0-3 .. y0+FTH+2) lie inside the image and the rows
 // allow dword loads, so the border rules (reflect/replicate/zero) drop out.
 template <bool IN>
 __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, int y0, int low, int high, int vec,
-                                     uint8_t* g, uint8_t* bl, int16_t* mag, int16_t* gxy, uint8_t* K, int t) {
+                                     uint8_t* g, uint8_t* bl, int16_t* mag, int16_t* gxy, uint64_t* gm, uint64_t* sm,
+                                     int t) {
   constexpr int BLH = FTH + 4;
   int16_t* gx_s = gxy;
   int16_t* gy_s = gxy + FTW * FTH;
@@ -394,225 +358,351 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
         if (push) c = (m > high) ? 2 : 1;
       }
     }
-    K[i] = c;
+    // a wave covers 64 consecutive tile pixels (uniform trip count)
+    const uint64_t mc = __ballot(c != 0), ms = __ballot(c == 2);
+    if ((t & 63) == 0) {
+      gm[i >> 6] = mc;
+      sm[i >> 6] = ms;
+    }
   }
   __syncthreads();
 }
 
 // vec: every frame of the batch has W % 4 == 0 and a 4-byte aligned base, so a
-// 4-pixel group is three aligned dwords. Stencils run down columns with
-// rolling register windows (one LDS read per new row instead of a 3x3 gather).
-__global__ __launch_bounds__(256) void k_canny_uf(const FrameDesc* __restrict__ frames, int low, int high, int vec,
-                                                  uint32_t* __restrict__ cbits, uint32_t* __restrict__ rbits,
-                                                  uint16_t* __restrict__ croot, size_t lstride, int32_t* __restrict__ lab,
-                                                  uint8_t* __restrict__ strong, size_t plane, size_t bstride) {
+// 4-pixel group is three aligned dwords.
+__global__ __launch_bounds__(256) void k_canny(const FrameDesc* __restrict__ frames, int low, int high, int vec,
+                                               uint32_t* __restrict__ cbits, uint32_t* __restrict__ sbits,
+                                               size_t bstride) {
   const int f = blockIdx.z;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
   const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
   if (x0 >= W || y0 >= H) return;
-  // LDS regions reused across phases (38 KB: four blocks per CU):
-  //   R1: gray (x0-4 .., y0-3 ..) -> magnitude (x0-1 .., y0-1 ..) -> candidate list
+  // LDS regions reused across phases:
+  //   R1: gray (x0-4 .., y0-3 ..) -> magnitude (x0-1 .., y0-1 ..)
   //   R2: blurred (x0-2 .., y0-2 ..)
-  //   R3: horizontal blur -> gx | gy of the tile -> union-find labels
-  constexpr int BLH = FTH + 4;                     // blurred rows y0-2 .. y0+FTH+1
-  // (interior tiles: magnitude FMH x FGW int16, blurred BLH x FGW bytes)
-  constexpr int R1a = FMH * FGW * 2 > FGH * FGW ? FMH * FGW * 2 : FGH * FGW;
-  constexpr int R1 = R1a > FTW * FTH * 2 ? R1a : FTW * FTH * 2;
+  //   R3: horizontal blur -> gx | gy of the tile
+  constexpr int BLH = FTH + 4;  // blurred rows y0-2 .. y0+FTH+1
+  constexpr int R1 = FMH * FGW * 2 > FGH * FGW ? FMH * FGW * 2 : FGH * FGW;
   __shared__ __align__(16) uint8_t r1[R1];
   __shared__ __align__(16) uint8_t bl[BLH * FGW];
   __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];
-  __shared__ uint8_t K[FTW * FTH];
-  __shared__ uint64_t gm[FTW * FTH / 64], sm[FTW * FTH / 64];  // candidate / strong-root masks
-  __shared__ int32_t gpre[FTW * FTH / 64];
-  __shared__ int ncount;
-  uint8_t* g = r1;
-  int16_t* mag = (int16_t*)r1;
-  int16_t* list = (int16_t*)r1;
-  int* L = (int*)gxy;
+  __shared__ uint64_t gm[FTW * FTH / 64], sm[FTW * FTH / 64];  // candidate / strong masks
   const int t = threadIdx.x;
   const bool interior = vec && x0 >= 4 && x0 + FTW + 4 <= W && y0 >= 3 && y0 + FTH + 3 <= H;
-  if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, t);
-  else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, g, bl, mag, gxy, K, t);
-  if (t < FTW * FTH / 64) sm[t] = 0;
-  const int ncand = tile_uf(K, L, list, &ncount, gm, t);
-  for (int k = t; k < ncand; k += 256) {
-    const int i = list[k];
-    if (K[i] == 2) {
-      const int r = L[i];
-      atomicOr((unsigned long long*)&sm[r >> 6], 1ull << (r & 63));
-    }
-  }
-  // bit planes: candidates, strong tile roots (32-bit word j of the tile = row
-  // j / 4, quarter j % 4 = half j & 1 of the 64-pixel mask j / 2); the
-  // candidates' tile roots, 2 B each, in raster order within the tile (croot:
-  // index = candidates before it = prefix over the 64-pixel masks);
-  // k_hyst_edge finds them again from the candidate bit plane. Sparse labels:
-  // tile roots (own index, strong flag cleared) and the tile-border candidates
-  // the seam unions start from.
+  if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, r1, bl, (int16_t*)r1, gxy, gm, sm, t);
+  else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, r1, bl, (int16_t*)r1, gxy, gm, sm, t);
+  // 32-bit word j of the tile = row j / 4, quarter j % 4 = half j & 1 of mask j / 2
   const int WW = bits::words(W);
-  const size_t ob = (size_t)f * bstride;
-  __syncthreads();
   if (t < 64) {
     const int y = y0 + (t >> 2), w = (x0 >> 5) + (t & 3);
     if (y < H && w < WW) {
-      cbits[ob + (size_t)y * WW + w] = (uint32_t)(gm[t >> 1] >> (32 * (t & 1)));
-      rbits[ob + (size_t)y * WW + w] = (uint32_t)(sm[t >> 1] >> (32 * (t & 1)));
+      const size_t o = (size_t)f * bstride + (size_t)y * WW + w;
+      cbits[o] = (uint32_t)(gm[t >> 1] >> (32 * (t & 1)));
+      sbits[o] = (uint32_t)(sm[t >> 1] >> (32 * (t & 1)));
     }
-    constexpr int NGM = FTW * FTH / 64;
-    const int c = t < NGM ? __popcll(gm[t]) : 0;
-    int inc = c;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int v = __shfl_up(inc, o);
-      if (t >= o) inc += v;
+  }
+}
+
+// ------------------------------------------------ hysteresis: run CCL
+// Runs = maximal spans of candidates in a row, numbered in raster order per
+// frame (k_run_scan gives the row bases); 8-connected unions between
+// consecutive rows, first inside 32-row bands in LDS, then across the band
+// seams on the global labels (the contour CCL's two-level scheme); roots are
+// a component's smallest run id. Run extents (packed u32), labels (int32) and
+// flags (u8) live in planes sized for one run per pixel.
+// run starts / ends of word w of a row (bits past W are zero)
+__device__ inline uint32_t hb_starts(const uint32_t* row, int w) {
+  const uint32_t cur = row[w], prv = w > 0 ? row[w - 1] : 0u;
+  return cur & ~((cur << 1) | (prv >> 31));
+}
+__device__ inline uint32_t hb_ends(const uint32_t* row, int w, int WW) {
+  const uint32_t cur = row[w], nxt = w + 1 < WW ? row[w + 1] : 0u;
+  return cur & ~((cur >> 1) | (nxt << 31));
+}
+// mask of bits [a, b] of word w
+__device__ inline uint32_t span_mask(int w, int a, int b) {
+  const uint32_t lo = w == (a >> 5) ? (0xffffffffu << (a & 31)) : 0xffffffffu;
+  const uint32_t hi = w == (b >> 5) ? (0xffffffffu >> (31 - (b & 31))) : 0xffffffffu;
+  return lo & hi;
+}
+struct HystRuns {  // per-frame planes (frame f at + f * stride)
+  uint32_t* x;     // run extents: start | end << 16
+  int32_t* lab;    // run labels
+  uint8_t* flag;   // per root: bit 2 = the global component holds a strong pixel (denser bands: bits 0 / 1
+                   // = strong / reaches a seam, per band root)
+  int32_t* rowb;   // row bases (H + 1), then the list counters |A|, |B|
+  size_t x_stride, lab_stride, flag_stride, rstride, half;
+};
+
+// wave per row: candidate runs of the row
+__global__ __launch_bounds__(256) void k_hyst_count(const uint32_t* __restrict__ cbits, size_t bstride, HystRuns hr,
+                                                    int W, int H) {
+  const int f = blockIdx.y, y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= H) return;
+  const int WW = bits::words(W);
+  const uint32_t* row = cbits + (size_t)f * bstride + (size_t)y * WW;
+  int c = 0;
+  for (int w = lane; w < WW; w += 64) c += __popc(hb_starts(row, w));
+  c = wave_sum(c);
+  if (lane == 0) hr.rowb[(size_t)f * hr.rstride + y] = c;
+  if (y == 0 && lane == 0) {  // list counters (k_hyst_band): rowb[H + 1] = |A|, rowb[H + 2] = |B|
+    hr.rowb[(size_t)f * hr.rstride + H + 1] = 0;
+    hr.rowb[(size_t)f * hr.rstride + H + 2] = 0;
+  }
+}
+
+// wave per row: run extents; a run's end is the bit before the first zero at
+// or after its start (runs of NMS candidates are short: one or two words)
+__global__ __launch_bounds__(256) void k_hyst_runs(const uint32_t* __restrict__ cbits, size_t bstride, HystRuns hr,
+                                                   int W, int H) {
+  const int f = blockIdx.y, y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= H) return;
+  const int WW = bits::words(W);
+  const uint32_t* row = cbits + (size_t)f * bstride + (size_t)y * WW;
+  uint32_t* X = hr.x + (size_t)f * hr.x_stride;
+  int bs = hr.rowb[(size_t)f * hr.rstride + y];
+  for (int w0 = 0; w0 < WW; w0 += 64) {
+    const int w = w0 + lane;
+    uint32_t S = w < WW ? hb_starts(row, w) : 0u;
+    const int cs = __popc(S);
+    const int is = wave_incl_scan(cs, lane);
+    for (int os = bs + is - cs; S; S &= S - 1, os++) {
+      const int b = __ffs(S) - 1;
+      int ww = w;
+      uint32_t z = ~row[w] & (0xffffffffu << b);
+      while (!z && ++ww < WW) z = ~row[ww];
+      const int e = z ? 32 * ww + __ffs(z) - 2 : 32 * WW - 1;  // bits past W are zero: z is found by then
+      X[os] = (uint32_t)(32 * w + b) | ((uint32_t)e << 16);
     }
-    if (t < NGM) gpre[t] = inc - c;
+    bs += __shfl(is, 63);
+  }
+}
+
+// first run k of [0, n) whose end reaches v, n if none (packed extents)
+__device__ inline int hx_first_end(const uint32_t* x, int n, int v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int)(x[mid] >> 16) >= v) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+// unions of row y's runs [by, by + ny) with row y-1's [bp, bp + np), 8-connected
+template <class UF>
+__device__ inline void hyst_row_union(const uint32_t* x, int bp, int np, int by, int ny, int lane, const UF& uni) {
+  for (int j = lane; j < ny; j += 64) {
+    const int a = x[by + j] & 0xffff, b = x[by + j] >> 16;
+    for (int k = hx_first_end(x + bp, np, a - 1); k < np && (int)(x[bp + k] & 0xffff) <= b + 1; k++)
+      uni(by + j, bp + k);
+  }
+}
+// does the run [a, b] of srow hold a strong pixel
+__device__ inline bool run_strong(const uint32_t* srow, int a, int b) {
+  for (int w = a >> 5; w <= (b >> 5); w++)
+    if (srow[w] & span_mask(w, a, b)) return true;
+  return false;
+}
+
+// Per band of HB_ROWS rows: unions in LDS (labels = band roots, written to
+// the global labels for the seams), then the band's edge words: the runs of
+// band components holding a strong pixel are edges whatever the rest of the
+// frame holds; a band component without one that reaches the band's first or
+// last row (inside the frame) may still meet a strong pixel across a seam, so
+// its runs go to list B; the roots of strong components that reach them go to
+// list A. Lists live in the label plane above the labels (A from hr.half up,
+// B from the top of the plane down; |A| + |B| <= runs <= half). Denser bands
+// (more than HB_CAP runs) take the same steps on the global labels.
+#ifndef MK_HB_ROWS
+#define MK_HB_ROWS 32
+#endif
+#ifndef MK_HB_THREADS
+#define MK_HB_THREADS 512
+#endif
+constexpr int HB_ROWS = MK_HB_ROWS, HB_CAP = 4096, HB_THREADS = MK_HB_THREADS, HB_WAVES = HB_THREADS / 64;
+// band-local union-find on 16-bit labels in LDS (roots = smallest id); the
+// link is a 32-bit CAS on the dword holding the 16-bit slot
+__device__ inline int hb_find(const uint16_t* L, int x) {
+  int p;
+  while ((p = L[x]) != x) x = p;
+  return x;
+}
+__device__ inline void hb_union(uint16_t* L, int a, int b) {
+  while (true) {
+    a = hb_find(L, a);
+    b = hb_find(L, b);
+    if (a == b) return;
+    if (a < b) { const int tt = a; a = b; b = tt; }
+    uint32_t* wp = (uint32_t*)(L + (a & ~1));
+    const int sh = (a & 1) * 16;
+    const uint32_t old = *(volatile uint32_t*)wp;
+    if (((old >> sh) & 0xffffu) != (uint32_t)a) continue;  // a was linked meanwhile: find again
+    const uint32_t nw = (old & ~(0xffffu << sh)) | ((uint32_t)b << sh);
+    if (atomicCAS(wp, old, nw) == old) return;
+  }
+}
+// wave-aggregated list append (one atomic per wave and call; every active lane calls it)
+__device__ inline void hyst_push(int32_t* list, int32_t* count, int v, bool push, bool down, size_t top) {
+  const uint64_t m = __ballot(push);
+  if (!m) return;
+  const int lane = threadIdx.x & 63, leader = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(count, __popcll(m));
+  base = __shfl(base, leader);
+  if (push) {
+    const int k = base + __popcll(m & ((1ull << lane) - 1));
+    list[down ? top - 1 - k : k] = v;
+  }
+}
+__global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __restrict__ sbits, size_t bstride, HystRuns hr,
+                                                   uint32_t* __restrict__ ebits, int W, int H) {
+  __shared__ uint16_t Ll[HB_CAP];
+  __shared__ uint32_t Xl[HB_CAP];
+  __shared__ uint32_t Sl[HB_CAP / 4];  // per root byte: bit 0 strong, bit 1 reaches the band's edge rows
+  __shared__ int32_t rbl[HB_ROWS + 1];
+  extern __shared__ uint32_t Ew[];     // the band's edge words (rows x WW), then its strong words
+  const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int y0 = blockIdx.x * HB_ROWS;
+  if (y0 >= H) return;
+  const int y1 = min(y0 + HB_ROWS, H), WW = bits::words(W), nr = y1 - y0;
+  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
+  int32_t* cnt = hr.rowb + (size_t)f * hr.rstride + H + 1;
+  const uint32_t* X = hr.x + (size_t)f * hr.x_stride;
+  const uint32_t* sb = sbits + (size_t)f * bstride;
+  int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
+  int32_t* lists = L + hr.half;
+  const size_t top = hr.lab_stride - hr.half;
+  uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
+  uint32_t* eb = ebits + (size_t)f * bstride + (size_t)y0 * WW;
+  const int g0 = r[y0], n = r[y1] - g0;
+  // a row whose components may continue past the band: its first / last row inside the frame
+  const auto edge_row = [&](int y) { return (y == y0 && y0 > 0) || (y == y1 - 1 && y1 < H); };
+  if (n > HB_CAP) {
+    for (int i = t; i < n; i += HB_THREADS) {
+      L[g0 + i] = g0 + i;
+      fl[g0 + i] = 0;
+    }
+    for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = 0u;
+    __syncthreads();
+    const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
+    for (int y = y0 + 1 + wave; y < y1; y += HB_WAVES) hyst_row_union(X, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], lane, uni);
+    __syncthreads();
+    for (int y = y0 + wave; y < y1; y += HB_WAVES)
+      for (int j = r[y] + lane; j < r[y + 1]; j += 64) {
+        const int root = uf_find_c(L, j);
+        const uint32_t b = (run_strong(sb + (size_t)y * WW, X[j] & 0xffff, X[j] >> 16) ? 1u : 0u) | (edge_row(y) ? 2u : 0u);
+        if (b) atomicOr((uint32_t*)(fl + (root & ~3)), b << (8 * (root & 3)));
+      }
+    __syncthreads();
+    for (int y = y0 + wave; y < y1; y += HB_WAVES)
+      for (int j = r[y] + lane; j < r[y + 1]; j += 64) {
+        const int root = uf_find_c(L, j);
+        const int fb = fl[root] & 3;
+        if (fb & 1) {
+          const int a = X[j] & 0xffff, b = X[j] >> 16;
+          for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&eb[(y - y0) * WW + w], span_mask(w, a, b));
+        }
+        hyst_push(lists, cnt + 1, j, fb == 2, true, top);
+        hyst_push(lists, cnt, j, root == j && fb == 3, false, top);
+      }
+    return;
+  }
+  for (int i = t; i <= nr; i += HB_THREADS) rbl[i] = r[y0 + i] - g0;
+  for (int i = t; i < n; i += HB_THREADS) {
+    Xl[i] = X[g0 + i];
+    Ll[i] = (uint16_t)i;
+  }
+  uint32_t* Sw = Ew + nr * WW;
+  for (int i = t; i < (n + 3) / 4; i += HB_THREADS) Sl[i] = 0u;
+  for (int i = t; i < nr * WW; i += HB_THREADS) {
+    Ew[i] = 0u;
+    Sw[i] = sb[(size_t)y0 * WW + i];
   }
   __syncthreads();
-  int32_t* l = lab + (size_t)f * plane;
-  uint8_t* sg = strong + (size_t)f * plane;
-  uint16_t* cr = croot + (size_t)f * lstride + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * (FTW * FTH);
-  for (int k = t; k < ncand; k += 256) {
-    const int i = list[k];
-    cr[gpre[i >> 6] + __popcll(gm[i >> 6] & ((1ull << (i & 63)) - 1))] = (uint16_t)L[i];
+  uint16_t* Li = Ll;
+  const auto uni = [Li](int a, int b) { hb_union(Li, a, b); };
+  for (int y = y0 + 1 + wave; y < y1; y += HB_WAVES) {
+    const int q = y - y0;
+    hyst_row_union(Xl, rbl[q - 1], rbl[q] - rbl[q - 1], rbl[q], rbl[q + 1] - rbl[q], lane, uni);
   }
-  for (int k = t; k < ncand; k += 256) {
-    const int i = list[k];
-    const int lx = i % FTW, ly = i / FTW;
-    const int p = (y0 + ly) * W + x0 + lx;
-    const int r = L[i];
-    if (r == i) {
-      l[p] = p;
-      sg[p] = 0;
-    } else if (lx == 0 || ly == 0 || lx == FTW - 1 || ly == FTH - 1) {
-      l[p] = (y0 + r / FTW) * W + x0 + (r % FTW);
-    }
-  }
-}
-
-__device__ inline bool cbit(const uint32_t* cb, int WW, int x, int y) {
-  return (cb[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u;
-}
-
-// unions across tile seams: one thread per pixel of the vertical seams
-// (x = k*FTW), then one per 32-pixel word of the horizontal seams (y = k*FTH),
-// whose candidates meet the row above through shifted words
-__global__ __launch_bounds__(256) void k_hyst_seam(const uint32_t* __restrict__ cbits, int32_t* lab, int W, int H,
-                                                   size_t plane, size_t bstride) {
-  const int f = blockIdx.y;
-  const uint32_t* cb = cbits + (size_t)f * bstride;
-  const int WW = bits::words(W);
-  int32_t* l = lab + (size_t)f * plane;
-  const int nvs = (W - 1) / FTW, nhs = (H - 1) / FTH;
-  const size_t nv = (size_t)nvs * H, n = nv + (size_t)nhs * WW;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    if (k < nv) {
-      const int x = (int)(k / H + 1) * FTW, y = (int)(k % H);
-      if (!cbit(cb, WW, x, y)) continue;
-      const int p = y * W + x;
-      if (cbit(cb, WW, x - 1, y)) uf_union_c(l, p, p - 1);
-      if (y > 0 && cbit(cb, WW, x - 1, y - 1)) uf_union_c(l, p, p - W - 1);
-      if (y + 1 < H && cbit(cb, WW, x - 1, y + 1)) uf_union_c(l, p, p + W - 1);
-      continue;
-    }
-    const size_t h = k - nv;
-    const int y = (int)(h / WW + 1) * FTH, w = (int)(h % WW);
-    const uint32_t cur = cb[(size_t)y * WW + w];
-    if (!cur) continue;
-    const uint32_t* up = cb + (size_t)(y - 1) * WW;
-    const uint32_t a = up[w], ap = w > 0 ? up[w - 1] : 0u, an = w + 1 < WW ? up[w + 1] : 0u;
-    const uint32_t ul = (a << 1) | (ap >> 31), ur = (a >> 1) | (an << 31);  // bit b: x-1 / x+1 above
-    for (uint32_t mm = cur & (a | ul | ur); mm; mm &= mm - 1) {
-      const int b = __ffs(mm) - 1;
-      const int p = y * W + 32 * w + b;
-      if ((a >> b) & 1u) uf_union_c(l, p, p - W);
-      if ((ul >> b) & 1u) uf_union_c(l, p, p - W - 1);
-      if ((ur >> b) & 1u) uf_union_c(l, p, p - W + 1);
-    }
-  }
-}
-
-// strong tile roots mark their global root; one 32-pixel word per work-item
-__global__ __launch_bounds__(256) void k_hyst_mark(const uint32_t* __restrict__ rbits, int32_t* lab, uint8_t* strong,
-                                                   int W, int H, size_t plane, size_t bstride) {
-  const int f = blockIdx.y;
-  const int WW = bits::words(W);
-  const size_t n = (size_t)WW * H;
-  int32_t* l = lab + (size_t)f * plane;
-  uint8_t* sg = strong + (size_t)f * plane;
-  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (size_t)gridDim.x * blockDim.x) {
-    uint32_t w = rbits[(size_t)f * bstride + k];
-    if (!w) continue;
-    const int y = (int)(k / WW), xb = (int)(k % WW) * 32;
-    while (w) {
-      const int b = __ffs(w) - 1;
-      w &= w - 1;
-      sg[uf_find_c(l, y * W + xb + b)] = 1;
-    }
-  }
-}
-
-// edge = candidate whose global root is marked. One wave per tile, lane t
-// owning the tile's 32-pixel word t (row t / 4, quarter t % 4), so only the
-// sparse candidates are visited: their tile roots come from k_canny_uf's root
-// list (croot, raster order = lane order then bit order); each tile root looks
-// up its global root once (a bit of Fb), then every candidate reads its
-// tile root's bit. Four tiles per 256-thread block.
-__global__ __launch_bounds__(256) void k_hyst_edge(const uint32_t* __restrict__ cbits,
-                                                   const uint16_t* __restrict__ croot, size_t lstride, int32_t* lab,
-                                                   const uint8_t* __restrict__ strong, uint32_t* __restrict__ ebits,
-                                                   uint8_t* __restrict__ edge, int W, int H, size_t plane,
-                                                   size_t bstride, int gx, int ntiles) {
-  static_assert(FTW == 128 && FTW * FTH == 32 * 64, "one 32-pixel word per lane");
-  __shared__ uint16_t Rl[4][FTW * FTH];
-  __shared__ uint32_t Fb[4][64];
-  const int f = blockIdx.y, t = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int tile = blockIdx.x * 4 + wv;
-  const bool live = tile < ntiles;
-  const int bx = live ? tile % gx : 0, by = live ? tile / gx : 0;
-  const int x0 = bx * FTW, y0 = by * FTH;
-  const int WW = bits::words(W);
-  const size_t ob = (size_t)f * bstride;
-  const int y = y0 + (t >> 2), w = (x0 >> 5) + (t & 3);
-  const bool in = live && y < H && w < WW;
-  const uint32_t m = in ? cbits[ob + (size_t)y * WW + w] : 0u;
-  const int c = __popc(m);
-  int inc = c;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(inc, o);
-    if (t >= o) inc += v;
-  }
-  const uint16_t* cr = croot + (size_t)f * lstride + (size_t)tile * (FTW * FTH);
-  uint16_t* R = Rl[wv];
-  int32_t* l = lab + (size_t)f * plane;
-  const uint8_t* sg = strong + (size_t)f * plane;
-  uint32_t fl = 0;
-  {
-    int j = inc - c;
-    for (uint32_t mm = m; mm; mm &= mm - 1, j++) {
-      const int b = __ffs(mm) - 1, i = 32 * t + b;
-      const uint16_t r = cr[j];
-      R[j] = r;
-      if (r == i && sg[uf_find_c(l, y * W + x0 + 32 * (t & 3) + b)]) fl |= 1u << b;
-    }
-  }
-  Fb[wv][t] = fl;
   __syncthreads();
-  uint32_t e = 0;
-  {
-    int j = inc - c;
-    for (uint32_t mm = m; mm; mm &= mm - 1, j++) {
-      const int r = R[j];
-      e |= ((Fb[wv][r >> 5] >> (r & 31)) & 1u) << (__ffs(mm) - 1);
+  for (int y = y0 + wave; y < y1; y += HB_WAVES) {
+    const int q = y - y0;
+    for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
+      const int root = hb_find(Ll, j);
+      Ll[j] = (uint16_t)root;
+      const uint32_t b = (run_strong(Sw + q * WW, Xl[j] & 0xffff, Xl[j] >> 16) ? 1u : 0u) | (edge_row(y) ? 2u : 0u);
+      if (b) atomicOr(&Sl[root >> 2], b << (8 * (root & 3)));
     }
   }
-  if (in) ebits[ob + (size_t)y * WW + w] = e;
-  if (edge && in) {
-    uint8_t* ep = edge + (size_t)f * plane + (size_t)y * W;
-    for (int b = 0; b < 32; b++) {
-      const int x = 32 * w + b;
-      if (x < W) ep[x] = (e >> b) & 1u;
+  __syncthreads();
+  for (int y = y0 + wave; y < y1; y += HB_WAVES) {
+    const int q = y - y0;
+    for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
+      const int root = Ll[j];
+      const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
+      L[g0 + j] = g0 + root;
+      fl[g0 + j] = 0;
+      if (fb & 1) {
+        const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
+        for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
+      }
+      hyst_push(lists, cnt + 1, g0 + j, fb == 2, true, top);
+      hyst_push(lists, cnt, g0 + j, root == j && fb == 3, false, top);
     }
+  }
+  __syncthreads();
+  for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = Ew[i];
+}
+
+// one wave per band boundary row y = k * HB_ROWS against row y-1
+__global__ __launch_bounds__(256) void k_hyst_seam(HystRuns hr, int H) {
+  const int f = blockIdx.y, lane = threadIdx.x & 63;
+  const int y = (blockIdx.x * 4 + (threadIdx.x >> 6) + 1) * HB_ROWS;
+  if (y >= H) return;
+  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
+  int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
+  const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
+  hyst_row_union(hr.x + (size_t)f * hr.x_stride, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], lane, uni);
+}
+
+// list A: strong band components reaching a seam mark their global root (bit 2)
+__global__ __launch_bounds__(256) void k_hyst_mark(HystRuns hr, int H) {
+  const int f = blockIdx.y;
+  const int n = hr.rowb[(size_t)f * hr.rstride + H + 1];
+  int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
+  const int32_t* A = L + hr.half;
+  uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int root = uf_find_c(L, A[i]);
+    if (!(fl[root] & 4)) atomicOr((uint32_t*)(fl + (root & ~3)), 4u << (8 * (root & 3)));
+  }
+}
+
+// list B: runs of weak band components whose global root is marked become edges
+__global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restrict__ ebits, size_t bstride, int W,
+                                                  int H) {
+  const int f = blockIdx.y;
+  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
+  const int n = r[H + 2];
+  int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
+  const int32_t* Bl = L + hr.lab_stride - 1;  // B[i] = Bl[-i]
+  const uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
+  const uint32_t* X = hr.x + (size_t)f * hr.x_stride;
+  const int WW = bits::words(W);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int j = Bl[-i];
+    if (!(fl[uf_find_c(L, j)] & 4)) continue;
+    int lo = 0, hi = H - 1;  // row of run j: largest y with r[y] <= j
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (r[mid] <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    const int a = X[j] & 0xffff, b = X[j] >> 16;
+    uint32_t* eb = ebits + (size_t)f * bstride + (size_t)lo * WW;
+    for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&eb[w], span_mask(w, a, b));
   }
 }
 
@@ -812,17 +902,6 @@ __global__ __launch_bounds__(256) void k_bits_to_bytes(const uint32_t* __restric
 __device__ inline uint32_t run_starts(const uint32_t* row, int w) {
   const uint32_t cur = row[w], prv = w > 0 ? row[w - 1] : 0u;
   return cur ^ ((cur << 1) | (prv >> 31));
-}
-__device__ inline int wave_sum(int v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ inline int wave_incl_scan(int v, int lane) {
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o);
-    if (lane >= o) v += u;
-  }
-  return v;
 }
 
 __global__ __launch_bounds__(256) void k_run_count(const uint32_t* __restrict__ dbits, size_t dstride,
