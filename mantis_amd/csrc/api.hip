@@ -285,9 +285,9 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const size_t P = c->plane;
   mark(c, "start");
   const size_t B = c->bstride;
-  dim3 gf((W + FTW - 1) / FTW, (H + FTH - 1) / FTH, n);
-  k_canny<<<gf, 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low, c->vec_ok ? 1 : 0, c->d_b1,
-                                c->d_b2, B);
+  const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
+  k_canny<<<(unsigned)(tgx * tgy * n), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
+                                                      c->vec_ok ? 1 : 0, c->d_b1, c->d_b2, B, tgx, tgy);
   mark(c, "canny_nms");
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
   HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, P, c->rstride, P / 2};

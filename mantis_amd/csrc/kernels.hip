@@ -370,13 +370,20 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
 
 // vec: every frame of the batch has W % 4 == 0 and a 4-byte aligned base, so a
 // 4-pixel group is three aligned dwords.
+// One-dimensional grid of gx * gy tiles per frame, remapped XCD-aware: blocks
+// b and b + 8 share an XCD (round-robin dealing), so every group of blocks
+// with the same b % 8 takes one contiguous run of tiles (frame-major,
+// row-major within a frame) and a tile's halo rows, read again by the tile
+// below, stay in that XCD's L2 (bijective remap, cdna_hip_programming.md T1).
 __global__ __launch_bounds__(256) void k_canny(const FrameDesc* __restrict__ frames, int low, int high, int vec,
                                                uint32_t* __restrict__ cbits, uint32_t* __restrict__ sbits,
-                                               size_t bstride) {
-  const int f = blockIdx.z;
+                                               size_t bstride, int gx, int gy) {
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+  const int f = wgid / (gx * gy), ti = wgid - f * (gx * gy);
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const int x0 = blockIdx.x * FTW, y0 = blockIdx.y * FTH;
+  const int x0 = (ti % gx) * FTW, y0 = (ti / gx) * FTH;
   if (x0 >= W || y0 >= H) return;
   // LDS regions reused across phases:
   //   R1: gray (x0-4 .., y0-3 ..) -> magnitude (x0-1 .., y0-1 ..)

@@ -1,28 +1,43 @@
 #!/bin/bash
-# HBM traffic of the Canny front-end kernel (GPU box): FETCH_SIZE and WRITE_SIZE
-# in separate passes (MI355X_MICROARCH.md: they do not fit one pass), 256
-# frames per launch; writes gpurun_out/pmc_traffic.json (bytes per frame).
+# HBM traffic of the Canny front-end and hysteresis kernels (GPU box):
+# FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md: they do
+# not fit one pass), 256 frames per launch (707 MB of BGR input: past the
+# 256 MiB Infinity Cache); writes gpurun_out/pmc_traffic.json (bytes per frame).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
-  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C -f csv -d "$R/gpurun_out/pmc_$C" -o run -- python3 "$R/bench.py" --no-cpu --rigs 64 --contexts 1 --steps 2 --warmup 1 --latency-iters 1 > "$R/gpurun_out/pmc_$C.log" 2>&1 || { tail -20 "$R/gpurun_out/pmc_$C.log"; exit 1; }
+  cd /tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $C -f csv -d "$R/gpurun_out/pmc_$C" -o run -- python3 "$R/bench.py" --no-cpu --rigs 64 --contexts 1 --steps 2 --warmup 1 --latency-iters 1 --ingest-steps 0 > "$R/gpurun_out/pmc_$C.log" 2>&1 || { tail -20 "$R/gpurun_out/pmc_$C.log"; exit 1; }
 done
 python3 - "$R/gpurun_out" <<'P'
 import csv, glob, json, sys
-out = {"stage": "canny_nms", "kernel": "k_canny_uf"}
+FR = 256
+kern = {"canny_nms": ["k_canny"], "hysteresis": ["k_hyst_count", "k_run_scan", "k_hyst_runs", "k_hyst_band",
+                                                 "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"]}
+out = {"stage": "canny_nms", "kernel": "k_canny", "frames_per_launch": FR}
+per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(f"{sys.argv[1]}/pmc_{c}/**/*counter_collection.csv", recursive=True)[0]
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-            if r["Kernel_Name"].startswith("mk::k_canny_uf") and int(r["Grid_Size"]) == 10 * 45 * 256 * 256]
-    out[c + "_kB_per_launch"] = sum(vals) / len(vals)
-    out["launches_" + c] = len(vals)
-# FETCH_SIZE/WRITE_SIZE are in kB; FETCH_SIZE counts half of wide coalesced reads on gfx950
-out["fetch_raw_bytes_per_frame"] = out["FETCH_SIZE_kB_per_launch"] * 1024 / 256
-fetch = out["FETCH_SIZE_kB_per_launch"] * 1024 * 2
-write = out["WRITE_SIZE_kB_per_launch"] * 1024
-out["hbm_bytes_per_frame"] = (fetch + write) / 256
-out["note"] = "FETCH_SIZE doubled (gfx950 correction for wide coalesced reads; 12-byte-per-lane loads are uncalibrated), WRITE_SIZE as reported; per frame of 1280x720"
+    rows = list(csv.DictReader(open(f)))
+    for stage, names in kern.items():
+        tot = 0.0
+        for k in names:
+            sel = [r for r in rows if r["Kernel_Name"].split("(")[0] == "mk::" + k]
+            if not sel:
+                continue
+            g = max(int(r["Grid_Size"]) for r in sel)
+            vals = [float(r["Counter_Value"]) for r in sel if int(r["Grid_Size"]) == g]
+            v = sum(vals) / len(vals) * 1024 / FR  # kB per launch -> bytes per frame
+            per[f"{k}_{c}_bytes_per_frame"] = round(v)
+            tot += v
+        per[f"{stage}_{c}_bytes_per_frame"] = round(tot)
+out.update(per)
+# FETCH_SIZE counts half of wide coalesced reads on gfx950: doubled (uncalibrated for 12-B-per-lane loads)
+for stage in kern:
+    out[f"{stage}_hbm_bytes_per_frame"] = 2 * per[f"{stage}_FETCH_SIZE_bytes_per_frame"] + per[f"{stage}_WRITE_SIZE_bytes_per_frame"]
+out["hbm_bytes_per_frame"] = out["canny_nms_hbm_bytes_per_frame"]
+out["note"] = ("per 1280x720 frame; FETCH_SIZE doubled (gfx950 correction for wide coalesced reads; the 12-byte-"
+               "per-lane BGR loads are uncalibrated), WRITE_SIZE as reported")
 json.dump(out, open(f"{sys.argv[1]}/pmc_traffic.json", "w"), indent=1)
 print(json.dumps(out))
 P
