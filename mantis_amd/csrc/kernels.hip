@@ -1,20 +1,24 @@
 // HIP kernels (gfx950) of the mantis3 per-frame hot path. Host side: api.hip.
 //
 // Stage map (reference -> kernel):
-//   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny_uf (+ tile union-find)
-//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_seam / _mark / _edge
+//   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny (candidate / strong bit planes)
+//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_count / k_run_scan / k_hyst_runs /
+//                                                                    k_hyst_band / _seam / _mark / _fix (run CCL)
 //   dilate x2 / erode x1             QuadDetection.h:213-214         k_morph (bit planes, LDS bands)
 //   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_morph (same pass)
-//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_run_count/_scan/_emit/_union/_border (run CCL)
-//                                                                    + k_trace_borders
-//                                                                    + k_frame_contours
+//   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_run_count/_scan/_emit/_band/_seam/_border
+//                                                                    (run CCL) + k_tile_bits + k_trace_borders
+//                                                                    (+ _lds) + k_frame_contours
 //   approxPolyDP / Quadrilateral /
 //   removeDuplicateQuads / undistort QuadDetection.h:13-171, 219-228, 289-298   k_frame_contours
-//   CoPlanarPoseEstimator -> RPP     CoPlanarPoseEstimator.cpp:16-58 k_rpp_s1 / _s1b / _refine / _merge
+//   CoPlanarPoseEstimator -> RPP     CoPlanarPoseEstimator.cpp:16-58 k_rpp_prep, k_objpose_q<0>, k_rpp_s1b,
+//                                                                    k_objpose_q<1>, k_rpp_merge (+ per-quad GN)
 //   generateCentralHypotheses +
 //   PoseClusterer                    HypothesisGeneration.h:57-109, PoseClusterer.cpp:33-116  k_frame_hyps
 //   evaluate / PF / shifts / yaw /
-//   publish gate                     src/mantis3.cpp:102-132          k_frame_score
+//   publish gate                     src/mantis3.cpp:102-132          k_score_init / k_score_pf / k_score_final
+//   legacy camera weighting          legacy/mantis/MonteCarlo.cpp:183-241  k_rig_weight
+//   stage entries, dense grid        HypothesisEvaluation.h:31-41    k_score_api, k_argmin, k_quad_gn
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
