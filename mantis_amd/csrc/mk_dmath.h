@@ -33,6 +33,38 @@ __device__ inline double sk() {
 }
 __device__ inline double kd(unsigned long long b) { return __longlong_as_double((long long)b); }
 
+// __ocmlpriv_atanred_f64 + __ocml_atan_f64 for x = +0, positive or NaN with
+// inv = 1.0 / x already computed (the fisheye projection divides by r anyway:
+// sharing the one IEEE division is exact, fabs(x) == x and copysign is a no-op)
+__device__ inline double atan_pos(double x, double inv) {
+  const double ax = x;
+  const bool big = ax > 1.0;
+  const double a = big ? inv : ax;
+  const double s = a * a;
+  double p = __builtin_fma(s, sk<0x3EEBA404B5E68A13ull>(), sk<0xBF23E260BD3237F4ull>());
+  p = __builtin_fma(s, p, sk<0x3F4B2BB069EFB384ull>());
+  p = __builtin_fma(s, p, sk<0xBF67952DAF56DE9Bull>());
+  p = __builtin_fma(s, p, sk<0x3F7D6D43A595C56Full>());
+  p = __builtin_fma(s, p, sk<0xBF8C6EA4A57D9582ull>());
+  p = __builtin_fma(s, p, sk<0x3F967E295F08B19Full>());
+  p = __builtin_fma(s, p, sk<0xBF9E9AE6FC27006Aull>());
+  p = __builtin_fma(s, p, sk<0x3FA2C15B5711927Aull>());
+  p = __builtin_fma(s, p, sk<0xBFA59976E82D3FF0ull>());
+  p = __builtin_fma(s, p, sk<0x3FA82D5D6EF28734ull>());
+  p = __builtin_fma(s, p, sk<0xBFAAE5CE6A214619ull>());
+  p = __builtin_fma(s, p, sk<0x3FAE1BB48427B883ull>());
+  p = __builtin_fma(s, p, sk<0xBFB110E48B207F05ull>());
+  p = __builtin_fma(s, p, sk<0x3FB3B13657B87036ull>());
+  p = __builtin_fma(s, p, sk<0xBFB745D119378E4Full>());
+  p = __builtin_fma(s, p, sk<0x3FBC71C717E1913Cull>());
+  p = __builtin_fma(s, p, sk<0xBFC2492492376B7Dull>());
+  p = __builtin_fma(s, p, sk<0x3FC99999999952CCull>());
+  p = __builtin_fma(s, p, sk<0xBFD5555555555523ull>());
+  const double q = s * p;
+  const double red = __builtin_fma(a, q, a);
+  return big ? __builtin_fma(kd(0x3FEDD9AD336A0500ull), kd(0x3FFAF154EEB562D6ull), -red) : red;
+}
+
 // __ocmlpriv_atanred_f64 + __ocml_atan_f64
 __device__ inline double atan(double x) {
   const double ax = __builtin_fabs(x);
@@ -132,6 +164,7 @@ __device__ inline void sincos_small(double x, double* s_out, double* c_out) {
 #ifdef __HIPCC__
 // host pass of a HIP translation unit: declarations only (never executed)
 __host__ __device__ inline double atan(double x) { return ::atan(x); }
+__host__ __device__ inline double atan_pos(double x, double) { return ::atan(x); }
 __host__ __device__ inline void sincos_small(double x, double* s, double* c) {
   *s = ::sin(x);
   *c = ::cos(x);

@@ -171,16 +171,18 @@ struct Cam {
 MK_HD void distort(const Cam& cm, double X, double Y, double Z, double* u, double* v) {
   double x = X / Z, y = Y / Z;
   double r2 = x * x + y * y;
-  double r = sqrt(r2);
+  double r = sqrt(r2);  // +0, positive or NaN
 #if MK_DM_DEVICE
-  double theta = dm::atan(r);  // ocml atan, op for op (mk_dmath.h)
+  const double inv_r0 = 1.0 / r;                // shared by atan's reduction and the 1/r below
+  double theta = dm::atan_pos(r, inv_r0);       // ocml atan, op for op (mk_dmath.h)
 #else
+  const double inv_r0 = 1.0 / r;
   double theta = atan(r);
 #endif
   double theta2 = theta * theta, theta3 = theta2 * theta, theta4 = theta2 * theta2, theta5 = theta4 * theta,
          theta6 = theta3 * theta3, theta7 = theta6 * theta, theta8 = theta4 * theta4, theta9 = theta8 * theta;
   double theta_d = theta + cm.k[0] * theta3 + cm.k[1] * theta5 + cm.k[2] * theta7 + cm.k[3] * theta9;
-  double inv_r = r > 1e-8 ? 1.0 / r : 1;
+  double inv_r = r > 1e-8 ? inv_r0 : 1;
   double cdist = r > 1e-8 ? theta_d * inv_r : 1;
   double xd0 = x * cdist, xd1 = y * cdist;
   double xd3 = xd0 + 0.0 * xd1;

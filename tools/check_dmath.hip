@@ -23,6 +23,11 @@ __global__ void kcheck(uint64_t n, unsigned long long* bad) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const double x = input(i);
     if (__double_as_longlong(mk::dm::atan(x)) != __double_as_longlong(::atan(x))) atomicAdd(&bad[0], 1ull);
+    {  // the projection's form: x >= 0 with the shared reciprocal
+      const double ax = __builtin_fabs(x);
+      if (__double_as_longlong(mk::dm::atan_pos(ax, 1.0 / ax)) != __double_as_longlong(::atan(ax)))
+        atomicAdd(&bad[0], 1ull);
+    }
     if (__builtin_fabs(x) < 1073741824.0) {
       double s, c;
       mk::dm::sincos_small(x, &s, &c);
