@@ -316,40 +316,44 @@ def run_config3(a, rk, cpu):
     imgs = [M.make_image(None, K, D, T_base_cam=Tbc[i % nd], device_ptr=dev + (i % nd) * fb, width=W, height=H)
             for i in range(n_frames)]
     per_ctx = [imgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS] for k in range(nctx)]
+    batches = [M.Batch(ctxs[k], per_ctx[k], rigs_ctx) for k in range(nctx)]
     from concurrent.futures import ThreadPoolExecutor
 
     pool = ThreadPoolExecutor(max_workers=nctx)
+    stage_ms = {}
 
-    def run_step(parts):
-        """One step: every context processes its share of the rigs, concurrently."""
-        futs = [pool.submit(ctxs[k].process, parts[k], rigs_ctx) for k in range(nctx)]
-        outs = [f.result() for f in futs]
-        return [r for o in outs for r in o[0]], [c for o in outs for c in o[1]]
+    def run_steps(bs, k_steps, record=False):
+        """k_steps steps: every context's host thread runs its share of each step
+        back to back (one C call per step), the contexts concurrently."""
+        def worker(k):
+            for _ in range(k_steps):
+                bs[k].run()
+                if record and k == 0:
+                    for name, ms in m.kernel_times():
+                        stage_ms[name] = stage_ms.get(name, 0.0) + ms
+        for f in [pool.submit(worker, k) for k in range(nctx)]:
+            f.result()
 
     def barrier_sync():
         rk.barrier()
         for mc in ctxs:
             mc.synchronize()
 
-    for _ in range(a.warmup):
-        run_step(per_ctx)
+    run_steps(batches, a.warmup)
 
     # ---- timed region: stage events on context 0's stream
     m.set_profiling(True)
-    stage_ms, scored, published = {}, 0, 0
     barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        rig, cam = run_step(per_ctx)
-        for name, ms in m.kernel_times():
-            stage_ms[name] = stage_ms.get(name, 0.0) + ms
-        scored += sum(c.n_scored for c in cam)
-        published += sum(r.publish for r in rig)
+    run_steps(batches, a.steps, record=True)
     barrier_sync()
     elapsed = rk.max(time.perf_counter() - t0)
     m.set_profiling(False)
     value = a.rigs * a.steps * rk.world / elapsed
     ms_per_step = elapsed / a.steps * 1e3
+    # every step processes the same frames: the last step's records describe each step
+    scored = a.steps * sum(c.n_scored for b in batches for c in b.cam_out)
+    published = a.steps * sum(r.publish for b in batches for r in b.out)
 
     # ---- per-step work counts (every step processes the same frames, so the
     # counters of the last step describe each step): ObjPose iterations of the
@@ -452,12 +456,11 @@ def run_config3(a, rk, cpu):
     himgs = [M.make_image(host[i % nd], K, D, T_base_cam=Tbc[i % nd]) for i in range(n_frames)]
     p50_host = p50_of(himgs[:CAMS])
     if a.ingest_steps > 0:
-        hper = [himgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS] for k in range(nctx)]
-        run_step(hper)  # one untimed pass over the host path
+        hb = [M.Batch(ctxs[k], himgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS], rigs_ctx) for k in range(nctx)]
+        run_steps(hb, 1)  # one untimed pass over the host path
         barrier_sync()
         t0 = time.perf_counter()
-        for _ in range(a.ingest_steps):
-            run_step(hper)
+        run_steps(hb, a.ingest_steps)
         barrier_sync()
         el = rk.max(time.perf_counter() - t0)
         h2d_bytes = n_frames * fb * a.ingest_steps
@@ -468,6 +471,8 @@ def run_config3(a, rk, cpu):
                   "note": "frames passed as pageable host BGR buffers (mem_kind 0); staging H2D inside the timed "
                           "region; never the headline value"}
     del host, himgs
+    if a.ingest_steps > 0:
+        del hb
 
     line = None
     if rk.rank == 0:

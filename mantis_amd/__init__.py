@@ -252,6 +252,22 @@ def make_image(bgr, K, D, T_base_cam=None, device_ptr=None, width=None, height=N
     return im
 
 
+class Batch:
+    """mantis_process_batch arguments built once (the bench's throughput path:
+    no per-call Python conversion of thousands of ctypes records). run() is
+    one C call (ctypes releases the GIL); results stay in .out / .cam_out."""
+
+    def __init__(self, ctx, images, rigs):
+        self.ctx, self.n, self.rigs = ctx, len(images), rigs
+        self.cams = (MantisImage * self.n)(*images)
+        self.out = (MantisResult * rigs)()
+        self.cam_out = (MantisCamResult * self.n)()
+
+    def run(self):
+        st = lib().mantis_process_batch(self.ctx.h, self.cams, self.rigs, self.n // self.rigs, self.out, self.cam_out)
+        self.ctx._chk(st, "process_batch")
+
+
 class Mantis:
     """One mantis_amd context (one GPU, one HIP stream, one cv::RNG stream)."""
 
