@@ -495,3 +495,37 @@ def test_service_motion_prediction(landmark_map):
     c_, _ = m.process_motion(rigs[1][1], delta[:3, 3], q)
     assert bytes(c_) == bytes(b)
     m.close()
+
+
+def test_dense_config5_full_grid_8_shards(m720, landmark_map):
+    """Config 5 at its full size: 81 shifts x 4 yaws x 50 perturbations =
+    16,200 hypotheses x 720 landmarks. The device argmin equals the first
+    minimum of the per-hypothesis errors; the 8-shard split of BASELINE
+    config 5 (2,025 per rank) combined by the cross-rank rule (what the RCCL
+    all-gather feeds every rank) gives the same winner; a sample of 400
+    hypotheses (every 40th, plus the winner) is bit-identical to the oracle."""
+    import mantis_amd as M
+    from mantis_amd import dense
+
+    rng = np.random.default_rng(77)
+    R, pos = synth.random_pose(rng)
+    K, D = synth.intrinsics()
+    img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(5, 2))
+    im = M.make_image(img, K, D)
+    _, mask = m720.masks(im)
+    hyps = dense.config5_hypotheses(R, pos, np.random.default_rng(5))
+    assert len(hyps) == 16200
+    err, npj = m720.score(im, hyps, fast=True, mask=mask)
+    e, i = m720.score_argmin(im, hyps, 0, False, mask)
+    assert i == int(np.argmin(err)) and e == err.min()
+    pairs = []
+    for r in range(8):
+        lo, hi = dense.shard_range(len(hyps), r, 8)
+        assert hi - lo == 2025
+        pairs.append(m720.score_argmin(im, hyps[lo:hi], lo, False, mask))
+    assert M.argmin_pick(pairs) == (e, i)
+    orc = O.Oracle(*landmark_map, seed=1)
+    cleaned = img * (mask[..., None] != 0)
+    sel = np.unique(np.concatenate([np.arange(0, 16200, 40), [i]]))
+    oe, on = orc.score(cleaned, K, D, hyps[sel], fast=True)
+    assert np.array_equal(err[sel], oe) and np.array_equal(npj[sel], on)
