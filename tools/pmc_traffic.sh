@@ -32,12 +32,13 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             tot += v
         per[f"{stage}_{c}_bytes_per_frame"] = round(tot)
 out.update(per)
-# FETCH_SIZE counts half of wide coalesced reads on gfx950: doubled (uncalibrated for 12-B-per-lane loads)
-for stage in kern:
-    out[f"{stage}_hbm_bytes_per_frame"] = 2 * per[f"{stage}_FETCH_SIZE_bytes_per_frame"] + per[f"{stage}_WRITE_SIZE_bytes_per_frame"]
+# calibration (tools/pmc_calib.hip, profiles/r02_pmc_calib.txt): FETCH_SIZE reports 1/2 of the bytes of
+# 12- and 16-byte-per-lane reads; k_canny's 4-byte-per-lane tile-row stores report 2x their bytes
+out["canny_nms_hbm_bytes_per_frame"] = 2 * per["canny_nms_FETCH_SIZE_bytes_per_frame"] + per["canny_nms_WRITE_SIZE_bytes_per_frame"] // 2
+out["hysteresis_hbm_bytes_per_frame"] = 2 * per["hysteresis_FETCH_SIZE_bytes_per_frame"] + per["hysteresis_WRITE_SIZE_bytes_per_frame"]
 out["hbm_bytes_per_frame"] = out["canny_nms_hbm_bytes_per_frame"]
-out["note"] = ("per 1280x720 frame; FETCH_SIZE doubled (gfx950 correction for wide coalesced reads; the 12-byte-"
-               "per-lane BGR loads are uncalibrated), WRITE_SIZE as reported")
+out["note"] = ("per 1280x720 frame; k_canny: FETCH_SIZE x 2 + WRITE_SIZE / 2 (both factors calibrated on its access "
+               "widths, tools/pmc_calib.hip); hysteresis: FETCH_SIZE x 2 + WRITE_SIZE (its store widths uncalibrated)")
 json.dump(out, open(f"{sys.argv[1]}/pmc_traffic.json", "w"), indent=1)
 print(json.dumps(out))
 P
