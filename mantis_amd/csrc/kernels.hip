@@ -405,12 +405,13 @@ __global__ __launch_bounds__(256) void k_canny(const FrameDesc* __restrict__ fra
   else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, r1, bl, (int16_t*)r1, gxy, gm, sm, t);
   // 32-bit word j of the tile = row j / 4, quarter j % 4 = half j & 1 of mask j / 2
   const int WW = bits::words(W);
-  if (t < 64) {
-    const int y = y0 + (t >> 2), w = (x0 >> 5) + (t & 3);
+  static_assert(FTW == 128, "four 32-pixel words per tile row");
+  for (int j = t; j < FTW * FTH / 32; j += 256) {
+    const int y = y0 + (j >> 2), w = (x0 >> 5) + (j & 3);
     if (y < H && w < WW) {
       const size_t o = (size_t)f * bstride + (size_t)y * WW + w;
-      cbits[o] = (uint32_t)(gm[t >> 1] >> (32 * (t & 1)));
-      sbits[o] = (uint32_t)(sm[t >> 1] >> (32 * (t & 1)));
+      cbits[o] = (uint32_t)(gm[j >> 1] >> (32 * (j & 1)));
+      sbits[o] = (uint32_t)(sm[j >> 1] >> (32 * (j & 1)));
     }
   }
 }
