@@ -449,7 +449,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s));
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
-  k_score_init<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
+  k_score_init<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
                                               c->d_dbg, c->d_sst);
   // small batches (latency): 16 waves per frame, two per particle over halves
   // of the landmarks; large batches: 10 waves, one per particle
@@ -460,7 +460,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
     k_score_pf<kScoreThreads, 1><<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st,
                                                                 c->d_gauss, c->d_res, c->d_dbg, c->d_sst,
                                                                 c->cfg.particles, c->cfg.iterations);
-  k_score_final<<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
+  k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
                                                c->d_sst, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");
   HIP_OK(hipGetLastError());

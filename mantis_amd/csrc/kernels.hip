@@ -47,6 +47,15 @@ __device__ inline int wave_incl_scan(int v, int lane) {
   return v;
 }
 
+// Frame pointers come out of FrameDesc records in memory, so the compiler
+// cannot tell they are global and emits flat loads (which also count against
+// lgkmcnt, so every LDS wait waits for them too). Frames always live in
+// device memory: these views make the loads global_load_*.
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+__device__ inline gu8* gbytes(const uint8_t* p) { return (gu8*)p; }
+__device__ inline gu32* gwords(const void* p) { return (gu32*)p; }
+
 // ======================================================== union-find (CCL)
 // Concurrent union by index: roots are component minima, links point to
 // smaller indices only, so finds terminate and stale reads only cost retries.
@@ -122,7 +131,8 @@ __device__ inline int refl101(int i, int n) {  // BORDER_REFLECT_101
   return i;
 }
 
-__device__ inline uint8_t gray_px(const uint8_t* p) {
+template <class P>
+__device__ inline uint8_t gray_px(P p) {
   return (uint8_t)((1868 * p[0] + 9617 * p[1] + 4899 * p[2] + 8192) >> 14);
 }
 // gray_px of the 4 pixels in three dwords (b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3)
@@ -250,18 +260,18 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     const int y = y0 - 3 + ly, xs = x0 - 4 + 4 * lg;
     uint8_t* o = g + ly * FGW + 4 * lg;
     if (IN) {
-      const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
+      gu32* q = gwords(fd.bgr + ((size_t)y * W + xs) * 3);
       *(uint32_t*)o = gray4(q[0], q[1], q[2]);
     } else if (y < 0 || y >= H) {
       o[0] = o[1] = o[2] = o[3] = 0;
     } else if (vec && xs >= 0 && xs + 3 < W) {
-      const uint32_t* q = (const uint32_t*)(fd.bgr + ((size_t)y * W + xs) * 3);
+      gu32* q = gwords(fd.bgr + ((size_t)y * W + xs) * 3);
       *(uint32_t*)o = gray4(q[0], q[1], q[2]);
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int x = xs + k;
-        o[k] = (x >= 0 && x < W) ? gray_px(fd.bgr + ((size_t)y * W + x) * 3) : 0;
+        o[k] = (x >= 0 && x < W) ? gray_px(gbytes(fd.bgr + ((size_t)y * W + x) * 3)) : 0;
       }
     }
   }
@@ -2248,8 +2258,8 @@ struct MaskBits {
 // last pixel of the frame reads one byte early so the load stays in the buffer.
 __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
   const bool last = lin == npx - 1;
-  uint32_t v;
-  __builtin_memcpy(&v, bgr + 3 * lin - (last ? 1 : 0), 4);
+  typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;  // unaligned dword
+  const uint32_t v = *(gu32u*)(bgr + 3 * lin - (last ? 1 : 0));
   return last ? (v >> 8) : v;
 }
 
@@ -2425,6 +2435,11 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
 //   k_score_final  81 shifts, top-20, determineBestYaw, publish gate
 // Block size: 10 waves per frame (50 particles = 5 rounds of waves).
 constexpr int kScoreThreads = 640;
+#ifndef MK_SCORE_TAIL_THREADS
+#define MK_SCORE_TAIL_THREADS 640
+#endif
+constexpr int kScoreTail = MK_SCORE_TAIL_THREADS;  // k_score_init / k_score_final block size (>= 128: 81 shift lanes)
+static_assert(kScoreTail >= 128 && kScoreTail % 64 == 0, "score tail block");
 constexpr int kWaves = kScoreThreads / 64;
 
 struct PoseLds {
@@ -2454,7 +2469,8 @@ __device__ inline Xf rfl(const Xf& T) {
   return u;
 }
 
-__global__ __launch_bounds__(kScoreThreads) void k_score_init(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_score_init(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
     ScoreState* __restrict__ sst) {
@@ -2488,7 +2504,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_init(
   HypRec* Hh = hyps + (size_t)f * kMaxHyps;
   const int C = st[f].n_hyps;
   // evaluateHypotheses(hyps, cleaned)
-  for (int h = wave; h < C; h += kWaves) {
+  for (int h = wave; h < C; h += (NT / 64)) {
     double e;
     int n;
     wave_score_fast(Hh[h].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
@@ -2653,7 +2669,8 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   }
 }
 
-__global__ __launch_bounds__(kScoreThreads) void k_score_final(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_score_final(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
     const ScoreState* __restrict__ sst, double grid_spacing, int grid_size) {
@@ -2669,7 +2686,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
   __shared__ double lm[3 * 768];
   __shared__ PoseLds P[96];
   __shared__ ErrIdx ei[96];
-  __shared__ ColorLds cls[kWaves];
+  __shared__ ColorLds cls[(NT / 64)];
   __shared__ PoseLds cur;
   __shared__ double shv[9];
   __shared__ double yerr[4];
@@ -2696,7 +2713,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
     P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
   }
   __syncthreads();
-  for (int j = wave; j < NS; j += kWaves) {
+  for (int j = wave; j < NS; j += (NT / 64)) {
     double e;
     int n;
     wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
@@ -2759,7 +2776,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_final(
       Y[tid].c2w = h.c2w; Y[tid].w2c = h.w2c; Y[tid].q = h.q;
     }
     __syncthreads();
-    for (int j = wave; j < 20; j += kWaves) {
+    for (int j = wave; j < 20; j += (NT / 64)) {
       double e;
       int n;
       wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
