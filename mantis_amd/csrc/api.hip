@@ -370,14 +370,19 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
   return (unsigned)std::max<size_t>(1, std::min(b, cap));
 }
 
+// paired: pipeline items (orientation pairs of each quad, k_rpp_prep); the
+// first queue holds orientation 0 only and op_end<0> mirrors its result
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
-                       RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads) {
-  k_objpose_q<0><<<objpose_blocks(c, expected_items), 256, 0, c->s>>>(items, rf, jobs0, q, st);
+                       RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads,
+                       bool paired) {
+  const int pr = paired ? 1 : 0;
+  k_objpose_q<0><<<objpose_blocks(c, paired ? expected_items / 2 : expected_items), 256, 0, c->s>>>(items, rf, jobs0,
+                                                                                                    q, st, pr);
   mark(c, "rpp_first");
   k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
-      items, jobs0, jobs1, q);
+      items, jobs0, jobs1, q, pr);
   mark(c, "rpp_2nd");
-  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st);
+  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st, 0);
   mark(c, "rpp_cand");
   k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out, quads,
                                                                quads ? c->cfg.quad_gn_iterations : 0);
@@ -391,7 +396,7 @@ mantis_status run_pose(Ctx* c, int n) {
   const size_t ni = (size_t)n * kMaxQuads * 2;
   mark(c, "rpp_prep");
   launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160,
-                    c->d_quads);
+                    c->d_quads, true);
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
   HIP_OK(hipGetLastError());
@@ -1432,7 +1437,7 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
   mark(c, "start");
   k_rpp_prep_api<<<(n + 255) / 256, 256, 0, c->s>>>(d_ip, d_op, n, d_it, d_j0, d_q);
   mark(c, "rpp_prep");
-  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, nullptr, (size_t)n, (size_t)n, nullptr);
+  launch_rpp_queues(c, d_it, d_rf, d_j0, d_j1, d_q, d_out, nullptr, (size_t)n, (size_t)n, nullptr, false);
   HIP_OK(hipGetLastError());
   std::vector<RppOut> h(n);
   HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));

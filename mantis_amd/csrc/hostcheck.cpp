@@ -34,6 +34,19 @@ int hc_rpp(const double* model, const double* iprts, double* R, double* t, doubl
   return r.status;
 }
 
+// first ObjPose (stage1a): R[9], t[3], obj_err, img_err, iterations, Q after (12)
+void hc_first_objpose(const double* model, const double* iprts, double* R, double* t, double* errs, int32_t* it,
+                      double* Qout) {
+  mk::rpp::Stage1 s;
+  mk::rpp::stage1a(model, iprts, s);
+  std::memcpy(R, s.R, sizeof(s.R));
+  std::memcpy(t, s.t, sizeof(s.t));
+  errs[0] = s.obj_err;
+  errs[1] = s.img_err;
+  *it = s.iterations;
+  std::memcpy(Qout, s.Q, sizeof(s.Q));
+}
+
 // iteration counts of the phases: it[0] first ObjPose, it[1..5] candidate ObjPoses (-1 if absent)
 void hc_rpp_iters(const double* model, const double* iprts, int32_t* it) {
   mk::rpp::Stage1 s;

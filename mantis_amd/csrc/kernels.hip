@@ -1788,7 +1788,9 @@ __global__ __launch_bounds__(256) void k_rpp_prep(const QuadRec* __restrict__ qu
     it.s.Q[8 + k] = 1.0;
   }
   it.active = 1;
-  jobs[atomicAdd(&q->n0, 1)] = (int32_t)slot;
+  // the first ObjPose of orientation 1 is orientation 0's mirrored (op_end<0>):
+  // only orientation 0 items enter the first queue
+  if (o == 0) jobs[atomicAdd(&q->n0, 1)] = (int32_t)slot;
 }
 
 __global__ __launch_bounds__(256) void k_rpp_prep_api(const double* __restrict__ img_pts,
@@ -1837,9 +1839,19 @@ __device__ inline void op_begin(RppItem* items, int32_t job, rpp::OpState& s) {
   }
 }
 
+// Pipeline items come in orientation pairs (k_rpp_prep: slot = 2 quad + o)
+// whose model squares are mirror images in y (sy1 = -sy0, z = 0). The first
+// ObjPose of the pair is then one computation: every quantity it forms is
+// the same for both or changes sign exactly (negation is exact), and the
+// result of orientation 1 is R1 = R0 diag(1, -1, -1) with t, both errors, the
+// iteration count, the stop code and the rewritten image points identical --
+// R1 P1 = R0 P0 since the model's z row is zero. Checked bit for bit on the
+// host build (mk_rpp.h) over the bench scene's quads (tools/rpp_mirror_check.py)
+// and end to end by the GPU parity tests against the oracle, which computes
+// both orientations.
 template <int MODE>
 __device__ inline void op_end(RppItem* items, rpp::Refine* rf, FrameState* st, int32_t job, const rpp::OpState& s,
-                              int code) {
+                              int code, bool paired) {
   if (st) {
     const int32_t p = MODE == 0 ? job : job / rpp::kCand;
     atomicAdd(&st[p / (kMaxQuads * 2)].rpp_iters[MODE], s.it);
@@ -1859,6 +1871,24 @@ __device__ inline void op_end(RppItem* items, rpp::Refine* rf, FrameState* st, i
     o.iterations = s.it;
     o.error = code == 2 ? 2 : 0;
     o.keep_mask = 0;
+    if (paired) {
+      rpp::Stage1& m = items[job + 1].s;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        m.R[3 * r] = R.a[3 * r];
+        m.R[3 * r + 1] = -R.a[3 * r + 1];
+        m.R[3 * r + 2] = -R.a[3 * r + 2];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) m.t[k] = t.a[k];
+#pragma unroll
+      for (int k = 0; k < 12; k++) m.Q[k] = o.Q[k];
+      m.obj_err = oe;
+      m.img_err = ie;
+      m.iterations = s.it;
+      m.error = code == 2 ? 2 : 0;
+      m.keep_mask = 0;
+    }
   } else {
     rpp::Refine& o = rf[job];
 #pragma unroll
@@ -1874,7 +1904,8 @@ __device__ inline void op_end(RppItem* items, rpp::Refine* rf, FrameState* st, i
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
-                                                   const int32_t* __restrict__ jobs, RppQueue* q, FrameState* st) {
+                                                   const int32_t* __restrict__ jobs, RppQueue* q, FrameState* st,
+                                                   int paired) {
   const int lane = threadIdx.x & 63;
   const int32_t njobs = MODE == 0 ? q->n0 : q->n1;
   int32_t* next = MODE == 0 ? &q->next0 : &q->next1;
@@ -1906,7 +1937,7 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
     if (job >= 0) {
       const int code = rpp::op_step(s);
       if (code) {
-        op_end<MODE>(items, rf, st, job, s, code);
+        op_end<MODE>(items, rf, st, job, s, code, paired != 0);
         job = -1;
       }
     }
@@ -1919,10 +1950,10 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
 // needs ~390 registers per lane, so a 64-thread block fits on one SIMD
 // instead of waiting for a whole CU to drain.
 __global__ __launch_bounds__(64) void k_rpp_s1b(RppItem* __restrict__ items, const int32_t* __restrict__ jobs0,
-                                                int32_t* __restrict__ jobs1, RppQueue* q) {
-  const int n0 = q->n0;
+                                                int32_t* __restrict__ jobs1, RppQueue* q, int paired) {
+  const int n0 = q->n0 << (paired ? 1 : 0);  // paired: both orientations of every first-queue job
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n0; k += gridDim.x * blockDim.x) {
-    const int32_t i = jobs0[k];
+    const int32_t i = paired ? jobs0[k >> 1] + (k & 1) : jobs0[k];
     if (!items[i].active) continue;
     double model[12];
 #pragma unroll

@@ -224,3 +224,23 @@ def test_quad_gn_host_build_matches_restatement():
     R, t, steps, c0, c1 = HC.quad_gn(R00, t00, img0, obj0, 20)
     np.testing.assert_allclose(t, tt0, atol=1e-7)
     assert np.all(c1 < 1e-14)
+
+
+def test_first_objpose_orientation_pairs_mirror():
+    """k_objpose_q<0> runs one first ObjPose per quad: the mirrored model
+    orientation's result is R diag(1, -1, -1) with identical t, errors,
+    iterations and image points (host build of mk_rpp.h, bit for bit) -- on
+    the quads of bench-scene frames and on random quads (the full bench set,
+    38,418 quads of 128 rigs, is tools/rpp_mirror_check.py 128)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import rpp_mirror_check as RM
+    import _gn_ref as G
+
+    quads = RM.frame_quads(2)
+    assert len(quads) > 200
+    assert all(RM.mirror_pair_ok(q) for q in quads)
+    img, _, _, _, _, _ = G.quad_problems(np.random.default_rng(4), 300)
+    rnd = [np.vstack([p.T, np.ones(4)]) for p in img]
+    assert all(RM.mirror_pair_ok(q) for q in rnd)
