@@ -745,7 +745,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
   c->plane = (size_t)(c->Wmax + 2) * (c->Hmax + 2);
-  c->bstride = (size_t)((c->Wmax + 31) / 32) * c->Hmax;
+  c->bstride = bits::tiled_words(c->Wmax, c->Hmax);  // >= row-major words; the mask plane is tiled
   c->dstride = (size_t)dbits_wpw(c->Wmax + 2) * (c->Hmax + 2);
   c->pool_cap = cfg.max_contour_points;
   {
@@ -1321,7 +1321,7 @@ mantis_status mantis_masks(void* ctx, const mantis_image* img, uint8_t* det_out,
     HIP_OK(hipMemcpy2DAsync(det_out, W, c->d_det + (W + 2) + 1, W + 2, W, H, hipMemcpyDeviceToHost, c->s));
   }
   if (mask_out) {
-    k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_mbits, c->d_mask, W, H, 0);
+    k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_mbits, c->d_mask, W, H, -1);
     HIP_OK(hipMemcpyAsync(mask_out, c->d_mask, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
   }
   HIP_OK(hipStreamSynchronize(c->s));

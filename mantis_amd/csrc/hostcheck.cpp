@@ -47,6 +47,29 @@ void hc_first_objpose(const double* model, const double* iprts, double* R, doubl
   std::memcpy(Qout, s.Q, sizeof(s.Q));
 }
 
+// stage1 (first ObjPose + Get2ndPose setup): candidate initial rotations sR (kCand x 9), keep mask, error;
+// refine each kept candidate: R (kCand x 9), t (kCand x 3), errs (kCand x 2), iterations (kCand)
+int hc_stage1_cands(const double* model, const double* iprts, double* sR, double* R, double* t, double* errs,
+                    int32_t* its, int32_t* error) {
+  mk::rpp::Stage1 s;
+  mk::rpp::stage1(model, iprts, s);
+  *error = s.error;
+  std::memcpy(sR, s.sR, sizeof(s.sR));
+  for (int j = 0; j < mk::rpp::kCand; j++) {
+    its[j] = -1;
+    if (s.error != 1 && ((s.keep_mask >> j) & 1)) {
+      mk::rpp::Refine r;
+      mk::rpp::refine(model, s.Q, s.sR[j], r);
+      std::memcpy(R + 9 * j, r.R, sizeof(r.R));
+      std::memcpy(t + 3 * j, r.t, sizeof(r.t));
+      errs[2 * j] = r.obj_err;
+      errs[2 * j + 1] = r.img_err;
+      its[j] = r.iterations;
+    }
+  }
+  return s.keep_mask;
+}
+
 // iteration counts of the phases: it[0] first ObjPose, it[1..5] candidate ObjPoses (-1 if absent)
 void hc_rpp_iters(const double* model, const double* iprts, int32_t* it) {
   mk::rpp::Stage1 s;

@@ -887,19 +887,28 @@ __global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, 
   m = m.shrink(5, H);
   mb_hv<5, false>(A, B, m, y0, WW, W, H, L);
   __syncthreads();
-  // final erode(3) straight to the mask plane: output rows [yb, ye)
+  // final erode(3): output rows [yb, ye) -> A, then to the tiled mask plane
+  // (bits::tiled_word), lanes down a word column so the stores stay contiguous
+  mb_hv<3, false>(B, A, RowRange{yb, ye}, y0, WW, W, H, L);
+  __syncthreads();
   uint32_t* M = mbits + (size_t)f * bstride;
-  mb_hv<3, false>(B, M + (ptrdiff_t)y0 * WW, RowRange{yb, ye}, y0, WW, W, H, L);
+  const int nr = ye - yb;
+  for (int k = t; k < nr * WW; k += nt) {
+    const int w = k / nr, y = yb + (k - w * nr);
+    M[bits::tiled_word(y, w, WW)] = A[(y - y0) * WW + w];
+  }
 }
 
 // debug bytes (frame 0): a W x H bit plane (wpw = 0: ceil(W/32) words per
-// row) or the padded detector plane (wpw = its words per row) -> one byte per pixel
+// row; wpw = -1: the tiled mask plane) or the padded detector plane (wpw = its
+// words per row) -> one byte per pixel
 __global__ __launch_bounds__(256) void k_bits_to_bytes(const uint32_t* __restrict__ src, uint8_t* __restrict__ out,
                                                        int W, int H, int wpw) {
-  const int WW = wpw ? wpw : bits::words(W);
+  const int WW = wpw > 0 ? wpw : bits::words(W);
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < W * H; k += gridDim.x * blockDim.x) {
     const int y = k / W, x = k - y * W;
-    out[k] = (uint8_t)((src[(size_t)y * WW + (x >> 5)] >> (x & 31)) & 1u);
+    const size_t i = wpw < 0 ? bits::tiled_word(y, x >> 5, WW) : (size_t)y * WW + (x >> 5);
+    out[k] = (uint8_t)((src[i] >> (x & 31)) & 1u);
   }
 }
 
@@ -2282,7 +2291,7 @@ struct MaskBytes {
 struct MaskBits {
   const uint32_t* m;
   int WW, W;
-  __device__ uint32_t word(long, int x, int y) const { return m[(size_t)y * WW + (x >> 5)]; }
+  __device__ uint32_t word(long, int x, int y) const { return m[bits::tiled_word(y, x >> 5, WW)]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 // B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
@@ -2303,6 +2312,12 @@ __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
 // HypothesisEvaluation.h:218-227 on the cleaned image): the squared distance
 // of its BGR to white, or 3 * 255^2 when the pixel is masked out or lies past
 // the end of the buffer (linear-offset read of cvRound(px) == W / == H).
+#ifndef MK_FAST_PROJ
+#define MK_FAST_PROJ 1
+#endif
+#ifndef MK_LAZY_BGR
+#define MK_LAZY_BGR 1
+#endif
 #ifndef MK_FAST_UNROLL
 #define MK_FAST_UNROLL 3
 #endif
@@ -2320,17 +2335,40 @@ __device__ inline void wave_sums_fast(const Xf& c2w, const double* lm, int lb, i
     long lin[kFastUnroll];
     int px[kFastUnroll], py[kFastUnroll];
     bool in[kFastUnroll], ok[kFastUnroll];
-    // branch-free projections (z <= 0 or an off-frame point just fails the
-    // flags), so the kFastUnroll independent FP64 chains interleave
+    double pu[kFastUnroll], pv_[kFastUnroll];
+    bool zp[kFastUnroll];
+    // branch-free filtered projections (z <= 0 or an off-frame point just
+    // fails the flags), so the kFastUnroll independent FP64 chains
+    // interleave; the rare uncertain ones are redone exactly below
+    bool sure = true;
 #pragma unroll
     for (int k = 0; k < kFastUnroll; k++) {
       const int l = l0 + 64 * k;
       const double* X = lm + 3 * (l < nl ? l : nl - 1);  // nl > lb: a valid landmark
       double rp[3];
       xf_apply(c2w, X, rp);
-      double u, v;
-      distort(cm, rp[0], rp[1], rp[2], &u, &v);
-      in[k] = l < nl && rp[2] > 0 && in_frame(u, v, H, W);
+      zp[k] = rp[2] > 0;
+#if MK_FAST_PROJ
+      sure &= distort_fast(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k], W, H) || !zp[k];
+#else
+      distort(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k]);
+#endif
+    }
+    if (!__all(sure)) {
+#pragma unroll 1
+      for (int k = 0; k < kFastUnroll; k++) {
+        const int l = l0 + 64 * k;
+        if (!zp[k]) continue;
+        double rp[3];
+        xf_apply(c2w, lm + 3 * (l < nl ? l : nl - 1), rp);
+        distort(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) {
+      const int l = l0 + 64 * k;
+      const double u = pu[k], v = pv_[k];
+      in[k] = l < nl && zp[k] && in_frame(u, v, H, W);
       int x = in[k] ? cv_round(u) : 0, y = in[k] ? cv_round(v) : 0;
       long li = (long)y * W + x;
       ok[k] = in[k] && li >= 0 && li < npx;
@@ -2343,14 +2381,27 @@ __device__ inline void wave_sums_fast(const Xf& c2w, const double* lm, int lb, i
     uint32_t mw[kFastUnroll], pv[kFastUnroll];
 #pragma unroll
     for (int k = 0; k < kFastUnroll; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+#if MK_LAZY_BGR
+    bool hit[kFastUnroll];
+#pragma unroll
+    for (int k = 0; k < kFastUnroll; k++) {
+      hit[k] = ok[k] && mask.test(mw[k], px[k]);
+      pv[k] = hit[k] ? load_bgr(bgr, lin[k], npx) : 0u;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < kFastUnroll; k++) pv[k] = load_bgr(bgr, lin[k], npx);
+#endif
 #pragma unroll
     for (int k = 0; k < kFastUnroll; k++) {
       if (!in[k]) continue;
       n++;
       int e = 3 * 255 * 255;
+#if MK_LAZY_BGR
+      if (hit[k]) {
+#else
       if (ok[k] && mask.test(mw[k], px[k])) {
+#endif
         const int b = (int)(pv[k] & 0xffu), g = (int)((pv[k] >> 8) & 0xffu), r = (int)((pv[k] >> 16) & 0xffu);
         const int e0 = b - 255, e1 = g - 255, e2 = r - 255;
         e = e0 * e0 + e1 * e1 + e2 * e2;
@@ -2465,7 +2516,13 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
 //   k_score_pf     optimizeHypothesisWithParticleFilter (10 x 50)
 //   k_score_final  81 shifts, top-20, determineBestYaw, publish gate
 // Block size: 10 waves per frame (50 particles = 5 rounds of waves).
-constexpr int kScoreThreads = 640;
+#ifndef MK_SCORE_THREADS
+#define MK_SCORE_THREADS 640
+#endif
+constexpr int kScoreThreads = MK_SCORE_THREADS;
+#ifndef MK_PF_WPE
+#define MK_PF_WPE 0
+#endif
 #ifndef MK_SCORE_TAIL_THREADS
 #define MK_SCORE_TAIL_THREADS 640
 #endif
@@ -2601,7 +2658,7 @@ __global__ __launch_bounds__(NT) void k_score_init(
 // roll, z, y, x; best = first strict minimum (argmin by (error, index) over
 // the 50, taken only when strictly below the current error).
 template <int NT, int SPLIT>
-__global__ __launch_bounds__(NT) void k_score_pf(
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MK_PF_WPE > 0 && SPLIT == 1 ? MK_PF_WPE : 1))) void k_score_pf(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
     FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations) {

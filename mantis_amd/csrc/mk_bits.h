@@ -16,6 +16,12 @@ namespace mk {
 namespace bits {
 
 MK_HD int words(int W) { return (W + 31) >> 5; }
+// Tiled mask plane (the scorers' cleanImageByEdge mask): word (y, w) -- 32
+// pixels of row y -- at ((y / 32) * WW + w) * 32 + y % 32, so one 128-byte
+// line holds a 32 x 32 pixel tile and a pixel neighbourhood touches a few
+// lines instead of one line per row. Rows padded to a multiple of 32.
+MK_HD size_t tiled_word(int y, int w, int WW) { return ((size_t)(y >> 5) * WW + w) * 32 + (y & 31); }
+MK_HD size_t tiled_words(int W, int H) { return (size_t)words(W) * (((size_t)H + 31) & ~(size_t)31); }
 
 // mask of the valid pixels of word w
 MK_HD uint32_t valid(int w, int W) {

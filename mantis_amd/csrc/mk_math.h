@@ -189,6 +189,48 @@ MK_HD void distort(const Cam& cm, double X, double Y, double Z, double* u, doubl
   *u = xd3 * cm.fx + cm.cx;
   *v = xd1 * cm.fy + cm.cy;
 }
+#ifdef __HIPCC__
+// Filtered fisheye projection for the fast scorers. The scorers consume the
+// projection only through decisions: in_frame (thresholds 0, cols, 0, rows)
+// and cvRound (ties at k + 1/2). This version replaces the three IEEE
+// divisions and the IEEE square root of distort() by the hardware reciprocal
+// / reciprocal square root with Newton steps (same operation order
+// otherwise); its pixel coordinates differ from distort()'s by ~2e-12 px
+// (worst over 2^26 projections: tools/check_proj.hip). It returns whether
+// every decision is certain -- a coordinate farther than kProjCert = 1e-7 px
+// outside the frame, or both farther than that from the frame edges and
+// from the rounding ties -- and the caller recomputes with distort()
+// otherwise (~1 landmark in 3 million). r2 >= 1e200 (overflow: distort()
+// then takes cdist = theta_d / inf = 0) and NaN are never certain.
+constexpr double kProjCert = 1e-7;
+__device__ inline bool proj_in_certain(double a, int lim) {
+  const double f = a - floor(a);
+  return a > kProjCert && a < (double)lim - kProjCert && fabs(f - 0.5) > kProjCert;
+}
+__device__ inline bool proj_out_certain(double a, int lim) { return a < -kProjCert || a > (double)lim + kProjCert; }
+__device__ inline bool distort_fast(const Cam& cm, double X, double Y, double Z, double* u, double* v, int W, int H) {
+  double rz = __builtin_amdgcn_rcp(Z);
+  double e = __builtin_fma(-Z, rz, 1.0);
+  rz = __builtin_fma(rz, e, rz);
+  e = __builtin_fma(-Z, rz, 1.0);
+  rz = __builtin_fma(rz, e, rz);
+  const double x = X * rz, y = Y * rz;
+  const double r2 = x * x + y * y;
+  double rs = __builtin_amdgcn_rsq(r2);
+  rs = rs * __builtin_fma(-0.5 * r2, rs * rs, 1.5);
+  const double r = r2 * rs;
+  const double theta = dm::atan_pos(r, rs);
+  const double theta2 = theta * theta, theta3 = theta2 * theta, theta4 = theta2 * theta2, theta5 = theta4 * theta,
+               theta6 = theta3 * theta3, theta7 = theta6 * theta, theta8 = theta4 * theta4, theta9 = theta8 * theta;
+  const double theta_d = theta + cm.k[0] * theta3 + cm.k[1] * theta5 + cm.k[2] * theta7 + cm.k[3] * theta9;
+  const double cdist = r > 1e-8 ? theta_d * rs : 1;
+  const double uu = (x * cdist) * cm.fx + cm.cx, vv = (y * cdist) * cm.fy + cm.cy;
+  *u = uu;
+  *v = vv;
+  return r2 < 1e200 &&
+         (proj_out_certain(uu, W) || proj_out_certain(vv, H) || (proj_in_certain(uu, W) && proj_in_certain(vv, H)));
+}
+#endif
 // cv::fisheye::undistortPoints, no R/P (normalized output), 10 iterations,
 // theta_d clamped to [-pi/2, pi/2] (OpenCV 3.3 form)
 MK_HD void undistort(const Cam& cm, double px, double py, double* ox, double* oy) {
