@@ -2313,7 +2313,7 @@ __device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
 // of its BGR to white, or 3 * 255^2 when the pixel is masked out or lies past
 // the end of the buffer (linear-offset read of cvRound(px) == W / == H).
 #ifndef MK_FAST_PROJ
-#define MK_FAST_PROJ 1
+#define MK_FAST_PROJ 0
 #endif
 #ifndef MK_LAZY_BGR
 #define MK_LAZY_BGR 1

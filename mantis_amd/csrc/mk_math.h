@@ -202,6 +202,9 @@ MK_HD void distort(const Cam& cm, double X, double Y, double Z, double* u, doubl
 // from the rounding ties -- and the caller recomputes with distort()
 // otherwise (~1 landmark in 3 million). r2 >= 1e200 (overflow: distort()
 // then takes cdist = theta_d / inf = 0) and NaN are never certain.
+// Measured in the PF scorer: 24.4 ms against 23.0 with distort() (the
+// scorer waits on its gathers, not its FP64 pipe), so it is off by default
+// (kernels.hip MK_FAST_PROJ) and kept, with its checker, for that A/B.
 constexpr double kProjCert = 1e-7;
 __device__ inline bool proj_in_certain(double a, int lim) {
   const double f = a - floor(a);
