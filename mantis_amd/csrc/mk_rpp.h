@@ -549,6 +549,9 @@ MK_HD void jacobi_sweeps(double* At, double* W, double* Vt) {
     for (int i = 0; i < N - 1; i++)
 #pragma unroll
       for (int j = i + 1; j < N; j++) changed |= jacobi_pair<M, N>(At, W, Vt, i, j);
+#ifdef MK_JACOBI_COUNT
+    MK_JACOBI_COUNT(M, N, iter, changed);
+#endif
     if (!changed) break;
   }
 }
@@ -876,7 +879,11 @@ typedef Mt<3, 3> M33;
 typedef Mt<3, 1> M31;
 
 // AbsKernel (RPP.cpp:229-332): overwrites P (re-centred) and Q (F_i q_i) in place
+#ifndef MK_OP_STAMP
+#define MK_OP_STAMP(k)
+#endif
 MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t, M34& Qout, double& err2) {
+  MK_OP_STAMP(0);
 #pragma unroll
   for (int i = 0; i < NP; i++) {
     M31 q = mm(F[i], col(Q, i));
@@ -896,7 +903,9 @@ MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t
 #pragma unroll
       for (int b = 0; b < 3; b++) M(a, b) += P(a, i) * Q(b, i);
   M33 U, V;
+  MK_OP_STAMP(1);
   svd3(M, U, V);
+  MK_OP_STAMP(2);
   M33 Ut = tr(U);
   // ref: RPP.cpp:296-318. det(V U^T) > 0: try R = V U^T, and if t_z < 0
   // flip V's 3rd column and take R = -(V U^T). Otherwise flip first, take
@@ -933,6 +942,7 @@ MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t
     }
     err2 += sqnorm3(mm(sub(I, F[i]), qo));
   }
+  MK_OP_STAMP(3);
 }
 
 // ObjPose (RPP.cpp:66-208) as a resumable state machine: op_setup (everything

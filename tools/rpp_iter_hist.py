@@ -1,7 +1,8 @@
 """Diagnostic: ObjPose iteration counts per RPP job on the bench scene
 (host build of mk_rpp.h via tests/_hostcheck.py; quads/test points from the
 oracle). Prints the distribution of first-ObjPose and candidate iterations
-and the longest jobs, i.e. the serial tail of the persistent queues."""
+and the longest jobs, i.e. the serial tail of the persistent queues, and
+writes the 16 longest first-ObjPose problems to tools/objpose_long.bin."""
 import os
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -49,7 +50,7 @@ def one(j):
             HC.lib().hc_rpp_iters(model.ctypes.data_as(C.POINTER(C.c_double)),
                                   np.ascontiguousarray(ip).ctypes.data_as(C.POINTER(C.c_double)),
                                   it.ctypes.data_as(C.POINTER(C.c_int32)))
-            out.append((i, q, o, it.copy()))
+            out.append((i, q, o, it.copy(), np.concatenate([model.ravel(), ip.ravel()])))
     return out
 
 
@@ -64,3 +65,7 @@ for name, a in (("first", first), ("cand", cand)):
 worst = sorted(res, key=lambda x: -x[3].max())[:8]
 for w in worst:
     print("frame", w[0], "quad", w[1], "orient", w[2], "iters", list(w[3]))
+# the longest first-ObjPose problems (model 3x4 then image points 3x4, row-major
+# float64) for tools/objpose_lat.hip
+longest = sorted(res, key=lambda x: -x[3][0])[:16]
+np.stack([x[4] for x in longest]).astype(np.float64).tofile(os.path.join(ROOT, "tools", "objpose_long.bin"))
