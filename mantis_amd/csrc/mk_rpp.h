@@ -438,58 +438,60 @@ MK_HD int rpoly(const double* op, int degree, double* zeror, double* zeroi) {
 // N x N.
 
 // One rotation of rows (i, j) with its skip test; returns whether it rotated.
+// The reference's control flow is: skip if |p| <= eps sqrt(a b); else gamma =
+// hypot(2p, a - b) and the sign of beta = a - b picks which of c, s comes from
+// the square root. Here that is evaluated branch-free in one basic block --
+// the skip test's square root beside the rotation's chain, the beta branch as
+// selects of the operands -- so the in-order wave never stalls on the skip
+// test (the long ObjPose chains rotate in ~all 9 pair visits of their 3
+// sweeps; skips are < 0.1 %). Every value is computed by the reference's
+// operations on the reference's operands, so the results are identical. When
+// |2p| <= 2^-60 |beta|, hypot(2p, beta) == |beta| exactly and both square
+// roots are of 1, which the general formula reproduces.
 template <int M, int N>
 MK_HD bool jacobi_pair(double* At, double* W, double* Vt, int i, int j) {
   const double eps = DBL_EPSILON * 10;
   double a = W[i], p = 0, b = W[j];
 #pragma unroll
   for (int k = 0; k < M; k++) p += At[i * M + k] * At[j * M + k];
-  if (fabs(p) <= eps * sqrt(a * b)) return false;
+#ifndef MK_JACOBI_KIND
+#define MK_JACOBI_KIND(k)
+#endif
+  const bool skip = fabs(p) <= eps * sqrt(a * b);
   p *= 2;
-  double beta = a - b, gamma, c, s;
-  if (fabs(p) <= fabs(beta) * 0x1p-60) {
-    // hypot(p, beta) == |beta| exactly here (|p| is below half an ulp of
-    // |beta|), so the reference's sqrt of (2|beta| / 2|beta|) is exactly 1
-    // and one division is left. This is the common case once a row has
-    // decayed to rounding noise: a planar model makes M rank 2, and the
-    // reference keeps rotating that row until it underflows (~20 sweeps).
-    gamma = fabs(beta);
-    if (beta < 0) {
-      s = 1.0;
-      c = p / (gamma * s * 2);
-    } else {
-      c = 1.0;
-      s = p / (gamma * c * 2);
-    }
-  } else {
-    gamma = hypot(p, beta);
-    if (beta < 0) {
-      double delta = (gamma - beta) * 0.5;
-      s = sqrt(delta / gamma);
-      c = p / (gamma * s * 2);
-    } else {
-      c = sqrt((gamma + beta) / (gamma * 2));
-      s = p / (gamma * c * 2);
-    }
-  }
-  a = b = 0;
+  const double beta = a - b;
+  const double gamma = hypot(p, beta);
+  const bool neg = beta < 0;
+  // beta < 0: s = sqrt(((gamma - beta) * 0.5) / gamma), c = p / (gamma * s * 2)
+  // else:     c = sqrt((gamma + beta) / (gamma * 2)),   s = p / (gamma * c * 2)
+  const double num = neg ? (gamma - beta) * 0.5 : gamma + beta;
+  const double den = neg ? gamma : gamma * 2;
+  const double r = sqrt(num / den);
+  const double o = p / (gamma * r * 2);
+  const double c = neg ? o : r, s = neg ? r : o;
+  // commit by selects (a branch here would let the compiler sink the rotation
+  // behind the skip test again)
+  double na = 0, nb = 0;
 #pragma unroll
   for (int k = 0; k < M; k++) {
-    double t0 = c * At[i * M + k] + s * At[j * M + k];
-    double t1 = -s * At[i * M + k] + c * At[j * M + k];
-    At[i * M + k] = t0; At[j * M + k] = t1;
-    a += t0 * t0; b += t1 * t1;
+    const double x = At[i * M + k], y = At[j * M + k];
+    const double t0 = c * x + s * y;
+    const double t1 = -s * x + c * y;
+    At[i * M + k] = skip ? x : t0; At[j * M + k] = skip ? y : t1;
+    na += t0 * t0; nb += t1 * t1;
   }
-  W[i] = a; W[j] = b;
+  W[i] = skip ? a : na; W[j] = skip ? b : nb;
   if (Vt) {
 #pragma unroll
     for (int k = 0; k < N; k++) {
-      double t0 = c * Vt[i * N + k] + s * Vt[j * N + k];
-      double t1 = -s * Vt[i * N + k] + c * Vt[j * N + k];
-      Vt[i * N + k] = t0; Vt[j * N + k] = t1;
+      const double x = Vt[i * N + k], y = Vt[j * N + k];
+      const double t0 = c * x + s * y;
+      const double t1 = -s * x + c * y;
+      Vt[i * N + k] = skip ? x : t0; Vt[j * N + k] = skip ? y : t1;
     }
   }
-  return true;
+  MK_JACOBI_KIND(skip ? 0 : 2);
+  return !skip;
 }
 
 // Noise-phase fast-forward for a 3x3 At whose third components are exactly
@@ -509,26 +511,28 @@ MK_HD bool jacobi_pair(double* At, double* W, double* Vt, int i, int j) {
 //   underflow:         n0 (1e-14)^(sweeps left - 1) < 1e-163.
 // The only bits it does not reproduce are signs of the zero third
 // components of rows 0/1 (+-0 + +-0), which no later result depends on.
+// Evaluated without branches or square roots (all conditions are sufficient
+// forms; a doubtful case only declines the fast-forward):
+//   skip test of (0, 1): p^2 <= eps^2 W0 W1 (1 - 1e-10), W0 W1 in [1e-200, 1e200];
+//   underflow: 1.5 n0 < 2^(ilogb(n0) + 2), so (ilogb(n0) + 2) log10(2) <
+//   14 (sweeps left - 1) - 163 with log10(2) rounded toward the safe side.
 MK_HD bool jacobi_noise_ff(const double* At, const double* W, const double* Vt, int sweeps_left) {
-  if (!(At[2] == 0 && At[5] == 0 && At[8] == 0)) return false;
   const double eps = DBL_EPSILON * 10;
   double p = 0;
 #pragma unroll
   for (int k = 0; k < 3; k++) p += At[k] * At[3 + k];  // jacobi_pair's skip test of (0, 1)
-  if (!(fabs(p) <= eps * sqrt(W[0] * W[1]))) return false;
+  const double x = W[0] * W[1];
+  const bool skip01 = x >= 1e-200 && x <= 1e200 && p * p <= (eps * eps) * x * (1 - 1e-10);
   const double n0 = fmax(fabs(At[6]), fabs(At[7]));
   const double bmin = fmin(fmin(fabs(At[0]), fabs(At[1])), fmin(fabs(At[3]), fabs(At[4])));
   const double Bn = fmin(fmax(fabs(At[0]), fabs(At[1])), fmax(fabs(At[3]), fabs(At[4])));
   double vmin = fabs(Vt[0]);
 #pragma unroll
   for (int k = 1; k < 9; k++) vmin = fmin(vmin, fabs(Vt[k]));
-  if (!(n0 <= 0x1p-64 * Bn)) return false;
-  if (!(4.5 * n0 * n0 < 0x1p-55 * bmin * Bn)) return false;
-  if (!(3.0 * n0 < 0x1p-55 * vmin * Bn)) return false;
-  double bound = 1.5 * n0;
-#pragma unroll 1
-  for (int r = 1; r < sweeps_left && bound >= 1e-163; r++) bound *= 1e-14;
-  return bound < 1e-163;
+  const double e2 = n0 > 0 ? (double)(ilogb(n0) + 2) : -2000.0;
+  const bool under = (e2 < 0 ? e2 * 0.30102 : e2 * 0.30104) < 14.0 * (sweeps_left - 1) - 163.01;
+  return At[2] == 0 && At[5] == 0 && At[8] == 0 && skip01 && n0 <= 0x1p-64 * Bn &&
+         4.5 * n0 * n0 < 0x1p-55 * bmin * Bn && 3.0 * n0 < 0x1p-55 * vmin * Bn && under;
 }
 
 #ifndef MK_JACOBI_FF
