@@ -2804,7 +2804,12 @@ __global__ __launch_bounds__(NT) void k_score_final(
   for (int j = wave; j < NS; j += (NT / 64)) {
     double e;
     int n;
+#ifdef MK_DIAG_NO_SHIFTS  // timing diagnostic only: wrong results
+    e = 1.0 + j;
+    n = 1;
+#else
     wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+#endif
     if (lane == 0) { P[j].err = e; ei[j].e = e; ei[j].i = j; D.shift_err[j] = e; }
   }
   __syncthreads();
@@ -2867,7 +2872,12 @@ __global__ __launch_bounds__(NT) void k_score_final(
     for (int j = wave; j < 20; j += (NT / 64)) {
       double e;
       int n;
+#ifdef MK_DIAG_NO_COLOR  // timing diagnostic only: wrong results
+      e = 1.0 + j;
+      n = 1;
+#else
       wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
+#endif
       if (lane == 0) yset_err[j] = e;
     }
     __syncthreads();

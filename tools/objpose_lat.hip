@@ -35,7 +35,7 @@ struct Res {
   int it, code;
 };
 
-__global__ void k_lat(const double* pr, Res* out) {
+__global__ __launch_bounds__(64) void k_lat(const double* pr, Res* out) {
   if (threadIdx.x != 0) return;
   const double* p = pr + 24 * blockIdx.x;
   M34 P, Q;
