@@ -2441,7 +2441,39 @@ __device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, 
 struct ColorLds {
   double u[64], v[64];
   int32_t acc[64], ok[64];
+  int32_t x0[64], run[64];  // cvRound(u - 5); whether the 10 columns are x0 .. x0 + 9
 };
+// Window-row sum of the COLOR error over the 10 pixels lin0 .. lin0 + 9 (the
+// common case: the columns cvRound(u - 5 + k) are x0 + k, and the row lies
+// inside the buffer with 36 bytes to spare): two 16-byte loads and one dword
+// of the 30 bytes from the dword-aligned start, realigned with v_alignbyte,
+// instead of ten unaligned pixel loads. Same pixels, same integer sum.
+__device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
+  const long b = 3 * lin0;
+  const uint32_t m = (uint32_t)(b & 3);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1), aligned(4))) const u32x4 gu4a;
+  const uint8_t* a = bgr + (b - m);
+  const u32x4 q0 = *(gu4a*)a, q1 = *(gu4a*)(a + 16);
+  const uint32_t d8 = *(gu32*)(a + 32);
+  const uint32_t d[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, d8};
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], m);
+  int rs = 0;
+#pragma unroll
+  for (int k = 0; k < 10; k++) {
+    int c[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+      const int o = 3 * k + ch;  // byte of the realigned stream
+      c[ch] = (int)((w[o >> 2] >> (8 * (o & 3))) & 0xffu);
+    }
+    const int e0 = c[0] - 50, e1 = c[1] - 255, e2 = c[2] - 85;
+    rs += e0 * e0 + e1 * e1 + e2 * e2;
+  }
+  return rs;
+}
 __device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
                                         const uint8_t* bgr, int W, int H, ColorLds* cl, double* err_out,
                                         int* n_out) {
@@ -2461,10 +2493,16 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
         distort(cm, rp[0], rp[1], rp[2], &u, &v);
         ok = rp[2] > 0 && in_frame(u, v, H, W);
       }
+      const int x0 = cv_round(u + (-5.0 + 0.0));
+      int run = 1;
+#pragma unroll
+      for (int ox = 1; ox < 10; ox++) run &= cv_round(u + (-5.0 + (double)ox)) == x0 + ox;
       cl->u[lane] = u;
       cl->v[lane] = v;
       cl->ok[lane] = ok;
       cl->acc[lane] = 0;
+      cl->x0[lane] = x0;
+      cl->run[lane] = run;
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
@@ -2473,6 +2511,11 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
       if (!cl->ok[li]) continue;
       const double u = cl->u[li];
       const int y = cv_round(cl->v[li] + (-5.0 + (double)r));
+      const long lin0 = (long)y * W + cl->x0[li];
+      if (cl->run[li] && lin0 >= 0 && lin0 + 12 <= npx) {
+        atomicAdd(&cl->acc[li], color_row_run(bgr, lin0));
+        continue;
+      }
       int rs = 0;
 #pragma unroll
       for (int ox = 0; ox < 10; ox++) {
