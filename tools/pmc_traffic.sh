@@ -33,12 +33,15 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         per[f"{stage}_{c}_bytes_per_frame"] = round(tot)
 out.update(per)
 # calibration (tools/pmc_calib.hip, profiles/r02_pmc_calib.txt): FETCH_SIZE reports 1/2 of the bytes of
-# 12- and 16-byte-per-lane reads; k_canny's 4-byte-per-lane tile-row stores report 2x their bytes
-out["canny_nms_hbm_bytes_per_frame"] = 2 * per["canny_nms_FETCH_SIZE_bytes_per_frame"] + per["canny_nms_WRITE_SIZE_bytes_per_frame"] // 2
+# 12- and 16-byte-per-lane reads. The 2x WRITE_SIZE of 16-byte tile-row stores measured there came from
+# neighbouring tiles' partial sectors written back by different XCDs' L2s; with the XCD-aware tile order
+# the neighbours share an L2 and WRITE_SIZE equals the bit-plane bytes (2 x W H / 8), so it is taken as is.
+out["canny_nms_hbm_bytes_per_frame"] = 2 * per["canny_nms_FETCH_SIZE_bytes_per_frame"] + per["canny_nms_WRITE_SIZE_bytes_per_frame"]
 out["hysteresis_hbm_bytes_per_frame"] = 2 * per["hysteresis_FETCH_SIZE_bytes_per_frame"] + per["hysteresis_WRITE_SIZE_bytes_per_frame"]
 out["hbm_bytes_per_frame"] = out["canny_nms_hbm_bytes_per_frame"]
-out["note"] = ("per 1280x720 frame; k_canny: FETCH_SIZE x 2 + WRITE_SIZE / 2 (both factors calibrated on its access "
-               "widths, tools/pmc_calib.hip); hysteresis: FETCH_SIZE x 2 + WRITE_SIZE (its store widths uncalibrated)")
+out["note"] = ("per 1280x720 frame; k_canny: FETCH_SIZE x 2 (calibrated on its 12-byte reads, tools/pmc_calib.hip) "
+               "+ WRITE_SIZE (= the 2 x W H / 8 bit-plane bytes); hysteresis: FETCH_SIZE x 2 + WRITE_SIZE "
+               "(its access widths uncalibrated); algorithmic k_canny bytes: 3 W H + W H / 4 = 2,995,200")
 json.dump(out, open(f"{sys.argv[1]}/pmc_traffic.json", "w"), indent=1)
 print(json.dumps(out))
 P
