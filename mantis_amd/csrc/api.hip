@@ -134,6 +134,7 @@ struct Ctx {
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
   uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
+  size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
   size_t tstride = 0;
@@ -458,13 +459,25 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
                                               c->d_dbg, c->d_sst);
   // small batches (latency): 16 waves per frame, two per particle over halves
   // of the landmarks; large batches: 10 waves, one per particle
-  if (n <= c->trace_lds_frames)
-    k_score_pf<1024, 2><<<n, 1024, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res,
-                                              c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
-  else
-    k_score_pf<kScoreThreads, 1><<<n, kScoreThreads, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st,
-                                                                c->d_gauss, c->d_res, c->d_dbg, c->d_sst,
-                                                                c->cfg.particles, c->cfg.iterations);
+  // the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0: 720p yes, 1080p no)
+  const size_t ml = c->pf_mask_lds;
+  if (n <= c->trace_lds_frames) {
+    if (ml)
+      k_score_pf<1024, 2, true><<<n, 1024, ml, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss,
+                                                      c->d_res, c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
+    else
+      k_score_pf<1024, 2, false><<<n, 1024, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss,
+                                                       c->d_res, c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
+  } else {
+    if (ml)
+      k_score_pf<kScoreThreads, 1, true><<<n, kScoreThreads, ml, c->s>>>(
+          c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
+          c->cfg.iterations);
+    else
+      k_score_pf<kScoreThreads, 1, false><<<n, kScoreThreads, 0, c->s>>>(
+          c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
+          c->cfg.iterations);
+  }
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
                                                c->d_sst, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");
@@ -755,6 +768,22 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
                                           (int)c->trace_lds_max) == hipSuccess;
     const char* e = getenv("MANTIS_TRACE_LDS_FRAMES");
     c->trace_lds_frames = e ? atoi(e) : c->n_cu / 4;
+  }
+  {
+    // LDS-staged mask for the particle filter: the tiled plane of a max-size
+    // frame beside the kernels' static LDS (both block sizes must take it)
+    const size_t ml = bits::tiled_words(c->Wmax, c->Hmax) * 4;
+    hipFuncAttributes a1, a2;
+    c->pf_mask_lds = 0;
+    if (!getenv("MANTIS_PF_MASK_GLOBAL") &&
+        hipFuncGetAttributes(&a1, (const void*)k_score_pf<kScoreThreads, 1, true>) == hipSuccess &&
+        hipFuncGetAttributes(&a2, (const void*)k_score_pf<1024, 2, true>) == hipSuccess &&
+        std::max(a1.sharedSizeBytes, a2.sharedSizeBytes) + ml <= 160 * 1024 &&
+        hipFuncSetAttribute((const void*)k_score_pf<kScoreThreads, 1, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess &&
+        hipFuncSetAttribute((const void*)k_score_pf<1024, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)ml) == hipSuccess)
+      c->pf_mask_lds = ml;
   }
   if (morph_lds(c->Wmax) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize, (int)morph_lds(c->Wmax)) !=

@@ -2288,6 +2288,16 @@ struct MaskBytes {
   __device__ uint32_t word(long lin, int, int) const { return m[lin]; }
   __device__ bool test(uint32_t w, int) const { return w != 0; }
 };
+// the frame's tiled mask plane staged in LDS (k_score_pf, when it fits
+// beside the kernel's static LDS: a 720p plane is 115 KB): ds_read lookups
+// instead of mask-word gathers through the L1
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+struct MaskLds {
+  lds_cu32* m;
+  int WW;
+  __device__ uint32_t word(long, int x, int y) const { return m[bits::tiled_word(y, x >> 5, WW)]; }
+  __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
+};
 struct MaskBits {
   const uint32_t* m;
   int WW, W;
@@ -2563,9 +2573,6 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
 #define MK_SCORE_THREADS 640
 #endif
 constexpr int kScoreThreads = MK_SCORE_THREADS;
-#ifndef MK_PF_WPE
-#define MK_PF_WPE 0
-#endif
 #ifndef MK_SCORE_TAIL_THREADS
 #define MK_SCORE_TAIL_THREADS 640
 #endif
@@ -2700,8 +2707,8 @@ __global__ __launch_bounds__(NT) void k_score_init(
 // w2c_sample * rand, rand = Transform(setRPY(g,g,g), (g,g,g)) drawn yaw, pitch,
 // roll, z, y, x; best = first strict minimum (argmin by (error, index) over
 // the 50, taken only when strictly below the current error).
-template <int NT, int SPLIT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MK_PF_WPE > 0 && SPLIT == 1 ? MK_PF_WPE : 1))) void k_score_pf(
+template <int NT, int SPLIT, bool LM>
+__global__ __launch_bounds__(NT) void k_score_pf(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
     FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations) {
@@ -2710,7 +2717,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MK_PF_WPE > 
   if (!st[f].reaches_pf) return;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  const uint32_t* fm = mbits + (size_t)f * bstride;
+  extern __shared__ __align__(16) uint32_t pf_mask[];
+  if (LM) {  // stage the tiled plane (bits::tiled_words: a multiple of 32 words, 16-byte aligned)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int n4 = (int)(bits::tiled_words(W, H) / 4);
+    const u32x4* src = (const u32x4*)fm;
+    u32x4* dst = (u32x4*)pf_mask;
+    for (int i = tid; i < n4; i += NT) dst[i] = src[i];
+  }
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   __shared__ double lm[3 * 768];
@@ -2748,7 +2763,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MK_PF_WPE > 
       const int j = task / SPLIT, h = task - j * SPLIT;
       long long sum;
       int cnt;
-      wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr, mask, W, H, sum, cnt);
+      if (LM)
+        wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr,
+                       MaskLds{(lds_cu32*)pf_mask, bits::words(W)}, W, H, sum, cnt);
+      else
+        wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr,
+                       MaskBits{fm, bits::words(W), W}, W, H, sum, cnt);
       if (lane == 0) {
         Ps[task] = sum;
         Pn[task] = cnt;
