@@ -111,6 +111,8 @@ inline float rng_gauss(uint64_t& state) {
 struct Ctx {
   mantis_config cfg{};
   hipStream_t s = nullptr;
+  hipStream_t s_copy = nullptr;     // side stream: the gaussian stream's H2D, overlapped with RPP
+  hipEvent_t ev_gauss = nullptr;    // ... which s waits on before scoring
   std::string err;
   uint64_t rng_state = 1;
   // map
@@ -452,7 +454,13 @@ void gen_gauss(Ctx* c, int n) {  // n <= c->gauss_cap
 
 mantis_status run_score(Ctx* c, int n, int n_gauss) {
   const int per = c->cfg.particles * c->cfg.iterations * 6;
-  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s));
+  // on the side stream as soon as the host has drawn it (the caller joined the
+  // drawing thread), so the copy overlaps the RPP kernels still queued on s;
+  // s waits for it only before the scoring kernels. d_gauss / h_gauss are free:
+  // the previous batch's call synchronised s, which had waited on this copy.
+  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
+  HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
+  HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
   k_score_init<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
@@ -747,8 +755,12 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   Ctx* c = new Ctx();
   c->cfg = cfg;
   c->rng_state = cfg.rng_seed ? cfg.rng_seed : 0xffffffffULL;
-  if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gauss, hipEventDisableTiming) != hipSuccess) {
     g_create_err = "hipSetDevice/hipStreamCreate failed";
+    if (c->s) (void)hipStreamDestroy(c->s);
+    if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
     delete c;
     return MANTIS_ERR_DEVICE;
   }
@@ -881,6 +893,8 @@ mantis_status mantis_destroy(void* ctx) {
   for (void* p : hptrs)
     if (p) (void)hipHostFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->ev_gauss) (void)hipEventDestroy(c->ev_gauss);
+  if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
   if (c->s) (void)hipStreamDestroy(c->s);
   delete c;
   return MANTIS_OK;
