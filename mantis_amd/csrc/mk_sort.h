@@ -95,9 +95,18 @@ MK_HD ErrIdx* unguarded_partition(ErrIdx* first, ErrIdx* last, ErrIdx* pivot) {
 MK_HD void introsort_loop(ErrIdx* first, ErrIdx* last, int depth_limit) {
   // iterative form of the reference recursion: recurse on the right part,
   // loop on the left part (same visiting order, explicit stack)
+#if MK_DM_DEVICE
+  // one thread per block sorts (k_score_init / k_score_final, tid 0): the
+  // explicit stack lives in LDS instead of 1.3 KB of per-lane scratch that
+  // every lane of those kernels would otherwise be allocated
+  __shared__ ErrIdx* st_first[64];
+  __shared__ ErrIdx* st_last[64];
+  __shared__ int st_depth[64];
+#else
   ErrIdx* st_first[64];
   ErrIdx* st_last[64];
   int st_depth[64];
+#endif
   int sp = 0;
   st_first[sp] = first; st_last[sp] = last; st_depth[sp] = depth_limit; sp++;
   while (sp > 0) {
