@@ -273,6 +273,13 @@ mantis_status mantis_quad_gn(void* ctx, const double* img_pts, const double* obj
 mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
                                   int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
                                   int64_t* best_idx);
+/* The same with device-resident inputs: mask_dev (W*H bytes, or NULL) and c2w_dev
+ * (n x 12 doubles) are device pointers on the context's GPU (mantis_device_alloc
+ * or any allocation of that device), read in place -- no staging copy -- for
+ * callers whose hypotheses are produced on the device or reused across calls. */
+mantis_status mantis_score_argmin_dev(void* ctx, const mantis_image* img, const uint8_t* mask_dev,
+                                      const double* c2w_dev, int32_t n, int64_t index_base, int32_t use_comm,
+                                      double* best_err, int64_t* best_idx);
 /* The cross-shard rule on its own (host only): pairs = nranks x (err, global index). */
 mantis_status mantis_argmin_pick(const double* pairs, int32_t nranks, double* best_err, int64_t* best_idx);
 

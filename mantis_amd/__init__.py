@@ -140,6 +140,8 @@ _SIGS = {
     "mantis_gn_allreduce": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mantis_score_argmin": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
                                       C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_score_argmin_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
+                                      C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_argmin_pick": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
 }
 
@@ -444,6 +446,16 @@ class Mantis:
         self._chk(lib().mantis_score_argmin(self.h, C.byref(img), None if mk is None else mk.ctypes.data,
                                             c2w.ctypes.data, len(c2w), index_base, int(use_comm), C.byref(e),
                                             C.byref(i)), "score_argmin")
+        return e.value, i.value
+
+    def score_argmin_dev(self, img, c2w_dev, n, index_base=0, use_comm=False, mask_dev=None):
+        """score_argmin on device-resident inputs (mantis_score_argmin_dev): c2w_dev = device
+        pointer to n x 12 doubles, mask_dev = device pointer to W*H bytes or None."""
+        e = C.c_double()
+        i = C.c_int64()
+        self._chk(lib().mantis_score_argmin_dev(self.h, C.byref(img), None if mask_dev is None else C.c_void_p(mask_dev),
+                                                C.c_void_p(c2w_dev), int(n), index_base, int(use_comm), C.byref(e),
+                                                C.byref(i)), "score_argmin_dev")
         return e.value, i.value
 
     def rpp(self, img_pts, obj_pts):

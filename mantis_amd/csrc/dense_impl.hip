@@ -61,9 +61,13 @@ mantis_status mantis_argmin_pick(const double* pairs, int32_t nranks, double* be
   return MANTIS_OK;
 }
 
-mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
-                                  int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
-                                  int64_t* best_idx) {
+}  // extern "C"
+
+namespace {
+// dev: mask / c2w are device pointers read in place (mantis_score_argmin_dev)
+mantis_status score_argmin_impl(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
+                                int64_t* best_idx, bool dev) {
   Ctx* c = (Ctx*)ctx;
   if (c) bind_device(c);
   if (!c || !img || !c2w || n < 0 || !best_err || !best_idx) return MANTIS_ERR_ARG;
@@ -88,15 +92,21 @@ mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint
   }
   if (!c->d_pairs && dalloc(c, &c->d_pairs, (size_t)2 * 64) != MANTIS_OK) return MANTIS_ERR_OOM;
   const uint8_t* d_mask = nullptr;
-  if (mask) {
-    HIP_OK(hipMemcpyAsync(c->d_mask, mask, (size_t)W * H, hipMemcpyHostToDevice, c->s));
-    d_mask = c->d_mask;
+  const double* d_c2w = c->d_dense_c2w;
+  if (dev) {
+    d_mask = mask;
+    d_c2w = c2w;
+  } else {
+    if (mask) {
+      HIP_OK(hipMemcpyAsync(c->d_mask, mask, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+      d_mask = c->d_mask;
+    }
+    if (n > 0) HIP_OK(hipMemcpyAsync(c->d_dense_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
   }
-  if (n > 0) HIP_OK(hipMemcpyAsync(c->d_dense_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
   mark(c, "start");
   if (n > 0) {
-    k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, c->d_dense_c2w, n, 1, c->d_dense_err,
+    k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, 1, c->d_dense_err,
                                                c->d_dense_np);
     mark(c, "score_dense");
   }
@@ -117,6 +127,21 @@ mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint
   HIP_OK(hipStreamSynchronize(c->s));
   finish_profile(c);
   return mantis_argmin_pick(h, nr, best_err, best_idx);
+}
+}  // namespace
+
+extern "C" {
+
+mantis_status mantis_score_argmin(void* ctx, const mantis_image* img, const uint8_t* mask, const double* c2w,
+                                  int32_t n, int64_t index_base, int32_t use_comm, double* best_err,
+                                  int64_t* best_idx) {
+  return score_argmin_impl(ctx, img, mask, c2w, n, index_base, use_comm, best_err, best_idx, false);
+}
+
+mantis_status mantis_score_argmin_dev(void* ctx, const mantis_image* img, const uint8_t* mask_dev,
+                                      const double* c2w_dev, int32_t n, int64_t index_base, int32_t use_comm,
+                                      double* best_err, int64_t* best_idx) {
+  return score_argmin_impl(ctx, img, mask_dev, c2w_dev, n, index_base, use_comm, best_err, best_idx, true);
 }
 
 }  // extern "C"

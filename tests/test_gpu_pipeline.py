@@ -518,6 +518,16 @@ def test_dense_config5_full_grid_8_shards(m720, landmark_map):
     err, npj = m720.score(im, hyps, fast=True, mask=mask)
     e, i = m720.score_argmin(im, hyps, 0, False, mask)
     assert i == int(np.argmin(err)) and e == err.min()
+    # device-resident inputs (mantis_score_argmin_dev): the same winner
+    d_h = m720.device_alloc(hyps.nbytes)
+    d_m = m720.device_alloc(mask.nbytes)
+    try:
+        m720.h2d(d_h, np.ascontiguousarray(hyps, np.float64))
+        m720.h2d(d_m, np.ascontiguousarray(mask, np.uint8))
+        assert m720.score_argmin_dev(im, d_h, len(hyps), 0, False, d_m) == (e, i)
+    finally:
+        m720.device_free(d_h)
+        m720.device_free(d_m)
     pairs = []
     for r in range(8):
         lo, hi = dense.shard_range(len(hyps), r, 8)
