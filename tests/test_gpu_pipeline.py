@@ -539,3 +539,46 @@ def test_dense_config5_full_grid_8_shards(m720, landmark_map):
     sel = np.unique(np.concatenate([np.arange(0, 16200, 40), [i]]))
     oe, on = orc.score(cleaned, K, D, hyps[sel], fast=True)
     assert np.array_equal(err[sel], oe) and np.array_equal(npj[sel], on)
+
+
+def test_pf_mask_lds_and_global_paths_agree(landmark_map):
+    """k_score_pf reads the clean mask from an LDS copy of the frame's tiled
+    plane when it fits (720p) and through the L1 otherwise
+    (MANTIS_PF_MASK_GLOBAL=1 forces that path); both block shapes (the
+    small-batch 1024-thread one and the large-batch 640-thread one, chosen by
+    MANTIS_TRACE_LDS_FRAMES) must give bit-identical frame results."""
+    import os
+
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(23)
+    frames = []
+    for f in range(4):
+        R, pos = synth.random_pose(rng)
+        frames.append(M.make_image(synth.render_host(synth.make_cam(R, pos), synth.frame_seed(6, f)), K, D))
+
+    def run(env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            m = M.Mantis(max_cams=4)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        try:
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+            _, cams = m.process(frames)
+            return [(c.reason, c.publish, c.pf_error, tuple(c.position), tuple(c.orientation_xyzw)) for c in cams]
+        finally:
+            m.close()
+
+    for small in ("64", "0"):
+        lds = run({"MANTIS_TRACE_LDS_FRAMES": small})
+        glob = run({"MANTIS_TRACE_LDS_FRAMES": small, "MANTIS_PF_MASK_GLOBAL": "1"})
+        assert lds == glob, small
+        assert any(r[0] >= 0 for r in lds)
