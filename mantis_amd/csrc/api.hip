@@ -465,27 +465,19 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
   k_score_init<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
                                               c->d_dbg, c->d_sst);
-  // small batches (latency): 16 waves per frame, two per particle over halves
-  // of the landmarks; large batches: 10 waves, one per particle
-  // the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0: 720p yes, 1080p no)
+  // particle filter: 16 waves per frame, each task one particle over a
+  // 1/kPfSplit slice of the landmarks (the integer partial sums combine
+  // exactly); the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0:
+  // 720p yes, 1080p no)
   const size_t ml = c->pf_mask_lds;
-  if (n <= c->trace_lds_frames) {
-    if (ml)
-      k_score_pf<1024, 2, true><<<n, 1024, ml, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss,
-                                                      c->d_res, c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
-    else
-      k_score_pf<1024, 2, false><<<n, 1024, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss,
-                                                       c->d_res, c->d_dbg, c->d_sst, c->cfg.particles, c->cfg.iterations);
-  } else {
-    if (ml)
-      k_score_pf<kScoreThreads, 1, true><<<n, kScoreThreads, ml, c->s>>>(
-          c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-          c->cfg.iterations);
-    else
-      k_score_pf<kScoreThreads, 1, false><<<n, kScoreThreads, 0, c->s>>>(
-          c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-          c->cfg.iterations);
-  }
+  if (ml)
+    k_score_pf<kPfThreads, kPfSplit, true><<<n, kPfThreads, ml, c->s>>>(
+        c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
+        c->cfg.iterations);
+  else
+    k_score_pf<kPfThreads, kPfSplit, false><<<n, kPfThreads, 0, c->s>>>(
+        c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
+        c->cfg.iterations);
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
                                                c->d_sst, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw");
@@ -783,18 +775,15 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   }
   {
     // LDS-staged mask for the particle filter: the tiled plane of a max-size
-    // frame beside the kernels' static LDS (both block sizes must take it)
+    // frame beside the kernel's static LDS
     const size_t ml = bits::tiled_words(c->Wmax, c->Hmax) * 4;
-    hipFuncAttributes a1, a2;
+    hipFuncAttributes a1;
     c->pf_mask_lds = 0;
     if (!getenv("MANTIS_PF_MASK_GLOBAL") &&
-        hipFuncGetAttributes(&a1, (const void*)k_score_pf<kScoreThreads, 1, true>) == hipSuccess &&
-        hipFuncGetAttributes(&a2, (const void*)k_score_pf<1024, 2, true>) == hipSuccess &&
-        std::max(a1.sharedSizeBytes, a2.sharedSizeBytes) + ml <= 160 * 1024 &&
-        hipFuncSetAttribute((const void*)k_score_pf<kScoreThreads, 1, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess &&
-        hipFuncSetAttribute((const void*)k_score_pf<1024, 2, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)ml) == hipSuccess)
+        hipFuncGetAttributes(&a1, (const void*)k_score_pf<kPfThreads, kPfSplit, true>) == hipSuccess &&
+        a1.sharedSizeBytes + ml <= 160 * 1024 &&
+        hipFuncSetAttribute((const void*)k_score_pf<kPfThreads, kPfSplit, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess)
       c->pf_mask_lds = ml;
   }
   if (morph_lds(c->Wmax) > 160 * 1024 ||

@@ -2601,17 +2601,19 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
 //   k_score_init   evaluateHypotheses(C hyps) + getBestNHypotheses(1)
 //   k_score_pf     optimizeHypothesisWithParticleFilter (10 x 50)
 //   k_score_final  81 shifts, top-20, determineBestYaw, publish gate
-// Block size: 10 waves per frame (50 particles = 5 rounds of waves).
-#ifndef MK_SCORE_THREADS
-#define MK_SCORE_THREADS 640
+// init / final: 10 waves per frame. Particle filter block: 16 waves, tasks = (particle, 1/kPfSplit of the
+// landmarks): 100 tasks over 16 waves at split 2 -- 18.3 ms per 4096 frames
+// against 20.5 for 10 waves with one task per particle (50 tasks, 5 rounds)
+constexpr int kPfThreads = 1024;
+#ifndef MK_PF_SPLIT
+#define MK_PF_SPLIT 2
 #endif
-constexpr int kScoreThreads = MK_SCORE_THREADS;
+constexpr int kPfSplit = MK_PF_SPLIT;
 #ifndef MK_SCORE_TAIL_THREADS
 #define MK_SCORE_TAIL_THREADS 640
 #endif
 constexpr int kScoreTail = MK_SCORE_TAIL_THREADS;  // k_score_init / k_score_final block size (>= 128: 81 shift lanes)
 static_assert(kScoreTail >= 128 && kScoreTail % 64 == 0, "score tail block");
-constexpr int kWaves = kScoreThreads / 64;
 
 struct PoseLds {
   Xf c2w, w2c;
