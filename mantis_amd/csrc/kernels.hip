@@ -1119,7 +1119,11 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
   const int by = r[y], ny = r[y + 1] - by;
   for (int j = lane; j < ny; j += 64) {
     const int id = by + j;
-    if (id == 0 || uf_find_c(L, id) != id) continue;  // run 0 (ring) is the outside background
+    // a root is a run whose label is itself: one load (a find would walk, and
+    // path-halve, the chain of every non-root; halving never makes a non-root
+    // point to itself, so the test is exact while other lanes compress).
+    // Run 0 (ring) is the outside background.
+    if (id == 0 || L[id] != id) continue;
     const int key = y * Wp + X[id];
     Border b;
     b.key = key;
