@@ -664,8 +664,11 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = Ll[j];
       const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
-      L[g0 + j] = g0 + root;
-      fl[g0 + j] = 0;
+      // global labels only where a later kernel looks: the band's first and
+      // last rows (seam unions), list B runs (fb == 2) and band roots (finds
+      // end there; their flag byte is what k_hyst_mark / k_hyst_fix use)
+      if (q == 0 || q == nr - 1 || fb == 2 || root == j) L[g0 + j] = g0 + root;
+      if (root == j) fl[g0 + j] = 0;
       if (fb & 1) {
         const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
         for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
