@@ -1,15 +1,22 @@
-"""Per-kernel average of the batch launches (the 4 longest dispatches of each
-kernel) from a rocprofv3 kernel trace CSV. Usage: kern_avg.py <trace.csv> [n]"""
+"""Per-kernel average of the batch launches from a rocprofv3 kernel trace CSV:
+for each kernel, the dispatches with its largest grid (the batch launches;
+the latency runs' single-rig launches have smaller grids), averaged.
+Usage: kern_avg.py <trace.csv> [max rows]"""
 import collections
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-keep = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 d = collections.defaultdict(list)
 for r in rows:
-    d[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-out = sorted(((sum(sorted(v)[-keep:]) / min(keep, len(v)), k.split("(")[0][:48], len(v)) for k, v in d.items()),
-             reverse=True)
-for a, k, n in out[:40]:
-    print(f"{a:9.3f} ms  {k}  ({n})")
+    g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    d[r["Kernel_Name"]].append((g, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+out = []
+for k, v in d.items():
+    gmax = max(g for g, _ in v)
+    sel = [t for g, t in v if g == gmax]
+    out.append((sum(sel) / len(sel), k.split("(")[0][:48], len(sel), len(v)))
+out.sort(reverse=True)
+for a, k, n, m in out[:top]:
+    print(f"{a:9.3f} ms  {k}  ({n} of {m} launches)")
