@@ -73,10 +73,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, choices=(3, 4, 5))
     p.add_argument("--rigs", type=int, default=None,
-                   help="rigs per step per GPU (config 3, default 3072) / rigs per step (config 4, default 128)")
+                   help="rigs per step per GPU (config 3, default 1024 per context) / rigs per step (config 4, "
+                        "default 128)")
     p.add_argument("--frames", type=int, default=16, help="config 5: frames per step (16,200 hypotheses each)")
     p.add_argument("--distinct", type=int, default=128, help="distinct rendered rigs (cycled through the batch)")
-    p.add_argument("--contexts", type=int, default=3,
+    p.add_argument("--contexts", type=int, default=4,
                    help="config 3: library contexts per GPU, each driven by its own host thread (one ctx per "
                         "thread, include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--latency-iters", type=int, default=15)
@@ -86,8 +87,9 @@ def parse():
                    help="CPU baseline: seconds of oracle work per leg (1 core, all cores)")
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="CPU baseline all-cores leg: at most this many threads (the box's CPU share per GPU)")
-    p.add_argument("--hw-queues", type=int, default=4,
-                   help="GPU_MAX_HW_QUEUES for this process, so the contexts' streams run on separate hardware queues")
+    p.add_argument("--hw-queues", type=int, default=None,
+                   help="GPU_MAX_HW_QUEUES for this process (default 2 per context: each context has a compute "
+                        "and a copy stream, and streams that share a hardware queue serialise)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--gn", type=int, default=1,
                    help="joint rig Gauss-Newton after the per-camera pipeline (SURVEY §8 d configs 3/4); "
@@ -98,7 +100,9 @@ def parse():
                         "points used, max seen 28k; 262144 at 1080p); overflow is an error")
     a = p.parse_args()
     if a.rigs is None:
-        a.rigs = 3072 if a.config == 3 else 128
+        a.rigs = 1024 * a.contexts if a.config == 3 else 128
+    if a.hw_queues is None:
+        a.hw_queues = 2 * a.contexts
     if a.max_contour_points is None:
         a.max_contour_points = 262144 if a.config == 4 else 98304
     return a
@@ -680,7 +684,12 @@ def main():
         print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world} (run under torchrun with --nproc-per-node "
               f"{a.gpus}, or without torchrun to let bench.py spawn the ranks)", file=sys.stderr)
         return 2
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(32, a.hw_queues))))  # before HIP initialises
+    # before HIP initialises; never below what the environment already grants, at most 32
+    try:
+        env_q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        env_q = 4
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(4, env_q, a.hw_queues)))
     cpu = None
     if a.config == 3 and world == 1 and not a.no_cpu:
         try:
