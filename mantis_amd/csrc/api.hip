@@ -458,13 +458,16 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // drawing thread), so the copy overlaps the RPP kernels still queued on s;
   // s waits for it only before the scoring kernels. d_gauss / h_gauss are free:
   // the previous batch's call synchronised s, which had waited on this copy.
-  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
-  HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
-  HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
+  static const bool zc = getenv("MANTIS_GAUSS_COPY") == nullptr;  // A/B: the side-stream copy
+  if (!zc) {
+    HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
+    HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
+    HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
+  }
   mark(c, "gauss_h2d");
   Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
-  k_score_init<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
-                                              c->d_dbg, c->d_sst);
+  k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
+                                              c->d_dbg, c->d_sst, zc ? c->h_gauss : nullptr, c->d_gauss, per);
   // particle filter: 16 waves per frame, each task one particle over a
   // 1/kPfSplit slice of the landmarks (the integer partial sums combine
   // exactly); the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0:

@@ -2624,7 +2624,7 @@ constexpr int kPfSplit = MK_PF_SPLIT;
 // score stage 18.4 -> 17.5 ms per 4096 frames)
 constexpr int kScoreTail = MK_SCORE_TAIL_THREADS;
 #ifndef MK_SCORE_INIT_THREADS
-#define MK_SCORE_INIT_THREADS 640
+#define MK_SCORE_INIT_THREADS 1024
 #endif
 constexpr int kScoreInit = MK_SCORE_INIT_THREADS;  // k_score_init block size
 static_assert(kScoreTail >= 128 && kScoreTail % 64 == 0, "score tail block");
@@ -2660,9 +2660,16 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_score_init(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
-    ScoreState* __restrict__ sst) {
+    ScoreState* __restrict__ sst, const float* __restrict__ hgauss, float* __restrict__ dgauss, int per) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // hgauss != null: this frame's slice of the host-drawn gaussian stream is
+  // read from pinned host memory straight into the device buffer the
+  // particle filter reads (no separate copy and no cross-stream wait)
+  if (hgauss && st[f].reaches_pf) {
+    const size_t o = (size_t)st[f].gauss_offset;
+    for (int i = tid; i < per; i += NT) dgauss[o + i] = hgauss[o + i];
+  }
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
   const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
