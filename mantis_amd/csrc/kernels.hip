@@ -474,30 +474,28 @@ __global__ __launch_bounds__(256) void k_hyst_count(const uint32_t* __restrict__
   }
 }
 
-// wave per row: run extents; a run's end is the bit before the first zero at
-// or after its start (runs of NMS candidates are short: one or two words)
+// wave per row: run extents. Runs of a row are disjoint, so its k-th start
+// bit and its k-th end bit bound run k: starts and ends are numbered by two
+// wave scans and written as the two 16-bit halves of the packed extent (no
+// search for the end).
 __global__ __launch_bounds__(256) void k_hyst_runs(const uint32_t* __restrict__ cbits, size_t bstride, HystRuns hr,
                                                    int W, int H) {
   const int f = blockIdx.y, y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (y >= H) return;
   const int WW = bits::words(W);
   const uint32_t* row = cbits + (size_t)f * bstride + (size_t)y * WW;
-  uint32_t* X = hr.x + (size_t)f * hr.x_stride;
-  int bs = hr.rowb[(size_t)f * hr.rstride + y];
+  uint16_t* X16 = (uint16_t*)(hr.x + (size_t)f * hr.x_stride);  // extent j = start | end << 16
+  int bs = hr.rowb[(size_t)f * hr.rstride + y], be = bs;
   for (int w0 = 0; w0 < WW; w0 += 64) {
     const int w = w0 + lane;
     uint32_t S = w < WW ? hb_starts(row, w) : 0u;
-    const int cs = __popc(S);
-    const int is = wave_incl_scan(cs, lane);
-    for (int os = bs + is - cs; S; S &= S - 1, os++) {
-      const int b = __ffs(S) - 1;
-      int ww = w;
-      uint32_t z = ~row[w] & (0xffffffffu << b);
-      while (!z && ++ww < WW) z = ~row[ww];
-      const int e = z ? 32 * ww + __ffs(z) - 2 : 32 * WW - 1;  // bits past W are zero: z is found by then
-      X[os] = (uint32_t)(32 * w + b) | ((uint32_t)e << 16);
-    }
+    uint32_t E = w < WW ? hb_ends(row, w, WW) : 0u;
+    const int cs = __popc(S), ce = __popc(E);
+    const int is = wave_incl_scan(cs, lane), ie = wave_incl_scan(ce, lane);
+    for (int os = bs + is - cs; S; S &= S - 1, os++) X16[2 * (size_t)os] = (uint16_t)(32 * w + __ffs(S) - 1);
+    for (int oe = be + ie - ce; E; E &= E - 1, oe++) X16[2 * (size_t)oe + 1] = (uint16_t)(32 * w + __ffs(E) - 1);
     bs += __shfl(is, 63);
+    be += __shfl(ie, 63);
   }
 }
 
