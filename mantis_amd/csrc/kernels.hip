@@ -2963,59 +2963,59 @@ __global__ __launch_bounds__(NT) void k_score_final(
   }
   __syncthreads();
   // determineBestYaw: 4 yaw sets (rotZ^k * w2c, left-multiplied), COLOR errors
-  // on the original image. P[0..19] keep the shifts; yaw sets go to P[81..]
-  // one set at a time (set k derives from set k-1).
+  // on the original image. Set k derives from set k-1; all four are built
+  // first (P[20k + i], the shifts are no longer needed) so their 80 scorings
+  // share one pass over the waves (5 rounds at 16 waves instead of 4 x 2).
   __shared__ PoseLds Y[20];
-  __shared__ double ysum[4];
   if (tid < 20) {
     const PoseLds& s = P[top[tid]];
     Y[tid] = s;
   }
   __syncthreads();
   const Xf rz = make_rot_z90();
-  const double* green = lm + 3 * (lmk.nw + lmk.nr);
-  __shared__ double yset_err[20];
-  __shared__ PoseLds last_best[1];
-  __shared__ double best_error;
-  __shared__ int32_t best_k;
-  if (tid == 0) { best_error = DBL_MAX; best_k = -1; }
-  for (int k = 0; k < 4; k++) {
-    if (k > 0 && tid < 20) {
+  if (tid < 20) {
+    P[tid] = Y[tid];
+    for (int k = 1; k < 4; k++) {
       Hyp h;
-      hyp_set_w2c(h, xf_mul(rz, Y[tid].w2c));
-      Y[tid].c2w = h.c2w; Y[tid].w2c = h.w2c; Y[tid].q = h.q;
+      hyp_set_w2c(h, xf_mul(rz, P[20 * (k - 1) + tid].w2c));
+      PoseLds& d = P[20 * k + tid];
+      d.c2w = h.c2w; d.w2c = h.w2c; d.q = h.q;
     }
-    __syncthreads();
-    for (int j = wave; j < 20; j += (NT / 64)) {
-      double e;
-      int n;
+  }
+  __syncthreads();
+  const double* green = lm + 3 * (lmk.nw + lmk.nr);
+  __shared__ double yset_err[80];
+  for (int j = wave; j < 80; j += (NT / 64)) {
+    double e;
+    int n;
 #ifdef MK_DIAG_NO_COLOR  // timing diagnostic only: wrong results
-      e = 1.0 + j;
-      n = 1;
+    e = 1.0 + j;
+    n = 1;
 #else
-      wave_score_color(Y[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
+    wave_score_color(P[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
 #endif
-      if (lane == 0) yset_err[j] = e;
-    }
-    __syncthreads();
-    if (tid == 0) {
+    if (lane == 0) yset_err[j] = e;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double best_error = DBL_MAX;
+    int best_k = -1;
+    for (int k = 0; k < 4; k++) {
       double tot = 0;
       int succ = 0;
       for (int j = 0; j < 20; j++)
-        if (fabs(yset_err[j] - DBL_MAX) > 0.001) { succ++; tot += yset_err[j]; }
+        if (fabs(yset_err[20 * k + j] - DBL_MAX) > 0.001) { succ++; tot += yset_err[20 * k + j]; }
       double te = succ == 0 ? DBL_MAX : tot / (double)succ;
       yerr[k] = te;
       D.yaw_err[k] = te;
       if (te < best_error) {
         best_error = te;
         best_k = k;
-        last_best[0] = Y[19];
-        last_best[0].err = yset_err[19];
       }
     }
-    __syncthreads();
-  }
-  if (tid == 0) {
+    // the published pose is the last of the best set (its last assignment)
+    PoseLds& pb = P[20 * (best_k < 0 ? 0 : best_k) + 19];
+    if (best_k >= 0) pb.err = yset_err[20 * best_k + 19];
     nsc += 80;
     double min1 = DBL_MAX, min2 = DBL_MAX;
     for (int k = 0; k < 4; k++) {
@@ -3038,7 +3038,6 @@ __global__ __launch_bounds__(NT) void k_score_final(
       D.reason = R.reason;
       D.publish = 0;
     } else {
-      const PoseLds& pb = last_best[0];
       for (int k = 0; k < 3; k++) { R.position[k] = pb.w2c.t[k]; D.position[k] = pb.w2c.t[k]; }
       R.orientation_xyzw[0] = pb.q.x; R.orientation_xyzw[1] = pb.q.y;
       R.orientation_xyzw[2] = pb.q.z; R.orientation_xyzw[3] = pb.q.w;
