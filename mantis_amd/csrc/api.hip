@@ -136,6 +136,7 @@ struct Ctx {
   uint32_t *d_eb = nullptr, *d_b1 = nullptr, *d_b2 = nullptr;  // bit planes
   uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
+  int morph_bh = 48;       // k_morph output rows per band (MB_BH, or MB_BH_NARROW at wide max_width)
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
@@ -234,8 +235,8 @@ inline void bind_device(const Ctx* c) {
   if (hipGetDevice(&d) != hipSuccess || d != c->cfg.device) (void)hipSetDevice(c->cfg.device);
 }
 
-// dynamic LDS of k_morph: three band buffers of (MB_BH + 2 MB_HALO) rows
-inline size_t morph_lds(int W) { return (size_t)3 * (MB_BH + 2 * MB_HALO) * ((W + 31) / 32) * sizeof(uint32_t); }
+// dynamic LDS of k_morph: three band buffers of (bh + 2 MB_HALO) rows
+inline size_t morph_lds(int W, int bh) { return (size_t)3 * (bh + 2 * MB_HALO) * ((W + 31) / 32) * sizeof(uint32_t); }
 
 inline int blocks_for(size_t n, int per = 256, int cap = 4096) {
   size_t b = (n + per - 1) / per;
@@ -307,8 +308,9 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
   mark(c, "hysteresis");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
-  dim3 gm((H + MB_BH - 1) / MB_BH, n);
-  k_morph<<<gm, 256, morph_lds(W), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride);
+  dim3 gm((H + c->morph_bh - 1) / c->morph_bh, n);
+  k_morph<<<gm, MB_THREADS, morph_lds(W, c->morph_bh), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
+                                                              c->morph_bh);
   if (det_bytes) k_bits_to_bytes<<<blocks_for((size_t)(W + 2) * (H + 2)), 256, 0, c->s>>>(c->d_dbits, c->d_det, W + 2, H + 2,
                                                                                           dbits_wpw(W + 2));
   mark(c, "morph");
@@ -789,8 +791,10 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess)
       c->pf_mask_lds = ml;
   }
-  if (morph_lds(c->Wmax) > 160 * 1024 ||
-      hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize, (int)morph_lds(c->Wmax)) !=
+  c->morph_bh = morph_lds(c->Wmax, MB_BH) <= 160 * 1024 ? MB_BH : MB_BH_NARROW;
+  if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
+      hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)morph_lds(c->Wmax, c->morph_bh)) !=
           hipSuccess) {
     g_create_err = "max_width too large for the morphology band kernel";
     (void)hipStreamDestroy(c->s);

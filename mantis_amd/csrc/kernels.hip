@@ -734,10 +734,18 @@ __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restr
 // 64-bit window at any x be read without a bounds test).
 __device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
 // ============================================================== morphology
+// output rows per band: MB_BH when the three band buffers fit in LDS at the
+// context's max width (≤ 2816 px), else MB_BH_NARROW (bands at 1280 px:
+// 3 x (96 + 2 x 29) rows x 40 words x 4 B = 74 KB, two per CU; measured
+// 4.75 -> 3.63 ms per 4096 frames against 48 rows at 256 threads)
 #ifndef MK_MB_BH
-#define MK_MB_BH 48  // 3 x (48 + 2 x 29) rows x 40 words x 4 B = 51 KB: three bands per CU at 1280 px
+#define MK_MB_BH 96
 #endif
-constexpr int MB_BH = MK_MB_BH;  // output rows per band
+#ifndef MK_MB_THREADS
+#define MK_MB_THREADS 512
+#endif
+constexpr int MB_BH = MK_MB_BH, MB_BH_NARROW = 48;
+constexpr int MB_THREADS = MK_MB_THREADS;
 constexpr int MB_HALO = 29;   // mask chain reach: M0 2 + (3+3+4+4+5+5) + 3
 struct RowRange {
   int lo, hi;  // absolute rows [lo, hi) valid in a buffer
@@ -787,7 +795,7 @@ __device__ inline void mb_hv(const uint32_t* src, uint32_t* dst, RowRange out, i
 }
 
 // Detector binary and cleanImageByEdge mask in one pass over the edge bit
-// plane (mk_bits.h word semantics). A block owns a band of MB_BH output rows of
+// plane (mk_bits.h word semantics). A block owns a band of bh output rows of
 // one frame and keeps the band plus a MB_HALO-row halo on each side in LDS
 // (three row buffers), so the stages of the two chains never touch HBM between
 // them: each stage recomputes the rows its successors still need (its valid
@@ -797,16 +805,16 @@ __device__ inline void mb_hv(const uint32_t* src, uint32_t* dst, RowRange out, i
 //             -> padded bit plane (zero ring) for the contour CCL
 //   mask      HypothesisEvaluation.h:319-363: NG = NOT(gradient), M0 = edge |
 //             border(NG), 3 x {dilate, erode}(3 + i), erode(3) -> mask bit plane
-__global__ __launch_bounds__(256) void k_morph(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
+__global__ __launch_bounds__(MB_THREADS) void k_morph(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
-                                               size_t dstride) {
+                                               size_t dstride, int bh) {
   extern __shared__ uint32_t mb_lds[];
   const int f = blockIdx.y, t = threadIdx.x, nt = blockDim.x;
   const int WW = bits::words(W);
   const MbLane L{t % WW, t / WW, nt / WW};
-  const int yb = blockIdx.x * MB_BH, ye = min(H, yb + MB_BH);
+  const int yb = blockIdx.x * bh, ye = min(H, yb + bh);
   const int y0 = max(0, yb - MB_HALO), y1 = min(H, ye + MB_HALO);
-  const int rows = MB_BH + 2 * MB_HALO;
+  const int rows = bh + 2 * MB_HALO;
   uint32_t* A = mb_lds;
   uint32_t* B = A + rows * WW;
   uint32_t* Cb = B + rows * WW;
