@@ -735,11 +735,11 @@ __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restr
 __device__ __host__ inline int dbits_wpw(int Wp) { return (Wp + 31) / 32 + 1; }
 // ============================================================== morphology
 // output rows per band: MB_BH when the three band buffers fit in LDS at the
-// context's max width (≤ 2816 px), else MB_BH_NARROW (bands at 1280 px:
-// 3 x (96 + 2 x 29) rows x 40 words x 4 B = 74 KB, two per CU; measured
-// 4.75 -> 3.63 ms per 4096 frames against 48 rows at 256 threads)
+// context's max width (<= 2496 px), else MB_BH_NARROW (bands at 1280 px:
+// 3 x (112 + 2 x 29) rows x 40 words x 4 B = 82 KB, one per CU; measured
+// 4.75 -> 3.34 ms per 4096 frames against 48 rows at 256 threads)
 #ifndef MK_MB_BH
-#define MK_MB_BH 96
+#define MK_MB_BH 112
 #endif
 #ifndef MK_MB_THREADS
 #define MK_MB_THREADS 512
