@@ -174,6 +174,18 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
                                          const int32_t* cam_index, int32_t cams_per_rig, mantis_result* out,
                                          mantis_cam_result* cam_out);
 
+/* Stage entry of the sharded call's cross-rank RNG bookkeeping (device
+ * kernel k_gauss_offsets_global, for parity tests): `pairs` = the gathered
+ * (global frame index, reaches-PF flag) pairs of every rank (npairs pairs,
+ * padding slots (-1, 0)); each of the n_local frames with global index gidx[i]
+ * gets offsets[i] = per_frame x (frames before it in global order that reach
+ * the particle filter), i.e. where a sequential run over all cameras draws its
+ * cv::RNG gaussians (Mantis3Params.h:87, PoseAdjustment.h:15-16); *total = the
+ * gaussians drawn by all n_global frames. Host rule: mantis_amd/csrc/mk_shard.h. */
+mantis_status mantis_shard_gauss_offsets(void* ctx, const int32_t* pairs, int32_t npairs, int32_t n_global,
+                                         const int32_t* gidx, int32_t n_local, int32_t per_frame, int32_t* offsets,
+                                         int32_t* total);
+
 /* Rig Gauss-Newton record of rig `rig` of the last batch (cfg.gn_enable):
  * the fused pose the correspondences were formed with, the refined pose, the
  * cost before / after, and this rank's correspondences as rows of

@@ -143,6 +143,8 @@ _SIGS = {
     "mantis_score_argmin_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
                                       C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_argmin_pick": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_shard_gauss_offsets": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                                             C.c_int32, C.c_void_p, C.POINTER(C.c_int32)]),
 }
 
 
@@ -207,6 +209,8 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} missing: build it with __graft_entry__.build() (hipcc, gfx950)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if not hasattr(L, name) and os.environ.get("MANTIS_AMD_LIB"):
+                continue  # an older library under A/B (MANTIS_AMD_LIB): entry points it lacks stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -368,6 +372,18 @@ class Mantis:
         st = lib().mantis_process_rig_sharded(self.h, cams, rigs, n_local, idx.ctypes.data, cams_per_rig, out, cam_out)
         self._chk(st, "process_rig_sharded")
         return list(out), list(cam_out)
+
+    def shard_gauss_offsets(self, pairs, n_global, gidx, per_frame):
+        """k_gauss_offsets_global on gathered (global index, PF flag) pairs
+        (mantis_shard_gauss_offsets): (offsets of the local frames gidx, total)."""
+        pairs = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        gidx = np.ascontiguousarray(gidx, np.int32)
+        off = np.zeros(len(gidx), np.int32)
+        tot = C.c_int32()
+        self._chk(lib().mantis_shard_gauss_offsets(self.h, pairs.ctypes.data, len(pairs), n_global, gidx.ctypes.data,
+                                                   len(gidx), per_frame, off.ctypes.data, C.byref(tot)),
+                  "shard_gauss_offsets")
+        return off, tot.value
 
     def comm_info(self):
         nr, rk = C.c_int32(), C.c_int32()

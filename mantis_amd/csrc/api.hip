@@ -130,6 +130,7 @@ struct Ctx {
   // device workspace
   uint16_t* d_lroot = nullptr;  // hysteresis run extents (k_hyst_*), then contour run starts
   size_t lstride = 0;            // d_lroot entries per frame: max(plane, tiles x FTW x FTH)
+  size_t fstride = 0;            // d_strong bytes per frame: plane rounded up to a dword (32-bit flag atomics)
   uint8_t *d_bgr = nullptr, *d_strong = nullptr, *d_edge = nullptr,
           *d_det = nullptr, *d_mask = nullptr;
   int32_t* d_lab = nullptr;
@@ -215,7 +216,16 @@ struct Ctx {
   double* d_markov = nullptr;
   MarkovOp* d_mops = nullptr;
   int markov_n = 0;
+  // MANTIS_SCREEN=0 at mantis_create: the fast scorers' FP32 projection screen is
+  // off (every landmark takes the exact FP64 fallback; a test / A-B switch)
+  bool screen_off = false;
+  std::vector<std::pair<Cam, ScreenCam>> scam_cache;  // screen_cam_cached
 };
+
+// the map as the scoring kernels read it: FP64 triples, then the FP32 screen table
+inline Landmarks lmk_of(const Ctx* c) {
+  return Landmarks{c->d_lm, c->nw, c->nr, c->ng, c->d_lm ? (const float4*)(c->d_lm + kLmfOffset) : nullptr};
+}
 
 void mark(Ctx* c, const char* name) {
   if (!c->prof) return;
@@ -253,6 +263,19 @@ Cam cam_from(const mantis_image& im) {
   return m;
 }
 
+// FP32 screen constants of a camera (mk_screen.h screen_cam_from samples the
+// distortion curve: ~0.1 ms), memoised per context on the intrinsics: the
+// frames of a batch share a few cameras
+ScreenCam screen_cam_cached(Ctx* c, const Cam& cm) {
+  for (const auto& e : c->scam_cache)
+    if (std::memcmp(&e.first, &cm, sizeof(Cam)) == 0) return e.second;
+  ScreenCam sc = screen_cam_from(cm);
+  if (c->screen_off) sc.sens = INFINITY;  // MANTIS_SCREEN=0: every landmark through the exact fallback
+  if (c->scam_cache.size() >= 64) c->scam_cache.erase(c->scam_cache.begin());
+  c->scam_cache.emplace_back(cm, sc);
+  return sc;
+}
+
 // Stage the frames into the batch: device-resident contiguous inputs are
 // used in place; everything else is copied (pitch-converted) into d_bgr.
 mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int& H) {
@@ -269,6 +292,7 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
     fd.w = W;
     fd.h = H;
     fd.cam = cam_from(im);
+    fd.scam = screen_cam_cached(c, fd.cam);
     if (im.mem_kind == 1 && im.step_bytes == 3 * W) {
       fd.bgr = im.bgr;
     } else {
@@ -294,7 +318,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
                                                       c->vec_ok ? 1 : 0, c->d_b1, c->d_b2, B, tgx, tgy);
   mark(c, "canny_nms");
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
-  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, P, c->rstride, P / 2};
+  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2};
   dim3 gr4((H + 3) / 4, n);
   k_hyst_count<<<gr4, 256, 0, c->s>>>(c->d_b1, B, hr, W, H);
   k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, H);
@@ -467,7 +491,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
     HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
   }
   mark(c, "gauss_h2d");
-  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  Landmarks L = lmk_of(c);
   k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
                                               c->d_dbg, c->d_sst, zc ? c->h_gauss : nullptr, c->d_gauss, per);
   // particle filter: 16 waves per frame, each task one particle over a
@@ -506,79 +530,11 @@ void finish_profile(Ctx* c, bool append = false) {
   c->ev_names.clear();
 }
 
-// 4x4 helpers for rig results (row-major)
-void mat4_mul(const double* a, const double* b, double* o) {
-  double r[16];
-  for (int i = 0; i < 4; i++)
-    for (int j = 0; j < 4; j++) {
-      double s = 0;
-      for (int k = 0; k < 4; k++) s += a[i * 4 + k] * b[k * 4 + j];
-      r[i * 4 + j] = s;
-    }
-  std::memcpy(o, r, sizeof(r));
-}
-void mat4_inv_rigid(const double* a, double* o) {
-  double r[16] = {0};
-  for (int i = 0; i < 3; i++)
-    for (int j = 0; j < 3; j++) r[i * 4 + j] = a[j * 4 + i];
-  for (int i = 0; i < 3; i++) r[i * 4 + 3] = -(r[i * 4 + 0] * a[3] + r[i * 4 + 1] * a[7] + r[i * 4 + 2] * a[11]);
-  r[15] = 1;
-  std::memcpy(o, r, sizeof(r));
-}
-void quat_to_mat4(const double* q, const double* p, double* T) {
-  mk::Quat qq{q[0], q[1], q[2], q[3]};
-  double R[9];
-  basis_from_quat(qq, R);
-  for (int i = 0; i < 16; i++) T[i] = 0;
-  for (int i = 0; i < 3; i++) {
-    for (int j = 0; j < 3; j++) T[i * 4 + j] = R[i * 3 + j];
-    T[i * 4 + 3] = p[i];
-  }
-  T[15] = 1;
-}
-
-// Rig pose from per-camera results (reference-parity mode: no GN): the
-// published camera with the lowest error, mapped through T_base_cam.
-void fuse_rig(const double* Tbc, const mantis_cam_result* cr, int nc, mantis_result* out) {
-  std::memset(out, 0, sizeof(*out));
-  int best = -1;
-  int npub = 0, nscored = 0, nq = 0;
-  for (int i = 0; i < nc; i++) {
-    nscored += cr[i].n_scored;
-    nq += cr[i].n_quads;
-    if (cr[i].publish) {
-      npub++;
-      if (best < 0 || cr[i].error < cr[best].error) best = i;
-    }
-  }
-  out->num_particles = nscored;
-  out->n_quads = nq;
-  out->n_cams_published = npub;
-  out->status = MANTIS_OK;
-  if (best < 0) {
-    // nothing passes the yaw gate: report the first camera that produced a pose, unpublished
-    for (int i = 0; i < nc && best < 0; i++)
-      if (cr[i].reason == MANTIS_PUBLISHED || cr[i].reason == MANTIS_YAW_AMBIGUOUS) best = i;
-    out->publish = 0;
-    if (best < 0) return;
-  } else {
-    out->publish = 1;
-  }
-  double Twc[16], Tbc_inv[16], Twb[16];
-  quat_to_mat4(cr[best].orientation_xyzw, cr[best].position, Twc);
-  mat4_inv_rigid(Tbc + 16 * (size_t)best, Tbc_inv);
-  mat4_mul(Twc, Tbc_inv, Twb);
-  double R[9];
-  for (int i = 0; i < 3; i++)
-    for (int j = 0; j < 3; j++) R[i * 3 + j] = Twb[i * 4 + j];
-  mk::Quat q = basis_to_quat(R);
-  out->orientation_xyzw[0] = q.x; out->orientation_xyzw[1] = q.y;
-  out->orientation_xyzw[2] = q.z; out->orientation_xyzw[3] = q.w;
-  for (int i = 0; i < 3; i++) out->position[i] = Twb[i * 4 + 3];
-  for (int i = 0; i < 36; i++) out->covariance[i] = cr[best].covariance[i];
-  out->weight = cr[best].error;
-  out->min_yaw_diff = cr[best].min_yaw_diff;
-}
+// rig fusion and 4x4 helpers: mk_shard.h (shared with the CPU test build)
+using mk::shard::fuse_rig;
+using mk::shard::mat4_inv_rigid;
+using mk::shard::mat4_mul;
+using mk::shard::quat_to_mat4;
 
 template <class T>
 mantis_status dalloc(Ctx* c, T** p, size_t count);
@@ -608,6 +564,11 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shar
   if (!c->d_lm) { c->err = "map not set (mantis_set_map)"; return MANTIS_ERR_STATE; }
   if (n <= 0 || n > c->F) { c->err = "frame count exceeds max_cams"; return MANTIS_ERR_ARG; }
   const int ng = sh ? sh->n_global : n;
+  // the gaussian offsets are int32 on the device (FrameState::gauss_offset)
+  if ((int64_t)c->cfg.particles * c->cfg.iterations * 6 * ng > INT32_MAX) {
+    c->err = "particles x iterations x 6 x frames (all rig cameras when sharded) exceeds 2^31 gaussians per call";
+    return MANTIS_ERR_ARG;
+  }
   if (mantis_status e = ensure_gauss(c, ng)) return e;
   // The gaussian stream depends only on the RNG state, so a host thread draws
   // it while the device runs the image stages and RPP (the pinned buffer is
@@ -727,8 +688,13 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     cfg = *cfg_in;
   }
   if (cfg.max_quads == 0) cfg.max_quads = kMaxQuads;
-  // iterations bound: particles * iterations * 6 gaussians per frame must stay
-  // far inside int32 for the offset scan (k_gauss_offsets)
+  // gaussian offsets are int32 on the device (k_gauss_offsets): a batch of
+  // max_cams frames must draw fewer than 2^31 (sharded calls check their
+  // rig-wide count per call, process_frames)
+  if ((int64_t)cfg.particles * cfg.iterations * 6 * (cfg.max_cams > 0 ? cfg.max_cams : 1) > INT32_MAX) {
+    g_create_err = "particles x iterations x 6 x max_cams exceeds 2^31 gaussians per batch";
+    return MANTIS_ERR_ARG;
+  }
   if (cfg.particles < 1 || cfg.particles > 96 || cfg.iterations < 0 || cfg.iterations > 1000 || cfg.max_cams < 1 ||
       cfg.max_width < 3 || cfg.max_height < 3 || cfg.gn_iterations < 0 || cfg.gn_iterations > 10 ||
       cfg.quad_gn_iterations < 0 || cfg.quad_gn_iterations > 20 || cfg.rig_weighting < 0 || cfg.rig_weighting > 1) {
@@ -775,6 +741,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     c->trace_lds_max = 160 * 1024 - 512 * 8 - 64;
     c->trace_lds_ok = hipFuncSetAttribute((const void*)k_trace_borders_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)c->trace_lds_max) == hipSuccess;
+    const char* so = getenv("MANTIS_SCREEN");
+    c->screen_off = so && so[0] == '0';
     const char* e = getenv("MANTIS_TRACE_LDS_FRAMES");
     c->trace_lds_frames = e ? atoi(e) : c->n_cu / 4;
   }
@@ -806,7 +774,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   mantis_status st = MANTIS_OK;
   auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
   chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
-  chk(dalloc(c, &c->d_strong, (size_t)F * c->plane));
+  c->fstride = (c->plane + 3) & ~(size_t)3;  // the hysteresis flags take dword atomics at (root & ~3)
+  chk(dalloc(c, &c->d_strong, (size_t)F * c->fstride));
   c->lstride = (c->plane + 1) & ~(size_t)1;  // even: the hysteresis views it as u32 run extents
   chk(dalloc(c, &c->d_lroot, (size_t)F * c->lstride));
   chk(dalloc(c, &c->d_edge, c->plane));  // debug / single-frame byte planes (frame 0)
@@ -914,10 +883,17 @@ mantis_status mantis_set_map(void* ctx, const double* white, int32_t nw, const d
   all.insert(all.end(), white, white + 3 * nw);
   all.insert(all.end(), red, red + 3 * nr);
   all.insert(all.end(), green, green + 3 * ng);
+  // then the screen's FP32 table (X, Y, Z, |X|_1 rounded up; mk_screen.h) at
+  // double index kLmfOffset: 768 float4 = 1536 doubles
+  const size_t nl = (size_t)nw + nr + ng;
+  std::vector<double> buf(kLmfOffset + 2 * 768, 0.0);
+  std::copy(all.begin(), all.end(), buf.begin());
+  float* lf = (float*)(buf.data() + kLmfOffset);
+  for (size_t i = 0; i < nl; i++) screen_landmark(all.data() + 3 * i, lf + 4 * i);
   if (c->d_lm) (void)hipFree(c->d_lm);
   c->d_lm = nullptr;
-  if (dalloc(c, &c->d_lm, all.size()) != MANTIS_OK) return MANTIS_ERR_OOM;
-  HIP_OK(hipMemcpy(c->d_lm, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice));
+  if (dalloc(c, &c->d_lm, buf.size()) != MANTIS_OK) return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpy(c->d_lm, buf.data(), sizeof(double) * buf.size(), hipMemcpyHostToDevice));
   c->nw = nw;
   c->nr = nr;
   c->ng = ng;
@@ -1037,7 +1013,7 @@ mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* al
   if (nj) {
     HIP_OK(hipMemcpyAsync(c->d_rwjobs, jobs.data(), sizeof(RigWJob) * nj, hipMemcpyHostToDevice, c->s));
     const RigWColors col{{255, 255, 255, 50, 85, 255, 50, 255, 85}};  // WHITE / RED / GREEN, Mantis3Params.h:40-42
-    Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+    Landmarks L = lmk_of(c);
     k_rig_weight<<<(unsigned)((nj + 3) / 4), 256, 0, c->s>>>(c->d_frames, L, c->d_rwjobs, (int)nj, col, c->d_rwout);
     HIP_OK(hipGetLastError());
     std::vector<double> o(2 * nj);
@@ -1118,14 +1094,10 @@ mantis_status process_batch_impl(Ctx* c, const mantis_image* cams, int32_t n_rig
   mantis_status st = process_frames(c, cams, n);
   if (st != MANTIS_OK) return st;
   const std::vector<double> Tbc = gather_tbc(cams, n);
-  int k = 0;
-  for (int r = 0; r < n_rigs; r++) {
-    const mantis_cam_result* cr = c->h_res + (size_t)r * cams_per_rig;
-    if (out) {
-      fuse_rig(&Tbc[16 * (size_t)r * cams_per_rig], cr, cams_per_rig, &out[r]);
-      for (int i = 0; i < cams_per_rig; i++) k += c->h_st[r * cams_per_rig + i].reaches_pf;
-      out[r].rng_state_after = c->h_states[k];
-    }
+  if (out) {
+    std::vector<int32_t> pf(n);
+    for (int f = 0; f < n; f++) pf[f] = c->h_st[f].reaches_pf;
+    mk::shard::rig_results(n_rigs, cams_per_rig, c->h_res, Tbc.data(), pf.data(), c->h_states, out);
   }
   if (out && (c->cfg.rig_weighting || pred_Twb)) {
     st = weight_rigs(c, n_rigs, cams_per_rig, c->h_res, Tbc.data(), nullptr, n, false, out, pred_Twb);
@@ -1143,12 +1115,7 @@ mantis_status process_batch_impl(Ctx* c, const mantis_image* cams, int32_t n_rig
 }  // namespace
 
 namespace {
-// one camera's result as exchanged between the ranks of a sharded rig
-struct ShardRec {
-  mantis_cam_result res;
-  double Tbc[16];
-  int32_t gidx, pad;
-};
+using ShardRec = mk::shard::Rec;  // one camera's result as exchanged between the ranks
 }  // namespace
 
 mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_cams, int32_t n_rigs, int32_t n_local,
@@ -1193,8 +1160,7 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
     c->sh_rec_bytes = rec_bytes;
   }
   std::vector<int32_t> gidx(n);
-  for (int r = 0; r < n_rigs; r++)
-    for (int j = 0; j < n_local; j++) gidx[(size_t)r * n_local + j] = r * cams_per_rig + cam_index[j];
+  mk::shard::global_indices(n_rigs, n_local, cam_index, cams_per_rig, gidx.data());
   Shard sh{ng, slots, gidx.data()};
   mantis_status st = process_frames(c, local_cams, n, &sh);
   if (st != MANTIS_OK) return st;
@@ -1218,22 +1184,14 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
   const ShardRec* recv = (const ShardRec*)(c->h_sh_rec + sbytes);
   std::vector<mantis_cam_result> all(ng);
   std::vector<double> Tall(16 * (size_t)ng);
-  std::vector<int> seen(ng, 0);
-  for (int i = 0; i < slots * c->nranks; i++) {
-    const int g = recv[i].gidx;
-    if (g < 0) continue;
-    if (g >= ng || seen[g]++) { c->err = "sharded rig: a camera is owned by two ranks"; return MANTIS_ERR_ARG; }
-    all[g] = recv[i].res;
-    std::memcpy(&Tall[16 * (size_t)g], recv[i].Tbc, sizeof(double) * 16);
+  std::vector<int32_t> seen(ng);
+  switch (mk::shard::merge_records(recv, slots * c->nranks, ng, all.data(), Tall.data(), seen.data())) {
+    case 0: break;
+    case 1: c->err = "sharded rig: a camera is owned by two ranks"; return MANTIS_ERR_ARG;
+    case 2: c->err = "sharded rig: a camera is owned by no rank"; return MANTIS_ERR_ARG;
+    default: c->err = "sharded rig: camera index out of range"; return MANTIS_ERR_ARG;
   }
-  for (int g = 0; g < ng; g++)
-    if (!seen[g]) { c->err = "sharded rig: a camera is owned by no rank"; return MANTIS_ERR_ARG; }
-  int k = 0;
-  for (int rr = 0; rr < n_rigs; rr++) {
-    fuse_rig(&Tall[16 * (size_t)rr * cams_per_rig], &all[(size_t)rr * cams_per_rig], cams_per_rig, &out[rr]);
-    for (int i = 0; i < cams_per_rig; i++) k += c->h_sh_flags[rr * cams_per_rig + i] ? 1 : 0;
-    out[rr].rng_state_after = c->h_states[k];
-  }
+  mk::shard::rig_results(n_rigs, cams_per_rig, all.data(), Tall.data(), c->h_sh_flags, c->h_states, out);
   if (c->cfg.rig_weighting) {
     st = weight_rigs(c, n_rigs, cams_per_rig, all.data(), Tall.data(), gidx.data(), n, true, out, nullptr);
     if (st != MANTIS_OK) return st;
@@ -1246,6 +1204,39 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
   if (cam_out) std::memcpy(cam_out, all.data(), sizeof(mantis_cam_result) * ng);
   for (int g = 0; g < ng; g++)
     if (all[g].status != 0) return MANTIS_ERR_CAPACITY;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_shard_gauss_offsets(void* ctx, const int32_t* pairs, int32_t npairs, int32_t n_global,
+                                         const int32_t* gidx, int32_t n_local, int32_t per_frame, int32_t* offsets,
+                                         int32_t* total) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !pairs || npairs < 0 || n_global < 0 || !gidx || n_local < 0 || n_local > c->F || per_frame < 0 ||
+      !offsets || !total)
+    return MANTIS_ERR_ARG;
+  if ((int64_t)per_frame * n_global > INT32_MAX) { c->err = "per_frame x n_global exceeds 2^31"; return MANTIS_ERR_ARG; }
+  for (int i = 0; i < n_local; i++)
+    if (gidx[i] < 0 || gidx[i] >= n_global) { c->err = "gidx outside [0, n_global)"; return MANTIS_ERR_ARG; }
+  int32_t *d_pairs = nullptr, *d_flags = nullptr, *d_gidx = nullptr, *d_total = nullptr;
+  struct Free {
+    std::vector<void*> p;
+    ~Free() { for (void* q : p) (void)hipFree(q); }
+  } fr;
+  if (dalloc(c, &d_pairs, (size_t)2 * npairs) || dalloc(c, &d_flags, (size_t)2 * n_global) ||
+      dalloc(c, &d_gidx, (size_t)n_local) || dalloc(c, &d_total, 1))
+    return MANTIS_ERR_OOM;
+  fr.p = {d_pairs, d_flags, d_gidx, d_total};
+  if (npairs) HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(int32_t) * 2 * npairs, hipMemcpyHostToDevice, c->s));
+  if (n_local) HIP_OK(hipMemcpyAsync(d_gidx, gidx, sizeof(int32_t) * n_local, hipMemcpyHostToDevice, c->s));
+  k_gauss_offsets_global<<<1, 1024, 0, c->s>>>(d_pairs, npairs, d_flags, n_global, c->d_st, d_gidx, n_local, per_frame,
+                                               d_total);
+  HIP_OK(hipGetLastError());
+  std::vector<FrameState> st(std::max(1, n_local));
+  if (n_local) HIP_OK(hipMemcpyAsync(st.data(), c->d_st, sizeof(FrameState) * n_local, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(total, d_total, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (int i = 0; i < n_local; i++) offsets[i] = st[i].gauss_offset;
   return MANTIS_OK;
 }
 
@@ -1414,9 +1405,9 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
     d_mask = c->d_mask;
   }
   HIP_OK(hipMemcpyAsync(d_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
-  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  Landmarks L = lmk_of(c);
   mark(c, "start");
-  k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, fast, d_err, d_np);
+  k_score_api<<<(n + kApiHyps - 1) / kApiHyps, 64 * kApiHyps, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, fast, d_err, d_np);
   mark(c, "score_api");
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(err, d_err, sizeof(double) * n, hipMemcpyDeviceToHost, c->s));

@@ -103,10 +103,10 @@ mantis_status score_argmin_impl(void* ctx, const mantis_image* img, const uint8_
     }
     if (n > 0) HIP_OK(hipMemcpyAsync(c->d_dense_c2w, c2w, sizeof(double) * 12 * n, hipMemcpyHostToDevice, c->s));
   }
-  Landmarks L{c->d_lm, c->nw, c->nr, c->ng};
+  Landmarks L = lmk_of(c);
   mark(c, "start");
   if (n > 0) {
-    k_score_api<<<(n + 3) / 4, 256, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, 1, c->d_dense_err,
+    k_score_api<<<(n + kApiHyps - 1) / kApiHyps, 64 * kApiHyps, 0, c->s>>>(c->d_frames, d_mask, L, d_c2w, n, 1, c->d_dense_err,
                                                c->d_dense_np);
     mark(c, "score_dense");
   }

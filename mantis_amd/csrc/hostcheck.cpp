@@ -17,6 +17,8 @@ static int g_jacobi_ff = 1;
 #include "mk_gn.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
+#include "mk_screen.h"
+#include "mk_shard.h"
 #include "mk_sort.h"
 
 extern "C" {
@@ -223,6 +225,73 @@ void hc_distort(const double* xyz, int n, const double* K, const double* D, doub
 void hc_undistort(const double* px, int n, const double* K, const double* D, double* out) {
   mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
   for (int i = 0; i < n; i++) mk::undistort(cm, px[2 * i], px[2 * i + 1], out + 2 * i, out + 2 * i + 1);
+}
+
+// FP32 projection screen (mk_screen.h) against the exact projection on n
+// (c2w, landmark) pairs: res[4 i] = screen state (0 out, 1 in, 2 unsure),
+// res[4 i + 1] = exact in-frame (z > 0 and inFrame), res[4 i + 2 / + 3] = the
+// screened pixel when in (else the exact pixel). Returns the number of
+// screened decisions that differ from the exact ones.
+int hc_screen_check(const double* c2w, const double* X, int n, const double* K, const double* D, int W, int H,
+                    int32_t* res) {
+  mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
+  const mk::ScreenCam sc = mk::screen_cam_from(cm);
+  int bad = 0;
+  for (int i = 0; i < n; i++) {
+    mk::Xf T;
+    for (int k = 0; k < 12; k++) (k < 9 ? T.R[k] : T.t[k - 9]) = c2w[12 * i + k];
+    double rp[3], u, v;
+    mk::xf_apply(T, X + 3 * i, rp);
+    mk::distort(cm, rp[0], rp[1], rp[2], &u, &v);
+    const bool in = rp[2] > 0 && mk::in_frame(u, v, H, W);
+    float xl[4];
+    mk::screen_landmark(X + 3 * i, xl);
+    int px = 0, py = 0;
+    const int st = mk::screen_project(mk::posef_from(T), xl[0], xl[1], xl[2], xl[3], sc, W, H, &px, &py);
+    res[4 * i] = st;
+    res[4 * i + 1] = in;
+    res[4 * i + 2] = st == mk::SCR_IN ? px : (in ? mk::cv_round(u) : 0);
+    res[4 * i + 3] = st == mk::SCR_IN ? py : (in ? mk::cv_round(v) : 0);
+    if ((st == mk::SCR_IN && (!in || px != mk::cv_round(u) || py != mk::cv_round(v))) || (st == mk::SCR_OUT && in))
+      bad++;
+  }
+  return bad;
+}
+
+// cross-rank bookkeeping of mantis_process_rig_sharded (mk_shard.h): the
+// library's own rules, for the gloo tests
+int hc_sizeof_cam_result(void) { return (int)sizeof(mantis_cam_result); }
+int hc_sizeof_result(void) { return (int)sizeof(mantis_result); }
+int hc_sizeof_shard_rec(void) { return (int)sizeof(mk::shard::Rec); }
+void hc_shard_global_indices(int n_rigs, int n_local, const int32_t* cam_index, int cams_per_rig, int32_t* gidx) {
+  mk::shard::global_indices(n_rigs, n_local, cam_index, cams_per_rig, gidx);
+}
+void hc_shard_pack_pairs(const int32_t* gidx, const int32_t* pf, int n_local, int slots, int32_t* pairs) {
+  mk::shard::pack_pairs(gidx, pf, n_local, slots, pairs);
+}
+int64_t hc_shard_offsets(const int32_t* pairs, int npairs, int ng, int64_t per, int32_t* flags, int64_t* offset) {
+  return mk::shard::offsets_from_pairs(pairs, npairs, ng, per, flags, offset);
+}
+// records of n local frames padded to slots (gidx -1)
+void hc_shard_make_recs(const mantis_cam_result* res, const double* Tbc, const int32_t* gidx, int n, int slots,
+                        mk::shard::Rec* out) {
+  for (int s = 0; s < slots; s++) {
+    std::memset(&out[s], 0, sizeof(out[s]));
+    out[s].gidx = -1;
+    if (s < n) {
+      out[s].res = res[s];
+      std::memcpy(out[s].Tbc, Tbc + 16 * (size_t)s, sizeof(double) * 16);
+      out[s].gidx = gidx[s];
+    }
+  }
+}
+int hc_shard_merge(const mk::shard::Rec* recv, int nrec, int ng, mantis_cam_result* all, double* Tall) {
+  std::vector<int32_t> seen(ng > 0 ? ng : 1);
+  return mk::shard::merge_records(recv, nrec, ng, all, Tall, seen.data());
+}
+void hc_rig_results(int n_rigs, int cams_per_rig, const mantis_cam_result* all, const double* Tall, const int32_t* pf,
+                    const uint64_t* states, mantis_result* out) {
+  mk::shard::rig_results(n_rigs, cams_per_rig, all, Tall, pf, states, out);
 }
 
 // rig GN accumulators of n_obs observations [cam, u, v, X, Y, Z] about T_w_b

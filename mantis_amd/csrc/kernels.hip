@@ -29,6 +29,7 @@
 #include "mk_gn.h"
 #include "mk_math.h"
 #include "mk_rpp.h"
+#include "mk_shard.h"
 #include "mk_sort.h"
 #include "mk_types.h"
 #include "synth.h"
@@ -2296,7 +2297,9 @@ __global__ __launch_bounds__(1024) void k_gauss_offsets_global(const int32_t* __
 struct Landmarks {
   const double* xyz;  // n x 3 (white, red, green in map order)
   int32_t nw, nr, ng;
+  const float4* xyzf;  // the same as the FP32 screen reads them: X, Y, Z, |X|_1 (mk_screen.h screen_landmark)
 };
+constexpr int kLmfOffset = 3 * 768;  // double index of the FP32 table in the map buffer (mantis_set_map)
 
 // Masks of the cleaned image (HypothesisEvaluation.h:364 img.copyTo(out, mask)):
 // none (original image), host bytes (standalone scoring API) or the k_morph
@@ -2306,182 +2309,38 @@ struct Landmarks {
 // [0, W)), test() extracts the bit. Out-of-buffer offsets (cvRound(px) == W /
 // == H) read as black; the caller never passes them in.
 struct MaskNone {
-  __device__ uint32_t word(long, int, int) const { return 1u; }
+  __device__ uint32_t word(int, int, int) const { return 1u; }
   __device__ bool test(uint32_t, int) const { return true; }
 };
 struct MaskBytes {
   const uint8_t* m;
-  __device__ uint32_t word(long lin, int, int) const { return m[lin]; }
+  __device__ uint32_t word(int lin, int, int) const { return m[lin]; }
   __device__ bool test(uint32_t w, int) const { return w != 0; }
 };
 // the frame's tiled mask plane staged in LDS (k_score_pf, when it fits
 // beside the kernel's static LDS: a 720p plane is 115 KB): ds_read lookups
 // instead of mask-word gathers through the L1
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+__device__ inline int tiled_word32(int y, int w, int WW) { return (((y >> 5) * WW + w) << 5) + (y & 31); }
 struct MaskLds {
   lds_cu32* m;
   int WW;
-  __device__ uint32_t word(long, int x, int y) const { return m[bits::tiled_word(y, x >> 5, WW)]; }
+  __device__ uint32_t word(int, int x, int y) const { return m[tiled_word32(y, x >> 5, WW)]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 struct MaskBits {
   const uint32_t* m;
   int WW, W;
-  __device__ uint32_t word(long, int x, int y) const { return m[bits::tiled_word(y, x >> 5, WW)]; }
+  __device__ uint32_t word(int, int x, int y) const { return m[tiled_word32(y, x >> 5, WW)]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 // B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
 // last pixel of the frame reads one byte early so the load stays in the buffer.
-__device__ inline uint32_t load_bgr(const uint8_t* bgr, long lin, long npx) {
+__device__ inline uint32_t load_bgr(const uint8_t* bgr, int lin, int npx) {
   const bool last = lin == npx - 1;
   typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;  // unaligned dword
-  const uint32_t v = *(gu32u*)(bgr + 3 * lin - (last ? 1 : 0));
+  const uint32_t v = *(gu32u*)(bgr + (3 * lin - (last ? 1 : 0)));
   return last ? (v >> 8) : v;
-}
-
-// one wave scores one hypothesis over all landmarks (64 lanes, int64 sum).
-// Software-pipelined: kFastUnroll landmarks per lane are projected first, then
-// their mask-word and pixel loads are issued together (the pixel load does
-// not wait for the mask bit), then the terms are summed -- the gathers of a
-// group overlap instead of costing two L2 round trips per landmark.
-// Term of a landmark with z > 0 and inFrame (computePointErrorFAST,
-// HypothesisEvaluation.h:218-227 on the cleaned image): the squared distance
-// of its BGR to white, or 3 * 255^2 when the pixel is masked out or lies past
-// the end of the buffer (linear-offset read of cvRound(px) == W / == H).
-#ifndef MK_FAST_PROJ
-#define MK_FAST_PROJ 0
-#endif
-#ifndef MK_FAST_UNROLL
-#define MK_FAST_UNROLL 3
-#endif
-constexpr int kFastUnroll = MK_FAST_UNROLL;
-// One group of kFastUnroll landmarks per lane (l0, l0 + 64, ...): projected,
-// mask looked up, and the pixel loads issued (only where the mask bit is set)
-// -- fast_group_sum consumes them.
-struct FastGroup {
-  uint32_t pv[kFastUnroll];
-  bool in[kFastUnroll], hit[kFastUnroll];
-};
-template <class MK>
-__device__ inline void fast_group_issue(const Xf& c2w, const double* lm, int l0, int nl, const Cam& cm,
-                                        const uint8_t* bgr, const MK& mask, int W, int H, long npx, FastGroup& g) {
-  long lin[kFastUnroll];
-  int px[kFastUnroll], py[kFastUnroll];
-  bool ok[kFastUnroll];
-  double pu[kFastUnroll], pv_[kFastUnroll];
-  bool zp[kFastUnroll];
-  // branch-free projections (z <= 0 or an off-frame point just fails the
-  // flags), so the kFastUnroll independent FP64 chains interleave
-  bool sure = true;
-#pragma unroll
-  for (int k = 0; k < kFastUnroll; k++) {
-    const int l = l0 + 64 * k;
-    const double* X = lm + 3 * (l < nl ? l : nl - 1);  // nl > lb: a valid landmark
-    double rp[3];
-    xf_apply(c2w, X, rp);
-    zp[k] = rp[2] > 0;
-#if MK_FAST_PROJ
-    sure &= distort_fast(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k], W, H) || !zp[k];
-#else
-    distort(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k]);
-#endif
-  }
-  if (!__all(sure)) {  // MK_FAST_PROJ: the rare uncertain projections redone exactly
-#pragma unroll 1
-    for (int k = 0; k < kFastUnroll; k++) {
-      const int l = l0 + 64 * k;
-      if (!zp[k]) continue;
-      double rp[3];
-      xf_apply(c2w, lm + 3 * (l < nl ? l : nl - 1), rp);
-      distort(cm, rp[0], rp[1], rp[2], &pu[k], &pv_[k]);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kFastUnroll; k++) {
-    const int l = l0 + 64 * k;
-    const double u = pu[k], v = pv_[k];
-    g.in[k] = l < nl && zp[k] && in_frame(u, v, H, W);
-    int x = g.in[k] ? cv_round(u) : 0, y = g.in[k] ? cv_round(v) : 0;
-    long li = (long)y * W + x;
-    ok[k] = g.in[k] && li >= 0 && li < npx;
-    if (x >= W) { x -= W; y += 1; }  // cvRound(u) == W: next row (linear offset)
-    if (!ok[k]) { li = 0; x = 0; y = 0; }
-    lin[k] = li;
-    px[k] = x;
-    py[k] = y;
-  }
-  uint32_t mw[kFastUnroll];
-#pragma unroll
-  for (int k = 0; k < kFastUnroll; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
-#pragma unroll
-  for (int k = 0; k < kFastUnroll; k++) {
-    g.hit[k] = ok[k] && mask.test(mw[k], px[k]);
-    g.pv[k] = g.hit[k] ? load_bgr(bgr, lin[k], npx) : 0u;
-  }
-}
-__device__ inline void fast_group_sum(const FastGroup& g, long long& s, int& n) {
-#pragma unroll
-  for (int k = 0; k < kFastUnroll; k++) {
-    if (!g.in[k]) continue;
-    n++;
-    int e = 3 * 255 * 255;
-    if (g.hit[k]) {
-      const int b = (int)(g.pv[k] & 0xffu), gg = (int)((g.pv[k] >> 8) & 0xffu), r = (int)((g.pv[k] >> 16) & 0xffu);
-      const int e0 = b - 255, e1 = gg - 255, e2 = r - 255;
-      e = e0 * e0 + e1 * e1 + e2 * e2;
-    }
-    s += e;
-  }
-}
-// Raw sums over the landmarks [lb, le): integer error sum and count (wave-reduced).
-// MK_SCORE_PIPE 1 software-pipelines across groups (a group's pixel loads
-// consumed only after the next group is projected): measured slower, 22.2 vs
-// 20.7 ms for the score stage, so off.
-#ifndef MK_SCORE_PIPE
-#define MK_SCORE_PIPE 0
-#endif
-template <class MK>
-__device__ inline void wave_sums_fast(const Xf& c2w, const double* lm, int lb, int le, const Cam& cm,
-                                      const uint8_t* bgr, const MK& mask, int W, int H, long long& s_out, int& n_out) {
-  const int lane = threadIdx.x & 63;
-  const long npx = (long)W * H;
-  long long s = 0;
-  int n = 0;
-#if MK_SCORE_PIPE
-  FastGroup prev;
-  bool have = false;
-  for (int l0 = lb + lane; l0 < le; l0 += 64 * kFastUnroll) {
-    FastGroup cur;
-    fast_group_issue(c2w, lm, l0, le, cm, bgr, mask, W, H, npx, cur);
-    if (have) fast_group_sum(prev, s, n);
-    prev = cur;
-    have = true;
-  }
-  if (have) fast_group_sum(prev, s, n);
-#else
-  for (int l0 = lb + lane; l0 < le; l0 += 64 * kFastUnroll) {
-    FastGroup g;
-    fast_group_issue(c2w, lm, l0, le, cm, bgr, mask, W, H, npx, g);
-    fast_group_sum(g, s, n);
-  }
-#endif
-  for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o);
-    n += __shfl_xor(n, o);
-  }
-  s_out = s;
-  n_out = n;
-}
-template <class MK>
-__device__ inline void wave_score_fast(const Xf& c2w, const double* lm, int nl, const Cam& cm, const uint8_t* bgr,
-                                       const MK& mask, int W, int H, double* err_out, int* n_out) {
-  long long s;
-  int n;
-  wave_sums_fast(c2w, lm, 0, nl, cm, bgr, mask, W, H, s, n);
-  if ((threadIdx.x & 63) == 0) {
-    *n_out = n;
-    *err_out = n <= 0 ? DBL_MAX : (double)s / ((double)n * 1.1);
-  }
 }
 
 // COLOR (slow) error of one hypothesis (computePointError, HypothesisEvaluation.h:
@@ -2607,6 +2466,164 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
   }
 }
 
+// ------------------------------------------------------ screened fast scoring
+// Every landmark is first projected with the FP32 screen (mk_screen.h), whose
+// decision (z > 0, inFrame, cvRound pixel) is taken where it is certain; the
+// rare unsure landmarks (about 1 % of the in-frame ones on the bench frames,
+// tools/check_screen.hip) are appended to a per-block queue in LDS as
+// (tag, landmark) and recomputed with the exact FP64 projection by the whole
+// block after the screened pass -- full waves, whichever wave pushed them --
+// their integer terms added into the tag's sums with LDS atomics. The sums are
+// exact integers, so the order is free and the errors are identical to the
+// exact path's (HypothesisEvaluation.h:107-158, 218-227). A wave that finds the
+// queue full recomputes its own unsure landmarks in place.
+#ifndef MK_SCR_UNROLL
+#define MK_SCR_UNROLL 6
+#endif
+constexpr int kScrUnroll = MK_SCR_UNROLL;  // landmarks per lane in flight (their pixel loads overlap)
+struct UQueue {
+  uint32_t* e;  // entries: tag << 16 | landmark
+  int32_t* n;   // entries pushed (past cap: those were recomputed in place)
+  int cap;
+};
+// exact term of one landmark: the FP64 path the screen stands in for. Not
+// inlined: it runs for ~1 % of the landmarks, and inlined its FP64 constants
+// (mk_dmath.h atan coefficients in SGPRs) stay live across the screened loop
+// and spill it.
+template <class MK>
+__device__ __attribute__((noinline)) bool exact_term(const Xf& T, const double* X, const Cam& cm, int W, int H, const uint8_t* bgr,
+                                  const MK& mask, int& e) {
+  double rp[3], u, v;
+  xf_apply(T, X, rp);
+  distort(cm, rp[0], rp[1], rp[2], &u, &v);
+  if (!(rp[2] > 0 && in_frame(u, v, H, W))) return false;
+  const int npx = W * H;
+  int x = cv_round(u), y = cv_round(v);
+  const int li = y * W + x;
+  const bool ok = li >= 0 && li < npx;
+  if (x >= W) { x -= W; y += 1; }  // cvRound(u) == W: next row (linear offset)
+  e = 3 * 255 * 255;
+  if (ok && mask.test(mask.word(li, x, y), x)) {
+    const uint32_t pv = load_bgr(bgr, li, npx);
+    const int b = (int)(pv & 0xffu) - 255, g = (int)((pv >> 8) & 0xffu) - 255, r = (int)((pv >> 16) & 0xffu) - 255;
+    e = b * b + g * g + r * r;
+  }
+  return true;
+}
+// wave-uniform FP32 pose into SGPRs
+__device__ inline float rfl(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ inline PoseF rfl(const PoseF& P) {
+  PoseF u;
+#pragma unroll
+  for (int k = 0; k < 9; k++) u.R[k] = rfl(P.R[k]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) u.t[k] = rfl(P.t[k]);
+  u.tn = rfl(P.tn);
+  u.pad[0] = u.pad[1] = u.pad[2] = 0.f;
+  return u;
+}
+// One wave, pose P (wave-uniform), landmarks [lb, le): integer error sum and
+// count of the screened landmarks (wave-reduced); unsure ones go to q under
+// `tag` (Tx, lmd, cmp: the exact pose, the FP64 landmarks and the camera, read
+// only when the queue is full). States: 0 out, 1 in frame (pixel in the
+// buffer), 2 unsure, 3 in frame past the end of the buffer (cvRound == rows:
+// reads as black).
+template <int U, class MK>
+__device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int lb, int le, const ScreenCam& sc, int W,
+                                        int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
+                                        const double* lmd, const Cam* cmp, long long& s_out, int& n_out) {
+  const int lane = threadIdx.x & 63;
+  const int last = W * H - 1;
+  int s = 0, n = 0;  // per lane: <= 12 landmarks x 3 * 255^2, exact in int32
+  for (int b0 = lb; b0 < le; b0 += 64 * U) {  // wave-uniform trips
+    int st[U], lin[U], px[U], py[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const int l = b0 + lane + 64 * k;
+      const float4 L = lmf[l < le ? l : le - 1];
+      int x, y;
+      const int t = screen_project(P, L.x, L.y, L.z, L.w, sc, W, H, &x, &y);
+      st[k] = l < le ? t : SCR_OUT;
+      const bool in = st[k] == SCR_IN;  // interior pixel: no wrap, inside the buffer
+      px[k] = in ? x : 0;
+      py[k] = in ? y : 0;
+      lin[k] = in ? y * W + x : 0;
+    }
+    // mask words and pixel loads issued unconditionally (address 0 when not
+    // needed), so the U loads of a lane are in flight together
+    uint32_t mw[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+    uint32_t pv[U];
+    int hm[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const bool hit = st[k] == SCR_IN && mask.test(mw[k], px[k]);
+      hm[k] = hit ? -1 : 0;
+      const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
+      typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
+      pv[k] = *(gu32u*)(bgr + off);
+    }
+    // the terms as masks, not selects: every loaded value is consumed, so the
+    // compiler keeps the U loads unconditional (in flight together) instead
+    // of sinking each into a branch with its own wait
+    int cu = 0;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      cu += st[k] == SCR_UNSURE;
+      const uint32_t v = lin[k] == last ? pv[k] >> 8 : pv[k];
+      const uint32_t d = ~v & 0xffffffu;  // 255 - B, 255 - G, 255 - R as bytes
+      const int term = (int)__builtin_amdgcn_udot4(d, d, 0u, false);  // sum of their squares (v_dot4_u32_u8)
+      constexpr int kBlack = 3 * 255 * 255;  // masked out
+      const int e = kBlack ^ ((term ^ kBlack) & hm[k]);
+      const int im = st[k] == SCR_IN ? -1 : 0;
+      n -= im;
+      s += e & im;
+    }
+    if (__ballot(cu > 0)) {  // wave-aggregated queue append: one LDS atomic
+      const int incl = wave_incl_scan(cu, lane);
+      int base = 0;
+      if (lane == 63) base = atomicAdd(q.n, incl);
+      base = __shfl(base, 63);
+      int idx = base + incl - cu;
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        if (st[k] != SCR_UNSURE) continue;
+        const int l = b0 + lane + 64 * k;
+        if (idx < q.cap) {
+          q.e[idx] = ((uint32_t)tag << 16) | (uint32_t)l;
+        } else {
+          int e;
+          if (exact_term(*Tx, lmd + 3 * l, *cmp, W, H, bgr, mask, e)) { n++; s += e; }
+        }
+        idx++;
+      }
+    }
+  }
+  long long s64 = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    s64 += __shfl_xor(s64, o);
+    n += __shfl_xor(n, o);
+  }
+  s_out = s64;
+  n_out = n;
+}
+// the block recomputes the queued landmarks exactly: add(tag, term) for those
+// in frame (pose_of(tag) = the tag's FP64 c2w)
+template <class MK, class PoseOf, class Add>
+__device__ inline void block_drain(UQueue q, const double* lmd, const Cam* cmp, int W, int H, const uint8_t* bgr,
+                                   const MK& mask, const PoseOf& pose_of, const Add& add) {
+  const int n = min(*q.n, q.cap);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t en = q.e[i];
+    const int tag = (int)(en >> 16), l = (int)(en & 0xffffu);
+    int e;
+    if (exact_term(pose_of(tag), lmd + 3 * l, *cmp, W, H, bgr, mask, e)) add(tag, e);
+  }
+}
+
 // Scoring is three kernels per frame batch (one block per frame each), so
 // the particle filter -- 500 of the ~620 scored hypotheses of a frame -- runs
 // in a lean kernel whose register budget is not set by the sorting and
@@ -2633,6 +2650,8 @@ constexpr int kScoreTail = MK_SCORE_TAIL_THREADS;
 #define MK_SCORE_INIT_THREADS 1024
 #endif
 constexpr int kScoreInit = MK_SCORE_INIT_THREADS;  // k_score_init block size
+// unsure-landmark queues (entries per block pass): init (C hypotheses), particle filter (one iteration), tail (81 shifts)
+constexpr int kInitQueue = 1024, kPfQueue = 1024, kTailQueue = 512;
 static_assert(kScoreTail >= 128 && kScoreTail % 64 == 0, "score tail block");
 
 struct PoseLds {
@@ -2682,8 +2701,12 @@ __global__ __launch_bounds__(NT) void k_score_init(
   mantis_cam_result& R = res[f];
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
-  __shared__ double lm[3 * 768];
+  __shared__ float4 lmf[768];
   __shared__ ErrIdx ei[kMaxHyps];
+  __shared__ unsigned long long hs[kMaxHyps];  // per hypothesis: integer error sum, count
+  __shared__ int32_t hn[kMaxHyps];
+  __shared__ uint32_t uqe[kInitQueue];
+  __shared__ int32_t uqn;
   __shared__ PoseLds cur;
   __shared__ int32_t nsc;
   if (!st[f].reaches_pf) {
@@ -2699,25 +2722,41 @@ __global__ __launch_bounds__(NT) void k_score_init(
     }
     return;
   }
-  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
+  if (tid == 0) uqn = 0;
   __syncthreads();
   HypRec* Hh = hyps + (size_t)f * kMaxHyps;
   const int C = st[f].n_hyps;
-  // evaluateHypotheses(hyps, cleaned)
-  for (int h = wave; h < C; h += (NT / 64)) {
-    double e;
+  // evaluateHypotheses(hyps, cleaned): screened pass, then the unsure landmarks exactly
+  const UQueue q{uqe, &uqn, kInitQueue};
+  for (int h = __builtin_amdgcn_readfirstlane(wave); h < C; h += (NT / 64)) {
+    long long s;
     int n;
-    wave_score_fast(Hh[h].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
+    wave_sums_screen<kScrUnroll>(posef_from(Hh[h].c2w), lmf, 0, nl, fd.scam, W, H, fd.bgr, mask, q, h,
+                                 &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
     if (lane == 0) {
-      Hh[h].error = e;
-      Hh[h].nproj = n;
-      ei[h].e = e;
-      ei[h].i = h;
-      for (int k = 0; k < 9; k++) D.hyp_c2w[h][k] = Hh[h].c2w.R[k];
-      for (int k = 0; k < 3; k++) D.hyp_c2w[h][9 + k] = Hh[h].c2w.t[k];
-      D.hyp_err[h] = e;
-      D.hyp_n[h] = n;
+      hs[h] = (unsigned long long)s;
+      hn[h] = n;
     }
+  }
+  __syncthreads();
+  block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return Hh[t].c2w; },
+              [&](int t, int e) {
+                atomicAdd(&hs[t], (unsigned long long)e);
+                atomicAdd(&hn[t], 1);
+              });
+  __syncthreads();
+  for (int h = tid; h < C; h += NT) {
+    const int n = hn[h];
+    const double e = n <= 0 ? DBL_MAX : (double)(long long)hs[h] / ((double)n * 1.1);
+    Hh[h].error = e;
+    Hh[h].nproj = n;
+    ei[h].e = e;
+    ei[h].i = h;
+    for (int k = 0; k < 9; k++) D.hyp_c2w[h][k] = Hh[h].c2w.R[k];
+    for (int k = 0; k < 3; k++) D.hyp_c2w[h][9 + k] = Hh[h].c2w.t[k];
+    D.hyp_err[h] = e;
+    D.hyp_n[h] = n;
   }
   __syncthreads();
   // getBestNHypotheses(1): std::sort, keep back(). When the minimum error is
@@ -2790,15 +2829,18 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   }
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
-  __shared__ double lm[3 * 768];
+  __shared__ float4 lmf[768];
   __shared__ Xf Pc[96], Pw[96];
+  __shared__ PoseF Pf[96];
   __shared__ double Pe[96];
-  __shared__ long long Ps[96 * SPLIT];
+  __shared__ unsigned long long Ps[96 * SPLIT];
   __shared__ int32_t Pn[96 * SPLIT];
+  __shared__ uint32_t uqe[kPfQueue];
+  __shared__ int32_t uqn;
   constexpr int kW = NT / 64;
   __shared__ Xf cur_c2w, cur_w2c;
   __shared__ double cur_err;
-  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
   if (tid == 0) {
     cur_c2w = sst[f].cur.c2w;
     cur_w2c = sst[f].cur.w2c;
@@ -2806,6 +2848,9 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   }
   __syncthreads();
   const float* gs = gauss + st[f].gauss_offset;
+  const UQueue q{uqe, &uqn, kPfQueue};
+  const MaskLds mlds{(lds_cu32*)pf_mask, bits::words(W)};
+  const MaskBits mglb{fm, bits::words(W), W};
   for (int it = 0; it < iterations; it++) {
     if (tid < particles) {
       const float* g6 = gs + (size_t)(it * particles + tid) * 6;
@@ -2815,9 +2860,12 @@ __global__ __launch_bounds__(NT) void k_score_pf(
       basis_from_rpy_small(roll, pitch, yaw, rnd.R);  // |angle| < 2 rad: float gaussian x 0.03
       rnd.t[0] = tx; rnd.t[1] = ty; rnd.t[2] = tz;
       const Xf w2c = xf_mul(cur_w2c, rnd);
+      const Xf c2w = xf_inverse(w2c);
       Pw[tid] = w2c;
-      Pc[tid] = xf_inverse(w2c);
+      Pc[tid] = c2w;
+      Pf[tid] = posef_from(c2w);
     }
+    if (tid == 0) uqn = 0;
     __syncthreads();
     // SPLIT waves per particle (landmark slices; integer sums, so the
     // partials combine exactly in any order)
@@ -2826,22 +2874,30 @@ __global__ __launch_bounds__(NT) void k_score_pf(
       long long sum;
       int cnt;
       if (LM)
-        wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr,
-                       MaskLds{(lds_cu32*)pf_mask, bits::words(W)}, W, H, sum, cnt);
+        wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr,
+                                     mlds, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
       else
-        wave_sums_fast(rfl(Pc[j]), lm, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.cam, fd.bgr,
-                       MaskBits{fm, bits::words(W), W}, W, H, sum, cnt);
+        wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr,
+                                     mglb, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
       if (lane == 0) {
-        Ps[task] = sum;
+        Ps[task] = (unsigned long long)sum;
         Pn[task] = cnt;
       }
     }
+    __syncthreads();
+    const auto pose_of = [&](int t) -> const Xf& { return Pc[t]; };
+    const auto add = [&](int t, int e) {
+      atomicAdd(&Ps[t * SPLIT], (unsigned long long)e);
+      atomicAdd(&Pn[t * SPLIT], 1);
+    };
+    if (LM) block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mlds, pose_of, add);
+    else block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mglb, pose_of, add);
     __syncthreads();
     if (tid < particles) {
       long long sum = 0;
       int cnt = 0;
       for (int h = 0; h < SPLIT; h++) {
-        sum += Ps[tid * SPLIT + h];
+        sum += (long long)Ps[tid * SPLIT + h];
         cnt += Pn[tid * SPLIT + h];
       }
       Pe[tid] = cnt <= 0 ? DBL_MAX : (double)sum / ((double)cnt * 1.1);
@@ -2896,7 +2952,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   mantis_cam_result& R = res[f];
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
-  __shared__ double lm[3 * 768];
+  __shared__ float4 lmf[768];
   __shared__ PoseLds P[96];
   __shared__ ErrIdx ei[96];
   __shared__ ColorLds cls[(NT / 64)];
@@ -2904,8 +2960,13 @@ __global__ __launch_bounds__(NT) void k_score_final(
   __shared__ double shv[9];
   __shared__ double yerr[4];
   __shared__ int32_t nsc;
-  for (int i = tid; i < 3 * nl && i < 3 * 768; i += blockDim.x) lm[i] = lmk.xyz[i];
+  __shared__ unsigned long long hs[96];
+  __shared__ int32_t hn[96];
+  __shared__ uint32_t uqe[kTailQueue];
+  __shared__ int32_t uqn;
+  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
   if (tid == 0) {
+    uqn = 0;
     cur = sst[f].cur;
     nsc = sst[f].nsc;
     // shift values accumulate in double exactly as the reference loop does
@@ -2926,16 +2987,31 @@ __global__ __launch_bounds__(NT) void k_score_final(
     P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
   }
   __syncthreads();
-  for (int j = wave; j < NS; j += (NT / 64)) {
-    double e;
+  const UQueue q{uqe, &uqn, kTailQueue};
+  for (int j = __builtin_amdgcn_readfirstlane(wave); j < NS; j += (NT / 64)) {
+    long long sum;
     int n;
-#ifdef MK_DIAG_NO_SHIFTS  // timing diagnostic only: wrong results
-    e = 1.0 + j;
-    n = 1;
-#else
-    wave_score_fast(P[j].c2w, lm, nl, fd.cam, fd.bgr, mask, W, H, &e, &n);
-#endif
-    if (lane == 0) { P[j].err = e; ei[j].e = e; ei[j].i = j; D.shift_err[j] = e; }
+    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, 0, nl, fd.scam, W, H, fd.bgr, mask, q, j, &P[j].c2w,
+                                 lmk.xyz, &frames[f].cam, sum, n);
+    if (lane == 0) {
+      hs[j] = (unsigned long long)sum;
+      hn[j] = n;
+    }
+  }
+  __syncthreads();
+  block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return P[t].c2w; },
+              [&](int t, int e) {
+                atomicAdd(&hs[t], (unsigned long long)e);
+                atomicAdd(&hn[t], 1);
+              });
+  __syncthreads();
+  if (tid < NS) {
+    const int n = hn[tid];
+    const double e = n <= 0 ? DBL_MAX : (double)(long long)hs[tid] / ((double)n * 1.1);
+    P[tid].err = e;
+    ei[tid].e = e;
+    ei[tid].i = tid;
+    D.shift_err[tid] = e;
   }
   __syncthreads();
   // getBestNHypotheses(20) (HypothesisEvaluation.h:484-518): std::sort by
@@ -2991,7 +3067,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
     }
   }
   __syncthreads();
-  const double* green = lm + 3 * (lmk.nw + lmk.nr);
+  const double* green = lmk.xyz + 3 * (lmk.nw + lmk.nr);
   __shared__ double yset_err[80];
   for (int j = wave; j < 80; j += (NT / 64)) {
     double e;
@@ -3130,23 +3206,69 @@ __global__ __launch_bounds__(256) void k_rig_weight(const FrameDesc* __restrict_
 }
 
 // ================================================ standalone scoring API
-__global__ __launch_bounds__(256) void k_score_api(const FrameDesc* __restrict__ frames, const uint8_t* mask,
-                                                   Landmarks lmk, const double* __restrict__ c2w, int n, int fast,
-                                                   double* __restrict__ err, int32_t* __restrict__ nproj) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int h = blockIdx.x * 4 + wave;
-  __shared__ ColorLds cls[4];
-  if (h >= n) return;
+// Fast errors: kApiHyps hypotheses per block (one wave each, screened, one
+// drain per block); COLOR errors: one wave per hypothesis, exact FP64.
+constexpr int kApiHyps = 16, kApiQueue = 512;
+template <class MK>
+__device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const MK& mask, Landmarks lmk,
+                                      const double* c2w, int n, double* err, int32_t* nproj) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int h0 = blockIdx.x * kApiHyps, h = h0 + wave;
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  __shared__ float4 lmf[768];
+  __shared__ unsigned long long hs[kApiHyps];
+  __shared__ int32_t hn[kApiHyps];
+  __shared__ uint32_t uqe[kApiQueue];
+  __shared__ int32_t uqn;
+  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
+  if (tid == 0) uqn = 0;
+  __syncthreads();
+  const UQueue q{uqe, &uqn, kApiQueue};
+  if (h < n) {
+    const Xf* T = (const Xf*)(c2w + 12 * (size_t)__builtin_amdgcn_readfirstlane(h));  // R[9], t[3] = mk::Xf
+    long long s;
+    int c;
+    wave_sums_screen<kScrUnroll>(posef_from(*T), lmf, 0, nl, fd.scam, fd.w, fd.h, fd.bgr, mask, q, wave, T,
+                                 lmk.xyz, cmp, s, c);
+    if (lane == 0) {
+      hs[wave] = (unsigned long long)s;
+      hn[wave] = c;
+    }
+  }
+  __syncthreads();
+  block_drain(q, lmk.xyz, cmp, fd.w, fd.h, fd.bgr, mask,
+              [&](int t) -> const Xf& { return *(const Xf*)(c2w + 12 * (size_t)(h0 + t)); },
+              [&](int t, int e) {
+                atomicAdd(&hs[t], (unsigned long long)e);
+                atomicAdd(&hn[t], 1);
+              });
+  __syncthreads();
+  if (tid < kApiHyps && h0 + tid < n) {
+    const int c = hn[tid];
+    err[h0 + tid] = c <= 0 ? DBL_MAX : (double)(long long)hs[tid] / ((double)c * 1.1);
+    nproj[h0 + tid] = c;
+  }
+}
+__global__ __launch_bounds__(64 * kApiHyps) void k_score_api(const FrameDesc* __restrict__ frames, const uint8_t* mask,
+                                                             Landmarks lmk, const double* __restrict__ c2w, int n,
+                                                             int fast, double* __restrict__ err,
+                                                             int32_t* __restrict__ nproj) {
   const FrameDesc fd = frames[0];
+  if (fast) {
+    if (mask) score_api_fast(fd, &frames[0].cam, MaskBytes{mask}, lmk, c2w, n, err, nproj);
+    else score_api_fast(fd, &frames[0].cam, MaskNone{}, lmk, c2w, n, err, nproj);
+    return;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = blockIdx.x * kApiHyps + wave;
+  __shared__ ColorLds cls[kApiHyps];
+  if (h >= n) return;
   Xf T;
   for (int k = 0; k < 9; k++) T.R[k] = c2w[12 * h + k];
   for (int k = 0; k < 3; k++) T.t[k] = c2w[12 * h + 9 + k];
   double e;
   int np;
-  const int nl = lmk.nw + lmk.nr + lmk.ng;
-  if (fast && mask) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskBytes{mask}, fd.w, fd.h, &e, &np);
-  else if (fast) wave_score_fast(T, lmk.xyz, nl, fd.cam, fd.bgr, MaskNone{}, fd.w, fd.h, &e, &np);
-  else wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, &cls[wave], &e, &np);
+  wave_score_color(T, lmk.xyz + 3 * (lmk.nw + lmk.nr), lmk.ng, fd.cam, fd.bgr, fd.w, fd.h, &cls[wave], &e, &np);
   if (lane == 0) {
     err[h] = e;
     nproj[h] = np;

@@ -5,6 +5,7 @@
 
 #include "../../include/mantis.h"
 #include "mk_math.h"
+#include "mk_screen.h"
 
 namespace mk {
 
@@ -18,6 +19,7 @@ struct FrameDesc {
   const uint8_t* bgr;  // contiguous BGR8, stride 3W
   int32_t w, h;
   Cam cam;
+  ScreenCam scam;      // FP32 projection screen of the fast scorers (mk_screen.h)
 };
 
 struct Border {  // one Suzuki–Abe border in the parallel formulation

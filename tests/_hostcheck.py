@@ -33,6 +33,18 @@ def lib():
         L.hc_gn_accumulate.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
         L.hc_quad_gn.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
                                  C.c_void_p, C.c_void_p]
+        vp = C.c_void_p
+        L.hc_shard_global_indices.argtypes = [C.c_int, C.c_int, vp, C.c_int, vp]
+        L.hc_shard_pack_pairs.argtypes = [vp, vp, C.c_int, C.c_int, vp]
+        L.hc_shard_make_recs.argtypes = [vp, vp, vp, C.c_int, C.c_int, vp]
+        L.hc_shard_merge.argtypes = [vp, C.c_int, C.c_int, vp, vp]
+        L.hc_rig_results.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp]
+        L.hc_shard_offsets.restype = C.c_int64
+        L.hc_shard_offsets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
+        L.hc_shard_merge.restype = C.c_int
+        L.hc_screen_check.restype = C.c_int
+        L.hc_screen_check.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                      C.c_void_p]
         _lib = L
     return _lib
 
@@ -153,3 +165,75 @@ def quad_gn(R, t, img, obj, iters):
     lib().hc_quad_gn(n, R.ctypes.data, t.ctypes.data, img.ctypes.data, obj.ctypes.data, iters, steps.ctypes.data,
                      c0.ctypes.data, c1.ctypes.data)
     return R.reshape(n, 3, 3), t, steps, c0, c1
+
+
+def screen_check(c2w, X, K, D, W, H):
+    """FP32 projection screen vs the exact projection (host build of
+    mk_screen.h): (mismatches, res[n, 4] = state, exact in-frame, px, py)."""
+    c2w = np.ascontiguousarray(c2w, np.float64).reshape(-1, 12)
+    X = np.ascontiguousarray(X, np.float64).reshape(-1, 3)
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    res = np.zeros((len(X), 4), np.int32)
+    bad = lib().hc_screen_check(c2w.ctypes.data, X.ctypes.data, len(X), K.ctypes.data, D.ctypes.data, W, H,
+                                res.ctypes.data)
+    return bad, res
+
+
+# cross-rank bookkeeping of mantis_process_rig_sharded (mantis_amd/csrc/mk_shard.h)
+def sizes():
+    L = lib()
+    return L.hc_sizeof_cam_result(), L.hc_sizeof_result(), L.hc_sizeof_shard_rec()
+
+
+def shard_global_indices(n_rigs, cam_index, cams_per_rig):
+    ci = np.ascontiguousarray(cam_index, np.int32)
+    g = np.zeros(n_rigs * len(ci), np.int32)
+    lib().hc_shard_global_indices(n_rigs, len(ci), ci.ctypes.data, cams_per_rig, g.ctypes.data)
+    return g
+
+
+def shard_pack_pairs(gidx, pf, slots):
+    gidx = np.ascontiguousarray(gidx, np.int32)
+    pf = np.ascontiguousarray(pf, np.int32)
+    pairs = np.zeros(2 * slots, np.int32)
+    lib().hc_shard_pack_pairs(gidx.ctypes.data, pf.ctypes.data, len(gidx), slots, pairs.ctypes.data)
+    return pairs
+
+
+def shard_offsets(pairs, n_global, per):
+    pairs = np.ascontiguousarray(pairs, np.int32)
+    flags = np.zeros(n_global, np.int32)
+    off = np.zeros(n_global, np.int64)
+    tot = lib().hc_shard_offsets(pairs.ctypes.data, len(pairs) // 2, n_global, per, flags.ctypes.data, off.ctypes.data)
+    return flags, off, tot
+
+
+def shard_make_recs(cam_bytes, tbc, gidx, slots):
+    cb = np.ascontiguousarray(cam_bytes, np.uint8)
+    tb = np.ascontiguousarray(tbc, np.float64).reshape(-1, 16)
+    g = np.ascontiguousarray(gidx, np.int32)
+    rs = sizes()[2]
+    out = np.zeros(slots * rs, np.uint8)
+    lib().hc_shard_make_recs(cb.ctypes.data, tb.ctypes.data, g.ctypes.data, len(g), slots, out.ctypes.data)
+    return out
+
+
+def shard_merge(recs, n_global):
+    recs = np.ascontiguousarray(recs, np.uint8)
+    cs, _, rs = sizes()
+    allb = np.zeros(n_global * cs, np.uint8)
+    tall = np.zeros((n_global, 16))
+    code = lib().hc_shard_merge(recs.ctypes.data, len(recs) // rs, n_global, allb.ctypes.data, tall.ctypes.data)
+    return code, allb.reshape(n_global, cs), tall
+
+
+def rig_results(n_rigs, cams_per_rig, all_bytes, tall, pf, states):
+    ab = np.ascontiguousarray(all_bytes, np.uint8)
+    tb = np.ascontiguousarray(tall, np.float64)
+    pf = np.ascontiguousarray(pf, np.int32)
+    st = np.ascontiguousarray(states, np.uint64)
+    out = np.zeros(n_rigs * sizes()[1], np.uint8)
+    lib().hc_rig_results(n_rigs, cams_per_rig, ab.ctypes.data, tb.ctypes.data, pf.ctypes.data, st.ctypes.data,
+                         out.ctypes.data)
+    return out.reshape(n_rigs, -1)

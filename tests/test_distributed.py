@@ -9,6 +9,15 @@
 * bench.py's weak-scaling reduction: the MAX of the per-rank times is used.
 * Config 5's argmin exchange: the library's mantis_argmin_pick over the
   all-gathered (err, index) pairs.
+* Camera-sharded rigs (mantis_process_rig_sharded) at world 2, 3 (8 cameras
+  over 3 ranks: 3 / 3 / 2, padding slots) and 4: the library's own
+  cross-rank bookkeeping (mk_shard.h, host build) -- PF-flag pairs ->
+  all-gather -> per-frame cv::RNG offsets; camera records -> all-gather ->
+  merge -> rig fusion and rng_state_after -- on the per-frame flags and camera
+  records of a real one-GPU batch (tests/golden/shard_batch.npz, written by
+  tests/golden/make_shard_fixture.py on the GPU box): every rank's offsets
+  equal the sequential prefix, and its fused rig results equal the batch's,
+  byte for byte.
 * bench.py --gpus 2 without torchrun spawns two ranks of itself, which get as
   far as creating the library context (no GPU here) and fail with a clear
   message.
@@ -148,6 +157,96 @@ def test_argmin_pick_rules():
     assert spans[0] == (0, 2025) and spans[-1] == (14175, 16200)
     assert all(spans[i][1] == spans[i + 1][0] for i in range(7))
     assert dense.shard_range(5, 3, 4) == (4, 5) and dense.shard_range(2, 3, 4) == (2, 2)
+
+
+SHARD_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "shard_batch.npz")
+
+
+def _shard_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mantis_amd import rig
+
+    z = np.load(SHARD_FIXTURE)
+    R, Cn, per = int(z["rigs"]), int(z["cams"]), int(z["per"])
+    ng = R * Cn
+    cams = rig.shard_cameras(Cn, rank, world)
+    gidx = HC.shard_global_indices(R, cams, Cn)
+    assert list(gidx) == [r * Cn + c for r in range(R) for c in cams]
+    nl_max = -(-Cn // world)
+    slots = R * nl_max
+    # (global index, PF flag) pairs -> all-gather (the library's ncclAllGather) -> offsets
+    pairs = torch.from_numpy(HC.shard_pack_pairs(gidx, z["pf"][gidx], slots))
+    got = [torch.zeros_like(pairs) for _ in range(world)]
+    dist.all_gather(got, pairs)
+    flags, off, tot = HC.shard_offsets(torch.cat(got).numpy(), ng, per)
+    # camera records -> all-gather -> merge -> fusion + rng_state_after
+    recs = torch.from_numpy(HC.shard_make_recs(z["cam_bytes"][gidx], z["tbc"][gidx], gidx, slots))
+    rgot = [torch.zeros_like(recs) for _ in range(world)]
+    dist.all_gather(rgot, recs)
+    code, allb, tall = HC.shard_merge(torch.cat(rgot).numpy(), ng)
+    rigs = HC.rig_results(R, Cn, allb, tall, flags, z["states"])
+    out[rank] = (cams, flags, off[gidx], off, tot, code, allb, tall, rigs, slots - len(gidx))
+    dist.destroy_process_group()
+
+
+def _check_shard_world(world):
+    z = np.load(SHARD_FIXTURE)
+    cs, rsz, _ = HC.sizes()
+    assert int(z["cam_result_size"]) == cs and int(z["result_size"]) == rsz, "fixture layout differs from mantis.h"
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    pf, per = z["pf"], int(z["per"])
+    seq = per * np.concatenate([[0], np.cumsum(pf)[:-1]])  # sequential offsets, global frame order
+    assert 0 < pf.sum() < len(pf)
+    owners = []
+    for r in range(world):
+        cams, flags, off_local, off_all, tot, code, allb, tall, rigs, pad = out[r]
+        owners += cams
+        assert code == 0
+        assert np.array_equal(flags, pf)
+        assert np.array_equal(off_all, seq) and tot == per * pf.sum()
+        gidx = HC.shard_global_indices(int(z["rigs"]), cams, int(z["cams"]))
+        assert np.array_equal(off_local, seq[gidx])
+        assert np.array_equal(allb, z["cam_bytes"]) and np.array_equal(tall, z["tbc"].reshape(-1, 16))
+        assert np.array_equal(rigs, z["rig_bytes"]), f"rank {r}: fused rig results differ from the batch's"
+    assert sorted(owners) == list(range(int(z["cams"])))
+    return out
+
+
+def test_sharded_bookkeeping_world2():
+    _check_shard_world(2)
+
+
+def test_sharded_bookkeeping_world3_uneven():
+    out = _check_shard_world(3)
+    assert [len(out[r][0]) for r in range(3)] == [3, 3, 2]  # 8 cameras: rank 2 sends padding slots
+    assert out[0][9] == 0 and out[2][9] == 3  # rank 2: one padding slot per rig
+
+
+def test_sharded_bookkeeping_world4():
+    _check_shard_world(4)
+
+
+def test_shard_merge_rejects_bad_ownership():
+    """A camera sent by two ranks, or by none, is an error (the library
+    returns MANTIS_ERR_ARG with a message instead of fusing)."""
+    z = np.load(SHARD_FIXTURE)
+    R, Cn = int(z["rigs"]), int(z["cams"])
+    ng = R * Cn
+    g = np.arange(ng, dtype=np.int32)
+    recs = HC.shard_make_recs(z["cam_bytes"], z["tbc"], g, ng)
+    rs = HC.sizes()[2]
+    code, allb, _ = HC.shard_merge(recs, ng)
+    assert code == 0 and np.array_equal(allb, z["cam_bytes"])
+    dup = np.concatenate([recs, recs[:rs]])
+    assert HC.shard_merge(dup, ng)[0] == 1
+    assert HC.shard_merge(recs[: (ng - 1) * rs], ng)[0] == 2
+    g2 = g.copy()
+    g2[3] = ng + 5
+    assert HC.shard_merge(HC.shard_make_recs(z["cam_bytes"], z["tbc"], g2, ng), ng)[0] == 3
 
 
 def test_bench_launcher_spawns_ranks():

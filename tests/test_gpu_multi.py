@@ -146,3 +146,42 @@ def test_config4_8cam_1080p_rig_and_sharded_one_rank(landmark_map):
         ms.process_sharded(imgs[:n_rigs * 4], n_rigs, [0, 1, 2, 3], n_cams)
     mb.close()
     ms.close()
+
+
+def test_gauss_offsets_global_fabricated_gathers():
+    """k_gauss_offsets_global (the device half of the sharded call's cv::RNG
+    bookkeeping, mantis_shard_gauss_offsets) on fabricated all-gathers of 2 and
+    8 ranks -- uneven camera splits with padding slots (-1, 0), random PF
+    flags -- against the library's host rule (mk_shard.h, CPU build) and the
+    sequential prefix a single run over all cameras consumes."""
+    import _hostcheck as HC
+    import mantis_amd as M
+    from mantis_amd import rig
+
+    m = M.Mantis(max_cams=64, max_width=64, max_height=64)
+    try:
+        rng = np.random.default_rng(31)
+        per = 3000
+        for world, n_rigs, cams in [(2, 5, 4), (8, 3, 8), (3, 7, 8), (8, 2, 5)]:
+            ng = n_rigs * cams
+            pf = (rng.random(ng) < 0.7).astype(np.int32)
+            nl_max = -(-cams // world)
+            slots = n_rigs * nl_max
+            gathered, locals_ = [], []
+            for r in range(world):
+                ci = rig.shard_cameras(cams, r, world)
+                g = HC.shard_global_indices(n_rigs, ci, cams) if ci else np.zeros(0, np.int32)
+                locals_.append(g)
+                gathered.append(HC.shard_pack_pairs(g, pf[g], slots))
+            pairs = np.concatenate(gathered)
+            flags, off_host, tot_host = HC.shard_offsets(pairs, ng, per)
+            seq = per * np.concatenate([[0], np.cumsum(pf)[:-1]])
+            assert np.array_equal(off_host, seq) and tot_host == per * pf.sum()
+            for r in range(world):
+                if len(locals_[r]) == 0:
+                    continue
+                off, tot = m.shard_gauss_offsets(pairs, ng, locals_[r], per)
+                assert np.array_equal(off, seq[locals_[r]]), f"world {world} rank {r}"
+                assert tot == tot_host
+    finally:
+        m.close()

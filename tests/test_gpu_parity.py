@@ -319,3 +319,89 @@ def test_mixed_batch_skipped_frames_keep_rng_stream(mantis, frames, landmark_map
             _cmp_debug(mantis.frame_debug(i), o, f"frame {i}")
     assert cams[1].reason == 1 and cams[5].reason == 1, "flat frames have no quadrilaterals"
     assert mantis.rng_state == orc.rng_state
+
+
+def test_odd_capacity_multi_frame_batch(landmark_map):
+    """A context whose padded plane (max_width + 2) x (max_height + 2) is not a
+    multiple of 4 bytes (1283 x 723), with several frames per batch: the
+    hysteresis flag plane of frame f >= 1 must stay dword-aligned for its
+    32-bit flag atomics. Frames of an odd size (1279 x 719) go
+    through the whole callback and match the oracle frame by frame."""
+    import mantis_amd as M
+
+    W, H = 1279, 719
+    K, D = synth.intrinsics(W, H)
+    rng = np.random.default_rng(55)
+    m = M.Mantis(max_cams=3, max_width=1281, max_height=721)
+    try:
+        m.set_map(*landmark_map)
+        m.rng_state = 1
+        seq = []
+        for f in range(3):
+            R, pos = synth.random_pose(rng)
+            seq.append(synth.render_host(synth.make_cam(R, pos, W, H), synth.frame_seed(7, f)))
+        _, cams = m.process([M.make_image(img, K, D) for img in seq], rigs=3)
+        orc = O.Oracle(*landmark_map, seed=1)
+        for i, img in enumerate(seq):
+            o = orc.process(img, K, D)
+            assert o.n_quads > 0
+            _cmp_debug(m.frame_debug(i), o, f"odd frame {i}")
+            assert cams[i].reason == o.reason and cams[i].publish == o.publish
+        assert m.rng_state == orc.rng_state
+    finally:
+        m.close()
+
+
+def test_screen_off_equals_screen_on(frames, landmark_map):
+    """The fast scorers' FP32 projection screen (mk_screen.h) against the
+    exact FP64 path: a context created with MANTIS_SCREEN=0 sends every
+    landmark through the exact fallback (the block queues overflow, so the
+    in-place path runs too, then the drains); every error, count and decision
+    must be identical, in the pipeline (init / particle filter / shifts) and in
+    the standalone scorer (k_score_api, with and without a mask)."""
+    import os
+
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    imgs = [M.make_image(fr[0], K, D) for fr in frames[:4]]
+    old = os.environ.get("MANTIS_SCREEN")
+    os.environ["MANTIS_SCREEN"] = "0"
+    try:
+        mx = M.Mantis(max_cams=4, max_width=1280, max_height=720)
+    finally:
+        if old is None:
+            del os.environ["MANTIS_SCREEN"]
+        else:
+            os.environ["MANTIS_SCREEN"] = old
+    ms = M.Mantis(max_cams=4, max_width=1280, max_height=720)
+    try:
+        for m in (mx, ms):
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+        _, cx = mx.process(imgs)
+        _, cs = ms.process(imgs)
+        for f in range(len(imgs)):
+            gx, gs = mx.frame_debug(f), ms.frame_debug(f)
+            assert gx.n_hyps == gs.n_hyps and gx.n_hyps > 0
+            c = gx.n_hyps
+            assert np.array_equal(np.array(gx.hyp_err)[:c], np.array(gs.hyp_err)[:c])
+            assert np.array_equal(np.array(gx.hyp_n)[:c], np.array(gs.hyp_n)[:c])
+            assert np.array_equal(np.array(gx.pf_iter_err), np.array(gs.pf_iter_err))
+            assert np.array_equal(np.array(gx.shift_err), np.array(gs.shift_err))
+            assert np.array_equal(np.array(gx.top20_err), np.array(gs.top20_err))
+            assert gx.yaw_best == gs.yaw_best and gx.publish == gs.publish
+            assert list(cx[f].position) == list(cs[f].position)
+        assert mx.rng_state == ms.rng_state
+        rng = np.random.default_rng(5)
+        img, R, pos = frames[0]
+        c2w = [synth.truth_c2w(R @ synth.rot_z(rng.normal() * 0.05), pos + rng.normal(size=3) * 0.02)
+               for _ in range(300)]
+        c2w = np.array(c2w)
+        for mask in (None, ms.masks(imgs[0])[1]):
+            ex, nx = mx.score(imgs[0], c2w, fast=True, mask=mask)
+            es, ns = ms.score(imgs[0], c2w, fast=True, mask=mask)
+            assert np.array_equal(nx, ns) and np.array_equal(ex, es)
+    finally:
+        mx.close()
+        ms.close()

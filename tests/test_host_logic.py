@@ -244,3 +244,46 @@ def test_first_objpose_orientation_pairs_mirror():
     img, _, _, _, _, _ = G.quad_problems(np.random.default_rng(4), 300)
     rnd = [np.vstack([p.T, np.ones(4)]) for p in img]
     assert all(RM.mirror_pair_ok(q) for q in rnd)
+
+
+def test_fp32_screen_decisions_match_exact_projection():
+    """The FP32 projection screen of the fast scorers (mk_screen.h, host build:
+    correctly rounded reciprocals instead of the GPU's v_rcp / v_rsq, which
+    tools/check_screen.hip covers on the device) never takes a decision --
+    z > 0, inFrame, cvRound pixel -- that differs from the exact FP64
+    projection, on the bench scene's pose distribution (truth and particle
+    perturbations, every map landmark) and on arbitrary poses; and it leaves
+    only a small fraction of the in-frame landmarks unsure."""
+    white, red, green = synth.load_map()
+    lm = np.vstack([white, red, green])
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(21)
+    c2w, X = [], []
+    for _ in range(60):
+        R, pos = synth.random_pose(rng)
+        for _ in range(5):
+            Rp = R @ synth.rot_x(rng.normal() * 0.03) @ synth.rot_y(rng.normal() * 0.03) @ synth.rot_z(rng.normal() * 0.03)
+            T = synth.truth_c2w(Rp, pos + rng.normal(size=3) * 0.01)
+            c2w.append(np.repeat(T[None], len(lm), 0))
+            X.append(lm)
+    n_any = 100000
+    Q = rng.normal(size=(n_any, 4))
+    Q /= np.linalg.norm(Q, axis=1)[:, None]
+    a, b, c, d = Q.T
+    Rr = np.stack([a * a + b * b - c * c - d * d, 2 * (b * c - a * d), 2 * (b * d + a * c),
+                   2 * (b * c + a * d), a * a - b * b + c * c - d * d, 2 * (c * d - a * b),
+                   2 * (b * d - a * c), 2 * (c * d + a * b), a * a - b * b - c * c + d * d], 1).reshape(-1, 3, 3)
+    Cc = rng.uniform(-3, 3, (n_any, 3))
+    t = -np.einsum("nij,nj->ni", Rr, Cc)
+    c2w.append(np.concatenate([Rr.reshape(-1, 9), t], 1))
+    X.append(rng.uniform(-3, 3, (n_any, 3)))
+    c2w = np.concatenate([np.asarray(x).reshape(-1, 12) for x in c2w])
+    X = np.concatenate(X)
+    bad, res = H.screen_check(c2w, X, K, D, 1280, 720)
+    assert bad == 0, f"{bad} screened decisions differ from the exact projection"
+    n_scene = len(X) - n_any
+    inside = res[:n_scene, 1] == 1
+    unsure = res[:n_scene, 0] == 2
+    assert inside.sum() > 0.5 * n_scene
+    assert (unsure & inside).sum() < 0.03 * inside.sum(), f"unsure {unsure.sum()} of {inside.sum()} in-frame"
+    assert (res[:, 0] == 1).sum() > 0 and (res[:, 0] == 0).sum() > 0
