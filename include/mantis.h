@@ -220,6 +220,9 @@ mantis_status mantis_get_rig_gn(void* ctx, int32_t rig, mantis_rig_gn_info* info
  * sums[K x C x 2] (sum, count; nullable), chosen = winning slot or -1. */
 mantis_status mantis_get_rig_weights(void* ctx, int32_t rig, double* weights, double* c2w, double* sums,
                                      int32_t* chosen);
+/* Shape of the last batch's weighting record: rigs and C (cameras per rig), so
+ * a caller sizes the buffers of mantis_get_rig_weights (K = C + 1 slots). */
+mantis_status mantis_get_rig_weights_info(void* ctx, int32_t* n_rigs, int32_t* cams_per_rig);
 
 /* Markov yaw filter (include/mantis3/Markov.{h,cpp}, MarkovModel,
  * included but unused upstream): n_filters 360-bin yaw distributions in the

@@ -143,6 +143,7 @@ _SIGS = {
     "mantis_score_argmin_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
                                       C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_argmin_pick": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_get_rig_weights_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "mantis_shard_gauss_offsets": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                              C.c_int32, C.c_void_p, C.POINTER(C.c_int32)]),
 }
@@ -486,11 +487,17 @@ class Mantis:
                                          t.ctypes.data, e.ctypes.data, s.ctypes.data), "rpp_batch")
         return R.reshape(n, 3, 3), t, e, s
 
-    def rig_weights(self, rig, cams_per_rig):
+    def rig_weights(self, rig, cams_per_rig=None):
         """Legacy rig weighting record of rig `rig` (mantis_get_rig_weights):
         (weights[C+1], c2w[C+1, C, 12], sums[C+1, C, 2], chosen slot or -1);
-        slot C = the mantisService motion prediction."""
-        Cn = cams_per_rig
+        slot C = the mantisService motion prediction. The buffers are sized from
+        the record's own camera count (mantis_get_rig_weights_info); a
+        cams_per_rig that disagrees with it is an error."""
+        rigs, Cn = C.c_int32(), C.c_int32()
+        self._chk(lib().mantis_get_rig_weights_info(self.h, C.byref(rigs), C.byref(Cn)), "get_rig_weights_info")
+        Cn = Cn.value
+        if cams_per_rig is not None and cams_per_rig != Cn:
+            raise MantisError(f"rig_weights: the last batch had {Cn} cameras per rig, not {cams_per_rig}")
         w = np.zeros(Cn + 1)
         c2w = np.zeros((Cn + 1, Cn, 12))
         sums = np.zeros((Cn + 1, Cn, 2))
@@ -505,9 +512,19 @@ class Mantis:
         self._markov_n = len(R)
         self._chk(lib().mantis_markov_init(self.h, len(R), R.ctypes.data), "markov_init")
 
+    def _markov_len(self, arr, what):
+        n = getattr(self, "_markov_n", None)
+        if n is None:
+            raise MantisError("markov: no filters (markov_init first)")
+        if len(arr) != n:  # the C API reads markov_n entries of each array
+            raise MantisError(f"markov: {what} has {len(arr)} entries, the context holds {n} filters")
+
     def markov_sense(self, w2c_R, active=None):
         R = np.ascontiguousarray(w2c_R, np.float64).reshape(-1, 9)
         a = None if active is None else np.ascontiguousarray(active, np.int32)
+        self._markov_len(R, "w2c_R")
+        if a is not None:
+            self._markov_len(a, "active")
         self._chk(lib().mantis_markov_sense(self.h, R.ctypes.data, None if a is None else a.ctypes.data),
                   "markov_sense")
 
@@ -515,6 +532,10 @@ class Mantis:
         th = np.ascontiguousarray(dtheta, np.float64)
         d = np.ascontiguousarray(dt, np.float64)
         a = None if active is None else np.ascontiguousarray(active, np.int32)
+        self._markov_len(th, "dtheta")
+        self._markov_len(d, "dt")
+        if a is not None:
+            self._markov_len(a, "active")
         self._chk(lib().mantis_markov_convolve(self.h, th.ctypes.data, d.ctypes.data,
                                                None if a is None else a.ctypes.data), "markov_convolve")
 

@@ -216,11 +216,39 @@ struct Ctx {
   double* d_markov = nullptr;
   MarkovOp* d_mops = nullptr;
   int markov_n = 0;
+  int32_t* d_agree = nullptr;  // sharded calls: the failure flag all-reduced by agree()
+  bool agreed_fail = false;     // the last failure was agreed on by every rank (agree())
   // MANTIS_SCREEN=0 at mantis_create: the fast scorers' FP32 projection screen is
   // off (every landmark takes the exact FP64 fallback; a test / A-B switch)
   bool screen_off = false;
   std::vector<std::pair<Cam, ScreenCam>> scam_cache;  // screen_cam_cached
 };
+
+// Camera-sharded calls: every rank must enter the same collectives in the same
+// order. A rank-local failure (an image the staging rejects, an allocation, a
+// launch error) is agreed on before each exchange phase with one small
+// ncclAllReduce (max of a failure flag, 4 bytes), so every rank returns
+// together -- the failing rank its own error, the others MANTIS_ERR_COMM --
+// instead of leaving them blocked in an all-gather.
+mantis_status agree(Ctx* c, mantis_status local) {
+  c->agreed_fail = false;
+  if (!c->comm || !c->d_agree) return local;
+  int32_t flag = local != MANTIS_OK ? 1 : 0;
+  if (hipMemcpyAsync(c->d_agree, &flag, sizeof(flag), hipMemcpyHostToDevice, c->s) != hipSuccess ||
+      ncclAllReduce(c->d_agree, c->d_agree, 1, ncclInt32, ncclMax, (ncclComm_t)c->comm, c->s) != ncclSuccess ||
+      hipMemcpyAsync(&flag, c->d_agree, sizeof(flag), hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+      hipStreamSynchronize(c->s) != hipSuccess) {
+    c->err = "agreement all-reduce failed";
+    return MANTIS_ERR_COMM;
+  }
+  c->agreed_fail = flag != 0;
+  if (local != MANTIS_OK) return local;
+  if (flag) {
+    c->err = "another rank of the communicator failed before this exchange (see its mantis_last_error)";
+    return MANTIS_ERR_COMM;
+  }
+  return MANTIS_OK;
+}
 
 // the map as the scoring kernels read it: FP64 triples, then the FP32 screen table
 inline Landmarks lmk_of(const Ctx* c) {
@@ -580,10 +608,11 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shar
   gauss.t = std::thread([c, ng] { gen_gauss(c, ng); });
   int W, H;
   mantis_status st = stage_frames(c, cams, n, W, H);
+  if (st == MANTIS_OK) st = run_image_stages(c, n, W, H);
+  if (st == MANTIS_OK) st = run_contours(c, n, W, H);
+  if (st == MANTIS_OK) st = run_pose(c, n);
+  if (sh) st = agree(c, st);  // before the PF-flag all-gather
   if (st != MANTIS_OK) return st;
-  if ((st = run_image_stages(c, n, W, H)) != MANTIS_OK) return st;
-  if ((st = run_contours(c, n, W, H)) != MANTIS_OK) return st;
-  if ((st = run_pose(c, n)) != MANTIS_OK) return st;
   if ((st = gauss_offsets(c, n, sh)) != MANTIS_OK) return st;
   gauss.t.join();
   if ((st = run_score(c, n, ng)) != MANTIS_OK) return st;
@@ -848,7 +877,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->d_markov) (void)hipFree(c->d_markov);
   if (c->d_mops) (void)hipFree(c->d_mops);
   if (c->d_rwout) (void)hipFree(c->d_rwout);
-  void* dptrs[] = {c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
+  void* dptrs[] = {c->d_agree, c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc, c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)
@@ -1006,8 +1035,13 @@ mantis_status weight_rigs(Ctx* c, int n_rigs, int C, const mantis_cam_result* al
     c->d_rwjobs = nullptr;
     c->d_rwout = nullptr;
     c->rw_cap = 0;
-    if (dalloc(c, &c->d_rwjobs, need) || dalloc(c, &c->d_rwout, 2 * need)) return MANTIS_ERR_OOM;
+    mantis_status st = MANTIS_OK;
+    if (dalloc(c, &c->d_rwjobs, need) || dalloc(c, &c->d_rwout, 2 * need)) st = MANTIS_ERR_OOM;
+    if (use_comm) st = agree(c, st);  // before the (sum, count) all-reduce
+    if (st != MANTIS_OK) return st;
     c->rw_cap = need;
+  } else if (use_comm) {
+    if (mantis_status st = agree(c, MANTIS_OK)) return st;
   }
   std::vector<double> sums(2 * nslot, 0.0);
   if (nj) {
@@ -1126,23 +1160,26 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
   if (!c || !local_cams || !cam_index || !out || n_rigs <= 0 || n_local <= 0 || cams_per_rig <= 0)
     return MANTIS_ERR_ARG;
   if (!c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
+  // from here every failure is agreed on with the other ranks before an exchange (agree())
+  mantis_status vst = MANTIS_OK;
   const int nl_max = (cams_per_rig + c->nranks - 1) / c->nranks;
   if (n_local * c->nranks < cams_per_rig && c->nranks == 1) {
     c->err = "sharded rig: a one-rank communicator must hold every camera";
-    return MANTIS_ERR_ARG;
+    vst = MANTIS_ERR_ARG;
   }
-  if (n_local > nl_max) {
+  if (vst == MANTIS_OK && n_local > nl_max) {
     c->err = "sharded rig: at most ceil(cams_per_rig / nranks) cameras per rank";
-    return MANTIS_ERR_ARG;
+    vst = MANTIS_ERR_ARG;
   }
-  for (int j = 0; j < n_local; j++)
+  for (int j = 0; j < n_local && vst == MANTIS_OK; j++)
     if (cam_index[j] < 0 || cam_index[j] >= cams_per_rig || (j > 0 && cam_index[j] <= cam_index[j - 1])) {
       c->err = "sharded rig: cam_index must be ascending indices in [0, cams_per_rig)";
-      return MANTIS_ERR_ARG;
+      vst = MANTIS_ERR_ARG;
     }
   const int n = n_rigs * n_local, ng = n_rigs * cams_per_rig, slots = n_rigs * nl_max;
   // exchange buffers: (index, flag) pairs and result records, send + nranks x recv
-  if ((size_t)ng > c->sh_cap || (size_t)slots * (c->nranks + 1) * sizeof(ShardRec) > c->sh_rec_bytes) {
+  if (vst == MANTIS_OK &&
+      ((size_t)ng > c->sh_cap || (size_t)slots * (c->nranks + 1) * sizeof(ShardRec) > c->sh_rec_bytes)) {
     HIP_OK(hipStreamSynchronize(c->s));
     void* d[] = {c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec};
     for (void* p : d) (void)hipFree(p);
@@ -1154,16 +1191,22 @@ mantis_status mantis_process_rig_sharded(void* ctx, const mantis_image* local_ca
     const size_t rec_bytes = (size_t)slots * (c->nranks + 1) * sizeof(ShardRec);
     if (dalloc(c, &c->d_sh_gidx, (size_t)ng) || dalloc(c, &c->d_sh_pf, (size_t)2 * ng * (c->nranks + 1)) ||
         dalloc(c, &c->d_sh_flags, (size_t)2 * ng) || halloc(c, &c->h_sh_flags, (size_t)2 * ng) ||
-        dalloc(c, &c->d_sh_rec, rec_bytes) || halloc(c, &c->h_sh_rec, rec_bytes))
-      return MANTIS_ERR_OOM;
-    c->sh_cap = ng;
-    c->sh_rec_bytes = rec_bytes;
+        dalloc(c, &c->d_sh_rec, rec_bytes) || halloc(c, &c->h_sh_rec, rec_bytes)) {
+      vst = MANTIS_ERR_OOM;
+    } else {
+      c->sh_cap = ng;
+      c->sh_rec_bytes = rec_bytes;
+    }
   }
+  if ((vst = agree(c, vst)) != MANTIS_OK) return vst;
   std::vector<int32_t> gidx(n);
   mk::shard::global_indices(n_rigs, n_local, cam_index, cams_per_rig, gidx.data());
   Shard sh{ng, slots, gidx.data()};
   mantis_status st = process_frames(c, local_cams, n, &sh);
-  if (st != MANTIS_OK) return st;
+  // a failure process_frames agreed on returns everywhere; a later one (after
+  // the PF-flag exchange) is agreed on before the result all-gather
+  if (st != MANTIS_OK && c->agreed_fail) return st;
+  if ((st = agree(c, st)) != MANTIS_OK) return st;
   // gather every camera's result (one ncclAllGather of fixed-size records)
   ShardRec* send = (ShardRec*)c->h_sh_rec;
   for (int s = 0; s < slots; s++) {
@@ -1237,6 +1280,14 @@ mantis_status mantis_shard_gauss_offsets(void* ctx, const int32_t* pairs, int32_
   HIP_OK(hipMemcpyAsync(total, d_total, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   for (int i = 0; i < n_local; i++) offsets[i] = st[i].gauss_offset;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_get_rig_weights_info(void* ctx, int32_t* n_rigs, int32_t* cams_per_rig) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c || !n_rigs || !cams_per_rig) return MANTIS_ERR_ARG;
+  *n_rigs = c->rw_rigs;
+  *cams_per_rig = c->rw_C;
   return MANTIS_OK;
 }
 

@@ -246,11 +246,16 @@ mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, 
     c->d_gnobs = nullptr;
     c->d_gnacc = nullptr;
     c->gn_rigs = 0;
+    mantis_status st = MANTIS_OK;
     if (dalloc(c, &c->d_gncam, (size_t)n) || dalloc(c, &c->d_rigio, (size_t)n_rigs) ||
         dalloc(c, &c->d_gnobs, (size_t)n_rigs * obs_cap * 6) || dalloc(c, &c->d_gnacc, (size_t)n_rigs * kGnSlot))
-      return MANTIS_ERR_OOM;
+      st = MANTIS_ERR_OOM;
+    if (use_comm) st = agree(c, st);  // the other ranks would wait in the per-iteration all-reduce
+    if (st != MANTIS_OK) return st;
     c->gn_rigs = n_rigs;
     c->gn_cpr = cams_local;
+  } else if (use_comm) {
+    if (mantis_status st = agree(c, MANTIS_OK)) return st;
   }
   HIP_OK(hipMemcpyAsync(c->d_gncam, gc.data(), sizeof(GnCam) * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(c->d_rigio, io.data(), sizeof(RigGnIO) * n_rigs, hipMemcpyHostToDevice, c->s));
@@ -365,6 +370,12 @@ mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int
     (void)ncclCommDestroy(comm);
     c->err = "ncclCommCount/UserRank disagree with the requested rank layout";
     return MANTIS_ERR_COMM;
+  }
+  // the failure flag of the sharded call's agreement steps (agree(), api.hip):
+  // allocated here so agreeing never needs an allocation
+  if (!c->d_agree && dalloc(c, &c->d_agree, 1) != MANTIS_OK) {
+    (void)ncclCommDestroy(comm);
+    return MANTIS_ERR_OOM;
   }
   c->comm = comm;
   c->nranks = nranks;

@@ -179,8 +179,16 @@ mantis_status mantis_markov_weight(void* ctx, int32_t filter, const double* w2c_
   if (n == 0) return MANTIS_OK;
   std::vector<int32_t> bins(n);
   for (int h = 0; h < n; h++) bins[h] = markov_bin(w2c_R + 9 * (size_t)h);
-  int32_t* d_b;
-  double* d_e;
+  int32_t* d_b = nullptr;
+  double* d_e = nullptr;
+  struct Free {  // the temporaries are freed on every path (also the HIP_OK early returns)
+    int32_t*& b;
+    double*& e;
+    ~Free() {
+      (void)hipFree(b);
+      (void)hipFree(e);
+    }
+  } fr{d_b, d_e};
   if (dalloc(c, &d_b, (size_t)n) || dalloc(c, &d_e, (size_t)n)) return MANTIS_ERR_OOM;
   HIP_OK(hipMemcpyAsync(d_b, bins.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->s));
   HIP_OK(hipMemcpyAsync(d_e, error, sizeof(double) * n, hipMemcpyHostToDevice, c->s));
@@ -188,8 +196,6 @@ mantis_status mantis_markov_weight(void* ctx, int32_t filter, const double* w2c_
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(error, d_e, sizeof(double) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
-  (void)hipFree(d_b);
-  (void)hipFree(d_e);
   return MANTIS_OK;
 }
 

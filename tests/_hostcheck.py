@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HC_SO = os.path.join(ROOT, "build", "libmantis_hostcheck.so")
+HC_SO = os.environ.get("MANTIS_HOSTCHECK_SO") or os.path.join(ROOT, "build", "libmantis_hostcheck.so")  # make sanitize: instrumented build
 _lib = None
 
 

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+ORACLE_SO = os.environ.get("MANTIS_ORACLE_SO") or os.path.join(ROOT, "oracle", "liboracle.so")  # make sanitize: instrumented build
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_rpp.so")
 
 ORC_MAX_QUADS = 256

@@ -144,6 +144,18 @@ def test_config4_8cam_1080p_rig_and_sharded_one_rank(landmark_map):
     # a rank that does not hold every camera of a one-rank rig is rejected up front
     with pytest.raises(M.MantisError):
         ms.process_sharded(imgs[:n_rigs * 4], n_rigs, [0, 1, 2, 3], n_cams)
+    # a rank-local staging failure (row step < 3 W) goes through the agreement
+    # all-reduce before the PF-flag exchange and returns an error (with more
+    # ranks the others return MANTIS_ERR_COMM instead of blocking in the
+    # all-gather); the communicator stays usable and the next call is correct
+    bad = [M.make_image(host[i], K, D, T_base_cam=ext[i % n_cams]) for i in range(n_rigs * n_cams)]
+    bad[3].step_bytes = 3 * W - 3
+    with pytest.raises(M.MantisError, match="step"):
+        ms.process_sharded(bad, n_rigs, list(range(n_cams)), n_cams)
+    ms.rng_state = 1
+    rs2, _ = ms.process_sharded(imgs, n_rigs, list(range(n_cams)), n_cams)
+    for a, b in zip(rb, rs2):
+        assert bytes(a) == bytes(b)
     mb.close()
     ms.close()
 

@@ -92,3 +92,17 @@ def test_grid1_oracle_plumbing_golden(landmark_map):
     assert np.array_equal(quads, g["quads"])
     assert dbg.reason == g["reason"] and dbg.publish == g["publish"] and dbg.n_hyps == g["n_hyps"]
     assert dbg.rng_state_after == g["rng_state_after"]
+
+
+@pytest.mark.skipif(not os.environ.get("MANTIS_SANITIZE"), reason="only under `make sanitize`")
+def test_sanitized_builds_are_the_ones_loaded():
+    """`make sanitize`: the oracle and the host build of the device-logic
+    headers in this process are the ASan/UBSan builds (build/san/), with the
+    sanitizer runtimes mapped, so the suite ran against them."""
+    import _hostcheck as HC
+
+    O.lib()
+    HC.lib()
+    maps = open("/proc/self/maps").read()
+    assert "build/san/liboracle.so" in maps and "build/san/libmantis_hostcheck.so" in maps
+    assert "libasan" in maps and "libubsan" in maps
