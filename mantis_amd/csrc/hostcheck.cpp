@@ -87,6 +87,37 @@ void hc_rpp_iters(const double* model, const double* iprts, int32_t* it) {
   }
 }
 
+// longest-first scheduling predictor (mk_rpp.h op_predict) for the first
+// ObjPose (sR == nullptr) or a candidate ObjPose from initial rotation sR
+float hc_objpose_predict(const double* model, const double* iprts, const double* sR, int kprobe) {
+  mk::rpp::M34 P, Q;
+  for (int i = 0; i < 12; i++) { P.a[i] = model[i]; Q.a[i] = iprts[i]; }
+  mk::rpp::OpState s;
+  mk::rpp::M33 R0;
+  if (sR)
+    for (int k = 0; k < 9; k++) R0.a[k] = sR[k];
+  mk::rpp::op_setup(P, Q, sR ? &R0 : nullptr, s);
+  return mk::rpp::op_predict(s, kprobe);
+}
+
+// the ObjPose error sequence (new_err after each AbsKernel, first n) and its
+// total AbsKernel count (predictor studies, tools/)
+int hc_objpose_trace(const double* model, const double* iprts, const double* sR, int n, double* errs) {
+  mk::rpp::M34 P, Q;
+  for (int i = 0; i < 12; i++) { P.a[i] = model[i]; Q.a[i] = iprts[i]; }
+  mk::rpp::OpState s;
+  mk::rpp::M33 R0;
+  if (sR)
+    for (int k = 0; k < 9; k++) R0.a[k] = sR[k];
+  mk::rpp::op_setup(P, Q, sR ? &R0 : nullptr, s);
+  int k = 0;
+  while (!mk::rpp::op_step(s)) {
+    if (k < n) errs[k] = s.new_err;
+    k++;
+  }
+  return s.it;
+}
+
 int hc_rpoly(const double* op, int deg, double* zr, double* zi) { return mk::rpp::rpoly(op, deg, zr, zi); }
 
 void hc_sort_desc(const double* err, int n, int* perm) {

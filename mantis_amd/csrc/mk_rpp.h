@@ -1084,6 +1084,34 @@ MK_HD int obj_pose(const M34& P0, M34& Qp, const M33* initR, M33& R, M31& t, int
   return r == 2 ? 1 : 0;
 }
 
+// Predicted AbsKernel count of an ObjPose from its state (longest-first
+// scheduling of the persistent job queues, kernels.hip k_objpose_probe):
+// kprobe more steps on a copy, then the stop test |de/e| <= kObjTol
+// (RPP.cpp:171) extrapolated with the observed linear convergence rate of
+// |de/e| over the last kPredSpan steps. Scheduling only: the results always
+// come from the unchanged iteration.
+constexpr int kPredSpan = 4;
+MK_HD float op_predict(OpState s, int kprobe) {
+  double e[2 + kPredSpan];  // the last errors (ring)
+  int n = 0;
+#pragma unroll 1
+  for (int i = 0; i < kprobe; i++) {
+    if (op_step(s)) return (float)s.it;  // converged (or capped) inside the probe
+#pragma unroll
+    for (int j = 0; j < 1 + kPredSpan; j++) e[j] = e[j + 1];
+    e[1 + kPredSpan] = s.new_err;
+    n++;
+  }
+  if (n < 2 + kPredSpan) return 1e6f;
+  const double r1 = fabs((e[kPredSpan] - e[1 + kPredSpan]) / e[kPredSpan]);
+  const double r0 = fabs((e[0] - e[1]) / e[0]);
+  if (!(r1 > kObjTol)) return (float)(s.it + 1);
+  const double rho = (r0 > 0 && r1 < r0) ? pow(r1 / r0, 1.0 / kPredSpan) : 1.0;
+  if (!(rho < 0.99999)) return 1e6f;
+  const double rem = log(kObjTol / r1) / log(rho);
+  return (float)(s.it + (rem > 0 ? rem : 0) + 1);
+}
+
 MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
   double d = v2[0] * v1[0] + v2[1] * v1[1] + v2[2] * v1[2];
   double winkel = acos(d);
