@@ -298,6 +298,17 @@ mantis_status mantis_score_argmin_dev(void* ctx, const mantis_image* img, const 
 /* The cross-shard rule on its own (host only): pairs = nranks x (err, global index). */
 mantis_status mantis_argmin_pick(const double* pairs, int32_t nranks, double* best_err, int64_t* best_idx);
 
+/* mantis_score_argmin_dev over n_frames frames in one call (BASELINE config 5
+ * batched): frame f's n_hyps[f] hypotheses (device c2w_dev[f], n x 12) scored
+ * against its cleaned mask (device masks_dev[f], nullable array / entries)
+ * in one launch, one argmin per frame, and with use_comm one ncclAllGather of
+ * every frame's (err, global index) pair per rank; best_err / best_idx get
+ * n_frames entries (global index = index_base[f] + local index). */
+mantis_status mantis_score_argmin_batch(void* ctx, const mantis_image* imgs, int32_t n_frames,
+                                        const uint8_t* const* masks_dev, const double* const* c2w_dev,
+                                        const int32_t* n_hyps, const int64_t* index_base, int32_t use_comm,
+                                        double* best_err, int64_t* best_idx);
+
 /* ----------------------------------------- Gauss–Newton rig refinement (new) */
 /* One GN step over m camera observations: for camera c, corr_c normalized image points u (2)
  * matched to world points X (3). Accumulates J^T J (21 upper-tri), J^T r (6), cost (1) into

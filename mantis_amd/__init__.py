@@ -143,6 +143,8 @@ _SIGS = {
     "mantis_score_argmin_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
                                       C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_argmin_pick": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "mantis_score_argmin_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_get_rig_weights_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "mantis_shard_gauss_offsets": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
                                              C.c_int32, C.c_void_p, C.POINTER(C.c_int32)]),
@@ -474,6 +476,21 @@ class Mantis:
                                                 C.c_void_p(c2w_dev), int(n), index_base, int(use_comm), C.byref(e),
                                                 C.byref(i)), "score_argmin_dev")
         return e.value, i.value
+
+    def score_argmin_batch(self, imgs, c2w_devs, ns, index_bases=None, use_comm=False, mask_devs=None):
+        """mantis_score_argmin_batch: per-frame device hypothesis blocks (and
+        masks) scored in one launch; returns [(err, global index)] per frame."""
+        nf = len(imgs)
+        arr = (MantisImage * nf)(*imgs)
+        cp = (C.c_void_p * nf)(*[C.c_void_p(p) for p in c2w_devs])
+        mp = None if mask_devs is None else (C.c_void_p * nf)(*[C.c_void_p(p) for p in mask_devs])
+        n = np.ascontiguousarray(ns, np.int32)
+        ib = np.ascontiguousarray(index_bases if index_bases is not None else np.zeros(nf), np.int64)
+        e = np.zeros(nf)
+        i = np.zeros(nf, np.int64)
+        self._chk(lib().mantis_score_argmin_batch(self.h, arr, nf, mp, cp, n.ctypes.data, ib.ctypes.data,
+                                                  int(use_comm), e.ctypes.data, i.ctypes.data), "score_argmin_batch")
+        return list(zip(e.tolist(), i.tolist()))
 
     def rpp(self, img_pts, obj_pts):
         img_pts = np.ascontiguousarray(img_pts, np.float64).reshape(-1, 4, 2)

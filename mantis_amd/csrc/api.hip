@@ -161,6 +161,9 @@ struct Ctx {
   double *d_dense_c2w = nullptr, *d_dense_err = nullptr, *d_pairs = nullptr;
   int32_t* d_dense_np = nullptr;
   size_t dense_cap = 0;
+  void* d_dense_jobs = nullptr;  // mantis_score_argmin_batch: per-frame DenseJob records
+  size_t dense_pairs_cap = 0;    // doubles d_pairs holds (0: the 64-rank single-frame buffer)
+  size_t dense_jobs_cap = 0;     // DenseJob records d_dense_jobs holds
   // rig GN (cfg.gn_enable): per-camera inv(T_base_cam), per-rig poses, correspondences
   GnCam* d_gncam = nullptr;
   RigGnIO* d_rigio = nullptr;
@@ -877,7 +880,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->d_markov) (void)hipFree(c->d_markov);
   if (c->d_mops) (void)hipFree(c->d_mops);
   if (c->d_rwout) (void)hipFree(c->d_rwout);
-  void* dptrs[] = {c->d_agree, c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
+  void* dptrs[] = {c->d_dense_jobs, c->d_agree, c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc, c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)

@@ -13,6 +13,16 @@ Fixtures (data only — inputs and expected outputs):
                     sigma 0.01 corner noise, GCC right-to-left draw order),
                     test/legacy/unit_test.cpp:49-76 (pinhole square), and
                     seeded random squares seen by a nadir-ish camera.
+  rpp_faults.npz    degenerate 4-point RPP problems -> the REFERENCE's outputs
+                    (same build): image points whose mean ray is the optical
+                    axis (a centred symmetric square), collinear, pairwise
+                    repeated and coincident points -- Rpp() returns false there
+                    (no 2nd-pose candidate: DecomposeR / RpyAng_X fail,
+                    RPP.cpp:13-64, 755-808), status 0 -- plus tiny / huge
+                    spreads that still succeed. (The exit(1) of
+                    GetRotationbyVector, RPP.cpp:450-453, needs a mean ray the
+                    rotation cannot map back; no image points with z = 1 reach
+                    it -- tests/test_oracle_pins.py searches for it.)
   rpp_demo.npz      demo.cpp:17-38 10-point problem -> reference output
                     (plus the Matlab answer quoted in demo.cpp:28-38).
   rpoly_golden.npz  quartics -> reference rpoly_ak1 roots (5 slots).
@@ -102,6 +112,47 @@ def rpp_cases():
     return out
 
 
+def rpp_fault_cases():
+    rng = np.random.default_rng(20261017)
+    s = 0.16
+    sq = np.array([[s, -s, -s, s], [s, s, -s, -s], [0, 0, 0, 0.0]])
+    models, iprts, names = [], [], []
+
+    def add(name, ip, m=sq):
+        models.append(m.copy())
+        iprts.append(np.asarray(ip, np.float64))
+        names.append(name)
+
+    for k in range(12):
+        a = rng.uniform(0.05, 0.6)
+        add(f"centred_square[{k}]", [[a, -a, -a, a], [a, a, -a, -a], [1, 1, 1, 1]])
+    for k in range(12):
+        d, o, tt = rng.normal(size=2), rng.normal(size=2) * 0.3, np.sort(rng.uniform(-1, 1, 4))
+        add(f"collinear[{k}]", [o[0] + d[0] * tt, o[1] + d[1] * tt, np.ones(4)])
+    for k in range(12):
+        p = rng.normal(size=(2, 4)) * 0.3
+        p[:, 1], p[:, 3] = p[:, 0], p[:, 2]
+        add(f"repeated[{k}]", np.vstack([p, np.ones(4)]))
+    for k in range(6):
+        p = rng.normal(size=2) * 0.3
+        add(f"coincident[{k}]", np.vstack([np.repeat(p[:, None], 4, 1), np.ones(4)]))
+    for k in range(6):
+        add(f"tiny_spread[{k}]", np.vstack([rng.normal(size=2)[:, None] * 0.5 + rng.normal(size=(2, 4)) * 1e-7,
+                                            np.ones(4)]))
+    for k in range(6):
+        add(f"huge_spread[{k}]", np.vstack([rng.normal(size=(2, 4)) * rng.uniform(5, 200), np.ones(4)]))
+    out = {"model": np.array(models), "iprts": np.array(iprts), "name": np.array(names)}
+    st, Rs, ts, es = [], [], [], []
+    for m, ip in zip(models, iprts):
+        a, R, t, e = ref_case(m, ip)
+        st.append(a)
+        Rs.append(R)
+        ts.append(t)
+        es.append(e)
+    out.update(status=np.array(st, np.int32), R=np.array(Rs), t=np.array(ts), errs=np.array(es))
+    return out
+
+
 def demo_case():
     md = [0.0685, 0.6383, 0.4558, 0.7411, -0.7219, 0.7081, 0.7061, 0.2887, -0.9521, -0.2553,
           0.4636, 0.0159, -0.1010, 0.2817, 0.6638, 0.1582, 0.3925, -0.7954, 0.6965, -0.7795]
@@ -155,7 +206,15 @@ def grid1_case():
 def main():
     if O.ref() is None:
         sys.exit("oracle/_ref/libref_rpp.so missing: run `make ref` first")
+    only = sys.argv[1:]  # e.g. `make_golden.py rpp_faults`: regenerate those fixtures only
+    if only:
+        for name in only:
+            fn = {"rpp_faults": rpp_fault_cases}[name]
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **fn())
+            print(name, os.path.getsize(os.path.join(HERE, name + ".npz")))
+        return
     np.savez_compressed(os.path.join(HERE, "rpp_golden.npz"), **rpp_cases())
+    np.savez_compressed(os.path.join(HERE, "rpp_faults.npz"), **rpp_fault_cases())
     np.savez_compressed(os.path.join(HERE, "rpp_demo.npz"), **demo_case())
     np.savez_compressed(os.path.join(HERE, "rpoly_golden.npz"), **rpoly_cases())
     if os.path.exists(REF_GRID1):

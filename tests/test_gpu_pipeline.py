@@ -582,3 +582,212 @@ def test_pf_mask_lds_and_global_paths_agree(landmark_map):
         glob = run({"MANTIS_TRACE_LDS_FRAMES": small, "MANTIS_PF_MASK_GLOBAL": "1"})
         assert lds == glob, small
         assert any(r[0] >= 0 for r in lds)
+
+
+def test_dense_batch_matches_per_frame(m720, landmark_map):
+    """mantis_score_argmin_batch (config 5 batched: one launch over several
+    frames' hypothesis blocks, per-frame argmins, device-resident inputs)
+    equals mantis_score_argmin per frame -- uneven block sizes, an empty
+    block, a frame without a mask -- also through the one-rank RCCL exchange."""
+    import mantis_amd as M
+    from mantis_amd import dense
+
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(97)
+    imgs, hyps, masks = [], [], []
+    for f in range(4):
+        R, pos = synth.random_pose(rng)
+        img = synth.render_host(synth.make_cam(R, pos), synth.frame_seed(5, 10 + f))
+        im = M.make_image(img, K, D)
+        imgs.append(im)
+        masks.append(m720.masks(im)[1])
+        hyps.append(dense.config5_hypotheses(R, pos, np.random.default_rng(f), n_particles=2 + f))
+    hyps[2] = hyps[2][:0]  # an empty block
+    bases = [0, 5000, 10, 77]
+    want = []
+    for f in range(4):
+        if len(hyps[f]) == 0:
+            want.append((np.finfo(np.float64).max, -1))
+            continue
+        want.append(m720.score_argmin(imgs[f], hyps[f], bases[f], False, masks[f] if f != 3 else None))
+    ptrs = []
+    try:
+        d_h = [m720.device_alloc(max(8, h.nbytes)) for h in hyps]
+        d_m = [m720.device_alloc(mk.nbytes) for mk in masks]
+        ptrs = d_h + d_m
+        for f in range(4):
+            if len(hyps[f]):
+                m720.h2d(d_h[f], np.ascontiguousarray(hyps[f], np.float64))
+            m720.h2d(d_m[f], np.ascontiguousarray(masks[f], np.uint8))
+        mptr = [d_m[0], d_m[1], d_m[2], 0]
+        got = m720.score_argmin_batch(imgs, d_h, [len(h) for h in hyps], bases, False, mptr)
+        for f in range(4):
+            if want[f][1] < 0:
+                assert got[f][1] == -1
+            else:
+                assert got[f] == want[f], f"frame {f}: {got[f]} vs {want[f]}"
+        mc = M.Mantis(max_cams=8, max_width=1280, max_height=720)
+        try:
+            mc.set_map(*landmark_map)
+            mc.comm_init(0, 1)
+            dh2 = [mc.device_alloc(max(8, h.nbytes)) for h in hyps]
+            dm2 = [mc.device_alloc(mk.nbytes) for mk in masks]
+            for f in range(4):
+                if len(hyps[f]):
+                    mc.h2d(dh2[f], np.ascontiguousarray(hyps[f], np.float64))
+                mc.h2d(dm2[f], np.ascontiguousarray(masks[f], np.uint8))
+            got2 = mc.score_argmin_batch(imgs, dh2, [len(h) for h in hyps], bases, True, [dm2[0], dm2[1], dm2[2], 0])
+            assert got2 == got
+        finally:
+            mc.close()
+    finally:
+        for p in ptrs:
+            m720.device_free(p)
+
+
+def test_rpp_fault_golden_on_gpu(m720):
+    """Fault injection, RPP: the degenerate problems of
+    tests/golden/rpp_faults.npz (outputs of the reference's own RPP.cpp) through
+    the device RPP (mantis_rpp_batch): status 0 where Rpp() returns false (no
+    2nd-pose candidate: the first ObjPose's pose is kept, RPP.cpp:13-64) and the
+    reference's R, t and errors."""
+    d = np.load(os.path.join(GOLD, "rpp_faults.npz"), allow_pickle=False)
+    ip = np.transpose(d["iprts"][:, :2, :], (0, 2, 1))
+    op = np.transpose(d["model"], (0, 2, 1))
+    R, t, e, st = m720.rpp(ip, op)
+    assert (d["status"] == 0).sum() >= 40
+    assert np.array_equal(st, d["status"])
+    stable = _rpp_stable(d)
+    assert stable.sum() >= 12  # the centred squares and huge spreads
+    np.testing.assert_allclose(R[stable], d["R"][stable], atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(t[stable], d["t"][stable], atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(e[stable], d["errs"][stable, :2], rtol=1e-9, atol=1e-15)
+    # rank-deficient problems (collinear, repeated, coincident points, 1e-7
+    # spreads): the reference's own pose moves by O(1) when an input moves by
+    # one ulp (_rpp_stable), so a 1-ulp difference of a device libm call picks
+    # another, equally valid, minimiser. There: a rotation, and errors that are
+    # the reference's error formulas (RPP.cpp ObjPose: object-space error over
+    # the line-of-sight projectors; image error against the FIRST image point,
+    # the reference's Qp(0,0) indexing) evaluated at the returned pose.
+    for k in np.flatnonzero(~stable):
+        Rk = R[k]
+        np.testing.assert_allclose(Rk.T @ Rk, np.eye(3), atol=1e-9, err_msg=str(d["name"][k]))
+        m = d["model"][k]
+        v = d["iprts"][k]
+        q = Rk @ m + t[k][:, None]
+        oe = 0.0
+        for i in range(m.shape[1]):
+            F = np.outer(v[:, i], v[:, i]) / (v[:, i] @ v[:, i])
+            oe += np.sum(((np.eye(3) - F) @ q[:, i]) ** 2)
+        ie = np.sum((q[0] / q[2] - v[0, 0]) ** 2 + (q[1] / q[2] - v[1, 0]) ** 2)
+        n = m.shape[1]
+        np.testing.assert_allclose(e[k], [np.sqrt(oe / n), np.sqrt(ie / n)], rtol=1e-6, atol=1e-9,
+                                   err_msg=str(d["name"][k]))
+
+
+def _rpp_stable(d, trials=12):
+    """Problems whose reference pose is stable to rounding: the oracle (bit-
+    exact with the reference on these problems, test_oracle_pins) moves by less
+    than 1e-9 under 1-ulp relative perturbations of the image points."""
+    rng = np.random.default_rng(1)
+    out = np.ones(len(d["model"]), bool)
+    for k in range(len(d["model"])):
+        for _ in range(trials):
+            ip = d["iprts"][k].copy()
+            ip[:2] *= 1 + rng.normal(size=ip[:2].shape) * 2e-16
+            _, Rk, tk, _, _ = O.rpp(d["model"][k], ip)
+            if max(np.abs(Rk.reshape(3, 3) - d["R"][k]).max(), np.abs(tk - d["t"][k]).max()) > 1e-9:
+                out[k] = False
+                break
+    return out
+
+
+def _irregular_quads_frame(rng, W=640, H=480):
+    """Dark, strongly non-square quadrilaterals on a light floor: the detector
+    finds 4-vertex contours, but RPP's square model fits them so badly that
+    every hypothesis fails the img_err > MAX_QUAD_ERROR gate
+    (HypothesisGeneration.h:80-85) -> no hypotheses (src/mantis3.cpp:94-97)."""
+    import PIL.Image
+    import PIL.ImageDraw
+
+    im = PIL.Image.fromarray(np.full((H, W, 3), 200, np.uint8))
+    dr = PIL.ImageDraw.Draw(im)
+    for _ in range(6):
+        cx, cy = rng.uniform(80, W - 80), rng.uniform(80, H - 80)
+        pts = [(cx + rng.uniform(-70, 70) * 2.5, cy + rng.uniform(-70, 70) * 0.3) for _ in range(4)]
+        pts = sorted(pts, key=lambda p: np.arctan2(p[1] - cy, p[0] - cx))
+        dr.polygon(pts, fill=(30, 30, 30))
+    return np.asarray(im).copy()
+
+
+def test_reason2_frames_match_oracle(landmark_map):
+    """Fault injection, pipeline: frames whose quads all fail the hypothesis
+    gate return reason 2 (no hypotheses, src/mantis3.cpp:94-97), publish
+    nothing and draw no gaussians -- in a batch with normal frames, whose
+    particle filters then read the cv::RNG stream where the sequential
+    reference does."""
+    import mantis_amd as M
+
+    rng = np.random.default_rng(5)
+    K, D = synth.intrinsics(640, 480)
+    seq, reasons = [], []
+    while len(seq) < 3:
+        img = _irregular_quads_frame(rng)
+        o = O.Oracle(*landmark_map, seed=1).process(img, K, D)
+        if o.reason == 2 and o.n_quads > 0:
+            seq.append(img)
+    R, pos = synth.random_pose(np.random.default_rng(8))
+    normal = synth.render_host(synth.make_cam(R, pos, 640, 480), synth.frame_seed(13, 0))
+    seq = [seq[0], normal, seq[1], seq[2], normal]
+    m = M.Mantis(max_cams=5, max_width=640, max_height=480)
+    try:
+        m.set_map(*landmark_map)
+        m.rng_state = 1
+        _, cams = m.process([M.make_image(img, K, D) for img in seq], rigs=5)
+        orc = O.Oracle(*landmark_map, seed=1)
+        for i, img in enumerate(seq):
+            o = orc.process(img, K, D)
+            _cmp_debug(m.frame_debug(i), o, f"frame {i}")
+            assert cams[i].reason == o.reason and cams[i].publish == o.publish
+            reasons.append(o.reason)
+        assert reasons.count(2) == 3 and reasons[1] not in (1, 2)
+        assert m.rng_state == orc.rng_state
+    finally:
+        m.close()
+
+
+def test_reason4_no_green_landmarks_match_oracle(landmark_map):
+    """Fault injection, yaw stage: with a map whose green set is empty every
+    COLOR yaw set averages DBL_MAX, so determineBestYaw picks nothing -- the
+    reference then reads hyps.back() of an empty set (UB); here
+    reason 4 (no yaw), no publish -- identical to the oracle, and the fast
+    scoring / particle filter before it is unchanged."""
+    import mantis_amd as M
+
+    white, red, green = landmark_map
+    no_green = green[:0]
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(14)
+    seq = []
+    for f in range(3):
+        R, pos = synth.random_pose(rng)
+        seq.append(synth.render_host(synth.make_cam(R, pos), synth.frame_seed(14, f)))
+    m = M.Mantis(max_cams=3, max_width=1280, max_height=720)
+    try:
+        m.set_map(white, red, no_green)
+        m.rng_state = 1
+        _, cams = m.process([M.make_image(img, K, D) for img in seq], rigs=3)
+        orc = O.Oracle(white, red, no_green, seed=1)
+        n4 = 0
+        for i, img in enumerate(seq):
+            o = orc.process(img, K, D)
+            assert cams[i].reason == o.reason and cams[i].publish == o.publish == 0
+            n4 += o.reason == 4
+            g = m.frame_debug(i)
+            assert g.n_hyps == o.n_hyps and g.pf_err == o.pf_err
+            np.testing.assert_array_equal(np.array(g.shift_err), np.array(o.shift_err))
+            assert g.yaw_best == o.yaw_best == -1
+        assert n4 == 3
+        assert m.rng_state == orc.rng_state
+    finally:
+        m.close()
