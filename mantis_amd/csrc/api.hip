@@ -155,6 +155,13 @@ struct Ctx {
   int32_t *d_jobs0 = nullptr, *d_jobs1 = nullptr;  // RPP ObjPose job queues
   RppQueue* d_rq = nullptr;
   int rpp_blocks = 0;
+  // ObjPose tail compaction (k_objpose_q rounds): two spill pools of op_cap
+  // lanes (kOpFields doubles + a job id each), their counters, rounds per queue
+  double* d_opool[2] = {nullptr, nullptr};
+  int32_t* d_ojob[2] = {nullptr, nullptr};
+  int32_t* d_octl = nullptr;  // [2][2]: entries, next
+  int32_t op_cap = 0;
+  int op_rounds = 6, op_spill = 32;
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -432,17 +439,40 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
 
 // paired: pipeline items (orientation pairs of each quad, k_rpp_prep); the
 // first queue holds orientation 0 only and op_end<0> mirrors its result
+// One ObjPose queue as op_rounds launches over one grid (k_objpose_q, tail
+// compaction): round 0 serves the job list, every later round the states the
+// previous one spilled, the last runs every job to the end.
+template <int MODE>
+mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::Refine* rf, const int32_t* jobs,
+                                 RppQueue* q, FrameState* st, int paired) {
+  const int rounds = std::max(1, c->op_rounds);
+  if ((size_t)blocks * 256 > (size_t)c->op_cap) blocks = (unsigned)(c->op_cap / 256);  // a pool holds a grid's lanes
+  for (int r = 0; r < rounds; r++) {
+    const int in = (r + 1) & 1, out = r & 1;
+    OpRound rd;
+    rd.in = OpPool{c->d_opool[in], c->d_ojob[in], c->d_octl + 2 * in};
+    rd.out = OpPool{c->d_opool[out], c->d_ojob[out], c->d_octl + 2 * out};
+    rd.cap = c->op_cap;
+    rd.first = r == 0;
+    rd.last = r == rounds - 1;
+    rd.spill_below = c->op_spill;
+    if (!rd.last) HIP_OK(hipMemsetAsync(rd.out.ctl, 0, 2 * sizeof(int32_t), c->s));
+    k_objpose_q<MODE><<<blocks, 256, 0, c->s>>>(items, rf, jobs, q, st, paired, rd);
+  }
+  return MANTIS_OK;
+}
+
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
                        RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads,
                        bool paired) {
   const int pr = paired ? 1 : 0;
-  k_objpose_q<0><<<objpose_blocks(c, paired ? expected_items / 2 : expected_items), 256, 0, c->s>>>(items, rf, jobs0,
-                                                                                                    q, st, pr);
+  run_objpose_rounds<0>(c, objpose_blocks(c, paired ? expected_items / 2 : expected_items), items, rf, jobs0, q, st,
+                        pr);
   mark(c, "rpp_first");
   k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
       items, jobs0, jobs1, q, pr);
   mark(c, "rpp_2nd");
-  k_objpose_q<1><<<objpose_blocks(c, expected_items * 2), 256, 0, c->s>>>(items, rf, jobs1, q, st, 0);
+  run_objpose_rounds<1>(c, objpose_blocks(c, expected_items * 2), items, rf, jobs1, q, st, 0);
   mark(c, "rpp_cand");
   k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out, quads,
                                                                quads ? c->cfg.quad_gn_iterations : 0);
@@ -761,6 +791,9 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   }
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg.device) != hipSuccess || c->n_cu < 1)
     c->n_cu = 256;
+  if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
+  if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
@@ -836,6 +869,16 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_jobs0, (size_t)F * kMaxQuads * 2));
   chk(dalloc(c, &c->d_jobs1, (size_t)F * kMaxQuads * 2 * rpp::kCand));
   chk(dalloc(c, &c->d_rq, 1));
+  {
+    // spill pools sized for the largest ObjPose grid objpose_blocks can return
+    const size_t blocks = c->rpp_blocks > 0 ? (size_t)c->rpp_blocks : (size_t)std::max(64, 3 * c->n_cu / 2);
+    c->op_cap = (int32_t)(blocks * 256);
+    for (int k = 0; k < 2; k++) {
+      chk(dalloc(c, &c->d_opool[k], (size_t)kOpFields * c->op_cap));
+      chk(dalloc(c, &c->d_ojob[k], (size_t)c->op_cap));
+    }
+    chk(dalloc(c, &c->d_octl, 4));
+  }
   chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_st, (size_t)F));
@@ -856,7 +899,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     mantis_destroy(c);
     return st;
   }
-  if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
   (void)hipGetLastError();
   if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess) {
     g_create_err = "hipMemset failed";
@@ -880,7 +922,7 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->d_markov) (void)hipFree(c->d_markov);
   if (c->d_mops) (void)hipFree(c->d_mops);
   if (c->d_rwout) (void)hipFree(c->d_rwout);
-  void* dptrs[] = {c->d_dense_jobs, c->d_agree, c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
+  void* dptrs[] = {c->d_opool[0], c->d_opool[1], c->d_ojob[0], c->d_ojob[1], c->d_octl, c->d_dense_jobs, c->d_agree, c->d_gn28, c->d_bgr, c->d_lroot, c->d_strong, c->d_edge, c->d_det, c->d_mask, c->d_lab, c->d_eb, c->d_b1, c->d_b2, c->d_mbits, c->d_dbits, c->d_tbits, c->d_rowb,
                    c->d_frames, c->d_borders, c->d_bcount, c->d_boff, c->d_pool, c->d_scratch, c->d_quads, c->d_rpp, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq,
                    c->d_dense_c2w, c->d_dense_err, c->d_dense_np, c->d_pairs, c->d_gncam, c->d_rigio, c->d_gnobs, c->d_gnacc, c->d_sh_gidx, c->d_sh_pf, c->d_sh_flags, c->d_sh_rec, c->d_gen, c->d_hyps, c->d_st, c->d_sst, c->d_dbg, c->d_res, c->d_gauss, c->d_gtotal, c->d_lm};
   for (void* p : dptrs)

@@ -1931,13 +1931,91 @@ __device__ inline void op_end(RppItem* items, rpp::Refine* rf, FrameState* st, i
   }
 }
 
+// Tail compaction. A queue's jobs run from ~10 to ~2,700 iterations, so once
+// the queue is empty a wave is kept alive by its last few long jobs while its
+// other lanes idle -- and it still issues every instruction for 64 lanes
+// (rocprofv3: ~10.8k VALU instructions per wave trip against ~2.7k for one
+// lane's AbsKernel, profiles/r03_pmc_objpose.json). The queue therefore runs as
+// a few rounds (launches) over one grid: in every round but the last, a wave
+// whose queue is exhausted and whose busy lanes drop below `spill_below` writes
+// their ObjPose states to a pool and exits; the next round starts from that
+// pool with the surviving long jobs packed into full waves. A state is copied
+// bit for bit (OpState fields as doubles), so every job runs exactly the
+// iterations it would have run in place.
+constexpr int kOpFields = 80;  // doubles per spilled OpState (76 values + 3 ints + pad)
+struct OpPool {
+  double* state;   // [kOpFields][cap], SoA so a wave's stores coalesce
+  int32_t* job;    // [cap]
+  int32_t* ctl;    // [0] entries, [1] next entry to take
+};
+struct OpRound {
+  OpPool in, out;  // in: unused in round 0 (the queue's job list instead)
+  int32_t cap;     // entries a pool holds (>= the grid's lanes)
+  int32_t first, last, spill_below;
+};
+__device__ inline void op_save(const OpPool& p, int32_t cap, int k, const rpp::OpState& s) {
+  double* d = p.state + k;
+  int f = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[(size_t)cap * f++] = s.P.a[i];
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[(size_t)cap * f++] = s.Qi.a[i];
+#pragma unroll
+  for (int i = 0; i < rpp::NP; i++)
+#pragma unroll
+    for (int j = 0; j < 6; j++) d[(size_t)cap * f++] = s.F6[i][j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[(size_t)cap * f++] = s.G.a[i];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[(size_t)cap * f++] = s.R.a[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) d[(size_t)cap * f++] = s.t.a[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) d[(size_t)cap * f++] = s.pbar.a[i];
+  d[(size_t)cap * f++] = s.old_err;
+  d[(size_t)cap * f++] = s.new_err;
+  d[(size_t)cap * f++] = s.qx0;
+  d[(size_t)cap * f++] = s.qy0;
+  d[(size_t)cap * f++] = (double)s.it;
+  d[(size_t)cap * f++] = (double)s.init_pass;
+  d[(size_t)cap * f++] = (double)s.first;
+}
+__device__ inline void op_load(const OpPool& p, int32_t cap, int k, rpp::OpState& s) {
+  const double* d = p.state + k;
+  int f = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) s.P.a[i] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < 12; i++) s.Qi.a[i] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < rpp::NP; i++)
+#pragma unroll
+    for (int j = 0; j < 6; j++) s.F6[i][j] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < 9; i++) s.G.a[i] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < 9; i++) s.R.a[i] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.t.a[i] = d[(size_t)cap * f++];
+#pragma unroll
+  for (int i = 0; i < 3; i++) s.pbar.a[i] = d[(size_t)cap * f++];
+  s.old_err = d[(size_t)cap * f++];
+  s.new_err = d[(size_t)cap * f++];
+  s.qx0 = d[(size_t)cap * f++];
+  s.qy0 = d[(size_t)cap * f++];
+  s.it = (int)d[(size_t)cap * f++];
+  s.init_pass = (int)d[(size_t)cap * f++];
+  s.first = (int)d[(size_t)cap * f++];
+}
+static_assert(12 + 12 + 6 * rpp::NP + 9 + 9 + 3 + 3 + 4 + 3 <= kOpFields, "OpState fields");
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
                                                    const int32_t* __restrict__ jobs, RppQueue* q, FrameState* st,
-                                                   int paired) {
+                                                   int paired, OpRound rd) {
   const int lane = threadIdx.x & 63;
-  const int32_t njobs = MODE == 0 ? q->n0 : q->n1;
-  int32_t* next = MODE == 0 ? &q->next0 : &q->next1;
+  const int32_t njobs = rd.first ? (MODE == 0 ? q->n0 : q->n1) : min(rd.in.ctl[0], rd.cap);
+  int32_t* next = rd.first ? (MODE == 0 ? &q->next0 : &q->next1) : &rd.in.ctl[1];
   rpp::OpState s;
   int32_t job = -1;
   bool exhausted = false;
@@ -1954,14 +2032,40 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
       if (job < 0) {
         const int k = base + __popcll(idle & ((1ull << lane) - 1));
         if (k < njobs) {
-          job = jobs[k];
-          op_begin<MODE>(items, job, s);
+          if (rd.first) {
+            job = jobs[k];
+            op_begin<MODE>(items, job, s);
+          } else {
+            job = rd.in.job[k];
+            op_load(rd.in, rd.cap, k, s);
+          }
         }
       }
     }
-    if (__ballot(job >= 0) == 0) {
+    const uint64_t busy = __ballot(job >= 0);
+    if (busy == 0) {
       if (exhausted) break;
       continue;
+    }
+    const int nbusy = __popcll(busy);
+    if (exhausted && !rd.last && nbusy < rd.spill_below) {
+      // hand the long jobs to the next round and free the SIMD slot. A lane
+      // spills at most once per round and the pool holds the grid's lanes
+      // (launch_rpp_queues checks), so the reservation always fits; the test
+      // below only keeps a misconfigured launch in bounds (the wave then runs on)
+      const int leader = __ffsll((unsigned long long)busy) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&rd.out.ctl[0], nbusy);
+      base = __shfl(base, leader);
+      if (base + nbusy <= rd.cap) {
+        if (job >= 0) {
+          const int k = base + __popcll(busy & ((1ull << lane) - 1));
+          op_save(rd.out, rd.cap, k, s);
+          rd.out.job[k] = job;
+        }
+        break;
+      }
+      rd.last = 1;
     }
     if (job >= 0) {
       const int code = rpp::op_step(s);
