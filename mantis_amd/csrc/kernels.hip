@@ -244,6 +244,139 @@ __device__ inline void sobel4(const uint8_t* bl, int16_t* mag, int16_t* gx_s, in
   }
 }
 
+// Sobel separated, vertical pass first (MK_CANNY_V): per column the
+// smoothed sum vs = a + 2b + c and the difference vd = c - a of the three
+// blurred rows, then gx = vs(x+1) - vs(x-1) and gy = vd(x-1) + 2 vd(x) +
+// vd(x+1) -- the same integers as the 3x3 sums of sobel4, on u16 / i16 pairs
+// of columns (-1, 0), (1, 2), (3, 4) of the group, with (0, 1) and (2, 3)
+// taken from them by one v_perm each.
+__device__ inline void sobel4v(const uint8_t* bl, int16_t* mag, int16_t* gx_s, int16_t* gy_s, int t) {
+  for (int u = t; u < (FTH + 2) * FG4; u += 256) {
+    const int ly = u / FG4, k = u - ly * FG4;
+    u16x2 vs[3];
+    s16x2 vd[3];
+    u16x2 a[3], c[3];
+#pragma unroll
+    for (int r = 0; r < 3; r += 2) {
+      const uint32_t* row = (const uint32_t*)(bl + (ly + r) * FGW);
+      const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
+      u16x2* o = r == 0 ? a : c;
+      o[0] = vpk<u16x2>(__builtin_amdgcn_perm(wc, wp, 0x0c040c03u));  // columns -1, 0
+      o[1] = vpk<u16x2>(__builtin_amdgcn_perm(wc, wc, 0x0c020c01u));  // 1, 2
+      o[2] = vpk<u16x2>(__builtin_amdgcn_perm(wn, wc, 0x0c040c03u));  // 3, 4
+    }
+    {
+      const uint32_t* row = (const uint32_t*)(bl + (ly + 1) * FGW);
+      const uint32_t wc = row[k], wp = row[k > 0 ? k - 1 : 0], wn = row[k + 1 < FG4 ? k + 1 : k];
+      const u16x2 b0 = vpk<u16x2>(__builtin_amdgcn_perm(wc, wp, 0x0c040c03u));
+      const u16x2 b1 = vpk<u16x2>(__builtin_amdgcn_perm(wc, wc, 0x0c020c01u));
+      const u16x2 b2 = vpk<u16x2>(__builtin_amdgcn_perm(wn, wc, 0x0c040c03u));
+      const u16x2 two = {2, 2};
+      vs[0] = a[0] + c[0] + b0 * two;
+      vs[1] = a[1] + c[1] + b1 * two;
+      vs[2] = a[2] + c[2] + b2 * two;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) vd[j] = vpk<s16x2>(upk(c[j])) - vpk<s16x2>(upk(a[j]));
+    const s16x2 gx01 = vpk<s16x2>(upk(vs[1])) - vpk<s16x2>(upk(vs[0]));
+    const s16x2 gx23 = vpk<s16x2>(upk(vs[2])) - vpk<s16x2>(upk(vs[1]));
+    const s16x2 d01 = vpk<s16x2>(__builtin_amdgcn_perm(upk(vd[1]), upk(vd[0]), 0x05040302u));  // vd(0), vd(1)
+    const s16x2 d23 = vpk<s16x2>(__builtin_amdgcn_perm(upk(vd[2]), upk(vd[1]), 0x05040302u));  // vd(2), vd(3)
+    const s16x2 gy01 = vd[0] + vd[1] + (d01 << 1);
+    const s16x2 gy23 = vd[1] + vd[2] + (d23 << 1);
+    const s16x2 m01 = __builtin_elementwise_max(gx01, -gx01) + __builtin_elementwise_max(gy01, -gy01);
+    const s16x2 m23 = __builtin_elementwise_max(gx23, -gx23) + __builtin_elementwise_max(gy23, -gy23);
+    *(uint2*)(mag + ly * FGW + 4 * k) = make_uint2(upk(m01), upk(m23));
+    if (ly >= 1 && ly <= FTH && k >= 1 && k <= FTW / 4) {
+      const int jj = (ly - 1) * FTW + 4 * (k - 1);
+      *(uint2*)(gx_s + jj) = make_uint2(upk(gx01), upk(gx23));
+      *(uint2*)(gy_s + jj) = make_uint2(upk(gy01), upk(gy23));
+    }
+  }
+}
+
+// Interior NMS, four pixels per work-item on i16 pairs (MK_CANNY_V). Per
+// pixel the reference's rule (cv::Canny, the direction from |gy| 2^15 against
+// |gx| tan(22.5) 2^15 and |gx| tan(67.5) 2^15, the neighbour pair along it,
+// m > a && (diagonal ? m > b : m >= b), then weak / strong against low / high)
+// as masks: every comparison of values <= 2040 is the sign of a 16-bit
+// difference (v_pk_sub + v_pk_ashr 15), the direction tests are the signs of
+// two 24-bit multiply-adds, the neighbour choice is v_bfi on the pairs. The
+// classes of a group go to cls (byte u: candidate nibble | strong nibble << 4).
+__device__ inline uint32_t sign_pair(int32_t lo, int32_t hi) {  // 0xffff per negative half
+  return __builtin_amdgcn_perm((uint32_t)(hi >> 31), (uint32_t)(lo >> 31), 0x05040100u);
+}
+__device__ inline void nms4(const int16_t* mag, const int16_t* gx_s, const int16_t* gy_s, int low, int high,
+                            uint8_t* cls, int t) {
+  constexpr int SHIFT = 15;
+  constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
+  const int lowc = low < -1 ? -1 : (low > 32767 ? 32767 : low);
+  const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
+  const s16x2 LOW = {(short)lowc, (short)lowc}, HIGH = {(short)highc, (short)highc};
+  for (int u = t; u < FTH * FTW / 4; u += 256) {
+    const int ly = u >> 5, k = u & 31;  // FTW / 4 = 32 groups per row
+    uint32_t P[3][3], C[3][2];          // per row (up, centre, down): pairs (-1,0) (1,2) (3,4); (0,1) (2,3)
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      const int16_t* row = mag + (ly + r) * FGW + 4 * k;  // mag row ly + r = image row y0 + ly - 1 + r
+      const uint32_t lo = *(const uint32_t*)(row + 2);
+      const uint2 mid = *(const uint2*)(row + 4);
+      const uint32_t hi = *(const uint32_t*)(row + 8);
+      C[r][0] = mid.x;
+      C[r][1] = mid.y;
+      P[r][0] = __builtin_amdgcn_perm(mid.x, lo, 0x05040302u);
+      P[r][1] = __builtin_amdgcn_perm(mid.y, mid.x, 0x05040302u);
+      P[r][2] = __builtin_amdgcn_perm(hi, mid.y, 0x05040302u);
+    }
+    const uint2 gxw = *(const uint2*)(gx_s + ly * FTW + 4 * k);
+    const uint2 gyw = *(const uint2*)(gy_s + ly * FTW + 4 * k);
+    uint32_t push[2], strong[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t gxp = h ? gxw.y : gxw.x, gyp = h ? gyw.y : gyw.x;
+      const s16x2 X = vpk<s16x2>(gxp), Y = vpk<s16x2>(gyp);
+      const s16x2 AX = __builtin_elementwise_max(X, -X), AY = __builtin_elementwise_max(Y, -Y);
+      const uint32_t ax = upk(AX), ay = upk(AY);
+      const int ax0 = (int)(ax & 0xffffu), ax1 = (int)(ax >> 16);
+      const int ay0 = (int)(ay & 0xffffu) << SHIFT, ay1 = (int)(ay >> 16) << SHIFT;
+      // hor: ay 2^15 < ax TG22; ver: ay 2^15 > ax (TG22 + 2^16)
+      const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
+      const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
+      const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);  // gx gy < 0: the (up-right, down-left) diagonal
+      // neighbour pairs of pixels (2h, 2h+1): left / centre / right columns of each row
+      const uint32_t UL = P[0][h], U = C[0][h], UR = P[0][h + 1];
+      const uint32_t L = P[1][h], M = C[1][h], R = P[1][h + 1];
+      const uint32_t DL = P[2][h], D = C[2][h], DR = P[2][h + 1];
+      const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
+      const uint32_t B = (HOR & R) | (~HOR & ((VER & D) | (~VER & ((NEG & DL) | (~NEG & DR)))));
+      const s16x2 Ms = vpk<s16x2>(M);
+      const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
+      const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
+      const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
+      const uint32_t HV = HOR | VER;
+      const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
+      const uint32_t GTL = upk((LOW - Ms) >> 15);
+      push[h] = GTA & BC & GTL;
+      strong[h] = push[h] & upk((HIGH - Ms) >> 15);
+    }
+    // nibbles: pixel 2h + j <-> bit j of half h's word
+    const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
+    const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
+    const uint32_t x = xp | (xs << 4);
+    cls[u] = (uint8_t)(x | (x >> 16));
+  }
+}
+// 32-bit word of candidate (strong: hi) bits from 8 class bytes (groups 0..7)
+__device__ inline uint32_t nibbles32(uint64_t v, bool hi) {
+  uint64_t x = (hi ? v >> 4 : v) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  return (uint32_t)(x | (x >> 16));
+}
+#ifndef MK_CANNY_V
+#define MK_CANNY_V 1
+#endif
+
 // The Canny stages of one tile into the candidate / strong masks gm, sm (bit
 // i & 63 of word i >> 6 = tile pixel i, i = ly * FTW + lx). IN: the tile and its halo
 // (x0-4 .. x0+FTW+3, y0-3 .. y0+FTH+2) lie inside the image and the rows
@@ -261,7 +394,9 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     const int y = y0 - 3 + ly, xs = x0 - 4 + 4 * lg;
     uint8_t* o = g + ly * FGW + 4 * lg;
     if (IN) {
-      gu32* q = gwords(fd.bgr + ((size_t)y * W + xs) * 3);
+      // 32-bit offset from the frame base (frames are < 4 GB): global_load with
+      // the base in SGPRs, no per-lane 64-bit address arithmetic
+      gu32* q = gwords(fd.bgr + (uint32_t)(((uint32_t)y * (uint32_t)W + (uint32_t)xs) * 3u));
       *(uint32_t*)o = gray4(q[0], q[1], q[2]);
     } else if (y < 0 || y >= H) {
       o[0] = o[1] = o[2] = o[3] = 0;
@@ -282,8 +417,14 @@ __device__ inline void canny_classes(const FrameDesc& fd, int W, int H, int x0, 
     __syncthreads();
     vblur4((const uint16_t*)gxy, bl, t);
     __syncthreads();
-    sobel4(bl, mag, gx_s, gy_s, t);
+    if (MK_CANNY_V) sobel4v(bl, mag, gx_s, gy_s, t);
+    else sobel4(bl, mag, gx_s, gy_s, t);
     __syncthreads();
+    if (MK_CANNY_V) {
+      nms4(mag, gx_s, gy_s, low, high, (uint8_t*)gm, t);  // gm, sm: one 512-byte class array here
+      __syncthreads();
+      return;
+    }
   } else {
   // horizontal blur on rows y0-3 .. y0+FTH+2, columns x0-2 .. x0+FTW+1
   // (BORDER_REFLECT_101); staged in the gradient buffer, not live yet
@@ -409,20 +550,31 @@ __global__ __launch_bounds__(256) void k_canny(const FrameDesc* __restrict__ fra
   __shared__ __align__(16) uint8_t r1[R1];
   __shared__ __align__(16) uint8_t bl[BLH * FGW];
   __shared__ __align__(16) int16_t gxy[2 * FTW * FTH];
-  __shared__ uint64_t gm[FTW * FTH / 64], sm[FTW * FTH / 64];  // candidate / strong masks
+  // candidate / strong masks (generic tiles); interior tiles (MK_CANNY_V)
+  // keep one class byte per 4-pixel group in the same 512 bytes
+  __shared__ uint64_t gms[2 * FTW * FTH / 64];
+  uint64_t* gm = gms;
+  uint64_t* sm = gms + FTW * FTH / 64;
   const int t = threadIdx.x;
   const bool interior = vec && x0 >= 4 && x0 + FTW + 4 <= W && y0 >= 3 && y0 + FTH + 3 <= H;
   if (interior) canny_classes<true>(fd, W, H, x0, y0, low, high, vec, r1, bl, (int16_t*)r1, gxy, gm, sm, t);
   else canny_classes<false>(fd, W, H, x0, y0, low, high, vec, r1, bl, (int16_t*)r1, gxy, gm, sm, t);
-  // 32-bit word j of the tile = row j / 4, quarter j % 4 = half j & 1 of mask j / 2
+  // 32-bit word j of the tile = row j / 4, quarter j % 4 = half j & 1 of mask
+  // j / 2 (generic), class bytes 8j .. 8j + 7 (interior)
   const int WW = bits::words(W);
   static_assert(FTW == 128, "four 32-pixel words per tile row");
   for (int j = t; j < FTW * FTH / 32; j += 256) {
     const int y = y0 + (j >> 2), w = (x0 >> 5) + (j & 3);
     if (y < H && w < WW) {
       const size_t o = (size_t)f * bstride + (size_t)y * WW + w;
-      cbits[o] = (uint32_t)(gm[j >> 1] >> (32 * (j & 1)));
-      sbits[o] = (uint32_t)(sm[j >> 1] >> (32 * (j & 1)));
+      if (MK_CANNY_V && interior) {
+        const uint64_t v = ((const uint64_t*)gms)[j];
+        cbits[o] = nibbles32(v, false);
+        sbits[o] = nibbles32(v, true);
+      } else {
+        cbits[o] = (uint32_t)(gm[j >> 1] >> (32 * (j & 1)));
+        sbits[o] = (uint32_t)(sm[j >> 1] >> (32 * (j & 1)));
+      }
     }
   }
 }
