@@ -86,7 +86,7 @@ def parse():
                    help="config 2: timed 256-hypothesis scoring microbatches")
     p.add_argument("--rigs", type=int, default=None,
                    help="rigs per step per GPU (config 3, default 1024 per context) / rigs per step (config 4, "
-                        "default 128)")
+                        "default 512)")
     p.add_argument("--frames", type=int, default=16, help="config 5: frames per step (16,200 hypotheses each)")
     p.add_argument("--distinct", type=int, default=128, help="distinct rendered rigs (cycled through the batch)")
     p.add_argument("--contexts", type=int, default=4,
@@ -117,7 +117,10 @@ def parse():
                         "points used, max seen 28k; 262144 at 1080p); overflow is an error")
     a = p.parse_args()
     if a.rigs is None:
-        a.rigs = 1024 * a.contexts if a.config == 3 else 128
+        # config 4: 512 rigs (128 per context at one rank) so the ObjPose chain
+        # floor of a launch (~25 ms) is shared by enough frames: 128 / 256 /
+        # 512 / 1024 rigs gave 2.3k / 3.3k / 4.2k / 4.8k rig poses/s on 1 GPU
+        a.rigs = 1024 * a.contexts if a.config == 3 else 512
     if a.hw_queues is None:
         a.hw_queues = 4 * a.contexts
     if a.max_contour_points is None:
