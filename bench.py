@@ -450,6 +450,49 @@ def run_config3(a, rk, cpu):
         roof["objpose_iterations_per_launch"] = iters
     roof_front = roofline("canny_nms")
 
+    # ---- the same rooflines from kernel durations (rocprofv3 batch-launch
+    # averages of this command, committed under profiles/): the event spans
+    # above also hold the queue waits between a stage's kernels
+    stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_final"), "canny_nms": ("k_canny",),
+                     "hysteresis": ("k_hyst_count", "k_run_scan", "k_hyst_runs", "k_hyst_band", "k_hyst_seam",
+                                    "k_hyst_mark", "k_hyst_fix"),
+                     "morph": ("k_morph",)}
+    prof_src = os.path.join("profiles", "r03_batch_launch_avg_default.json")
+
+    def profiled(r, stage):
+        if r is None or stage not in stage_kernels or a.rigs != 4096 or nctx != 4:
+            return  # the committed profile is of the default command
+        try:
+            pj = json.load(open(os.path.join(ROOT, prof_src)))
+        except (OSError, ValueError):
+            return
+        ms = 0.0
+        for k in stage_kernels[stage]:
+            hit = [v["avg_ms"] for name, v in pj.items() if ("::" + k + "<") in name or name.endswith("::" + k)]
+            if not hit:
+                return
+            ms += hit[0]
+        amount = work[stage][1]
+        ach = amount / (ms * 1e-3) / (1e9 if r["unit"] == "GB/s" else 1e12)
+        r["profiled"] = {"source": prof_src, "kernel_sum_ms": round(ms, 4), "achieved": round(ach, 4),
+                         "frac": round(ach / r["peak"], 5),
+                         "note": "sum of the stage kernels' rocprofv3 durations (batch launches, 4 contexts)"}
+
+    profiled(roof, dom)
+    profiled(roof_front, "canny_nms")
+    # HBM reads of the scoring kernels (FETCH_SIZE, kB per launch of 1024 frames,
+    # tools/pmc_score.sh; no write counter in that pass set), per this launch
+    if roof is not None and dom == "score_pf_yaw" and roof.get("traffic") is None:
+        try:
+            pj = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_score_screen.json")))
+            fk = sum(v["FETCH_SIZE"] for k, v in pj.items() if "k_score_" in k)
+            roof["traffic"] = int(fk * 1024 / 1024 * frames_step)
+            roof["traffic_note"] = ("HBM read bytes from FETCH_SIZE of k_score_init/pf/final "
+                                    "(profiles/r03_pmc_score_screen.json, 1024-frame launches, scaled per frame); "
+                                    "the stage is FP64-issue / gather-latency bound, not HBM-bound")
+        except (OSError, ValueError, KeyError):
+            pass
+
     # ---- the same stages with context 0 running alone (one step, after the
     # timed region): the timed-region launch durations above include the
     # other contexts' kernels sharing the CUs; these are the kernels' own

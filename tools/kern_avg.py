@@ -1,7 +1,10 @@
 """Per-kernel average of the batch launches from a rocprofv3 kernel trace CSV:
 for each kernel, the dispatches with its largest grid (the batch launches;
 the latency runs' single-rig launches have smaller grids), averaged.
-Usage: kern_avg.py <trace.csv> [max rows]"""
+Usage: kern_avg.py <trace.csv> [max rows] [out.json]  (the JSON maps the kernel
+name to its batch-launch average in ms and the number of such launches; bench.py
+reads profiles/r03_batch_launch_avg_default.json for its profiled roofline)"""
+import json
 import collections
 import csv
 import sys
@@ -20,3 +23,5 @@ for k, v in d.items():
 out.sort(reverse=True)
 for a, k, n, m in out[:top]:
     print(f"{a:9.3f} ms  {k}  ({n} of {m} launches)")
+if len(sys.argv) > 3:
+    json.dump({k: {"avg_ms": round(a, 4), "launches": n} for a, k, n, m in out}, open(sys.argv[3], "w"), indent=1)
