@@ -358,6 +358,13 @@ mantis_status mantis_set_profiling(void* ctx, int32_t on);
  * hypotheses, PF/shift/yaw errors); layout = oracle/oracle.h orc_frame_debug. */
 size_t mantis_frame_debug_size(void);
 mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t bytes);
+/* The border-following output of camera-frame `frame` of the last batch
+ * (findContours(RETR_CCOMP, CHAIN_APPROX_SIMPLE), QuadDetection.h:216, in the
+ * library's border order): per border its point count and hole flag, and all
+ * points (x, y pairs, image coordinates) border after border. Fails with
+ * MANTIS_ERR_CAPACITY when max_borders / max_points are too small. */
+mantis_status mantis_get_contours(void* ctx, int32_t frame, int32_t* counts, int32_t* holes, int32_t max_borders,
+                                  int32_t* points, int32_t max_points, int32_t* n_borders);
 /* Work counters of camera-frame `frame` of the last batch: borders, contour
  * points, raw/kept quads, generated/clustered hypotheses, PF flag, gaussian
  * offset, overflow flags, then 7 contour-kernel phase ends (10 ns ticks).

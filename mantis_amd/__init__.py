@@ -127,6 +127,8 @@ _SIGS = {
     "mantis_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "mantis_frame_debug_size": (C.c_size_t, []),
     "mantis_get_frame_debug": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_size_t]),
+    "mantis_get_contours": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
+                                      C.c_void_p]),
     "mantis_frame_counters": (C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]),
     "mantis_gn_accumulate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32,
                                        C.c_void_p]),
@@ -399,6 +401,21 @@ class Mantis:
         obs = np.zeros((cap, 6))
         self._chk(lib().mantis_get_rig_gn(self.h, rig, C.byref(info), obs.ctypes.data, cap), "get_rig_gn")
         return info, obs[: min(cap, info.n_obs_local if info.valid else 0)].copy()
+
+    def contours(self, i, max_borders=8192, max_points=1 << 20):
+        """Border-following output of frame i of the last batch: a list of
+        (points (n, 2) int32, hole) in the library's border order."""
+        cnt = np.zeros(max_borders, np.int32)
+        hol = np.zeros(max_borders, np.int32)
+        pts = np.zeros(2 * max_points, np.int32)
+        nb = C.c_int32(0)
+        self._chk(lib().mantis_get_contours(self.h, i, cnt.ctypes.data, hol.ctypes.data, max_borders,
+                                            pts.ctypes.data, max_points, C.byref(nb)), "get_contours")
+        out, k = [], 0
+        for b in range(nb.value):
+            out.append((pts[2 * k: 2 * (k + cnt[b])].reshape(-1, 2).copy(), int(hol[b])))
+            k += int(cnt[b])
+        return out
 
     def frame_counters(self, i):
         out = np.zeros(32, np.int32)

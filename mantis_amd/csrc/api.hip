@@ -162,6 +162,7 @@ struct Ctx {
   int32_t* d_octl = nullptr;  // [2][2]: entries, next
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
+  int seg_m = 64;  // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -397,16 +398,19 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
                                        kMaxBorders);
   mark(c, "components");
   const size_t tb_lds = (size_t)dbits_wpw(Wp) * Hp * sizeof(uint32_t);
+  k_seg_plan<<<n, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, c->d_borders,
+                                  c->d_st, c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders, c->seg_m);
   if (c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames) {
-    k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount,
-                                                   c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders);
+    k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_scratch,
+                                                   c->pool_cap, Wp, Hp, kMaxBorders, c->d_rowb, c->rstride, rx, P);
   } else {
     const int wpw = dbits_wpw(Wp);
     k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, 32 * wpw * sizeof(uint32_t), c->s>>>(c->d_dbits, c->dstride, c->d_tbits,
                                                                                   c->tstride, wpw, Hp);
-    k_trace_borders<<<n, 64, 0, c->s>>>(c->d_tbits, c->tstride, c->d_borders, c->d_st, c->d_bcount, c->d_scratch,
-                                        c->pool_cap, Wp, kMaxBorders);
+    k_trace_borders<<<n, 64 * MK_TB_WAVES, 0, c->s>>>(c->d_tbits, c->tstride, c->d_borders, c->d_st, c->d_scratch, c->pool_cap, Wp,
+                                        kMaxBorders, c->d_rowb, c->rstride, rx, P);
   }
+  k_seg_chain<<<n, 256, 0, c->s>>>(c->d_st, c->d_bcount, c->d_scratch, c->pool_cap, kMaxBorders);
   mark(c, "border_trace");
   // small batches (latency): 1024 threads per frame; large ones: 256, so the
   // per-frame blocks fit beside other contexts' kernels on a CU
@@ -794,6 +798,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
@@ -1410,6 +1415,39 @@ mantis_status mantis_get_frame_debug(void* ctx, int32_t frame, void* out, size_t
   return MANTIS_OK;
 }
 size_t mantis_frame_debug_size(void) { return sizeof(FrameDebug); }
+
+mantis_status mantis_get_contours(void* ctx, int32_t frame, int32_t* counts, int32_t* holes, int32_t max_borders,
+                                  int32_t* points, int32_t max_points, int32_t* n_borders) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !counts || !holes || !points || !n_borders || frame < 0 || frame >= c->F || !c->h_st) return MANTIS_ERR_ARG;
+  const int nb = std::min(c->h_st[frame].n_borders, kMaxBorders);
+  *n_borders = nb;
+  if (nb > max_borders) { c->err = "mantis_get_contours: max_borders too small"; return MANTIS_ERR_CAPACITY; }
+  std::vector<int32_t> cnt(nb), off(nb);
+  std::vector<Border> bs(nb);
+  const size_t fb = (size_t)frame * kMaxBorders;
+  if (nb > 0) {
+    HIP_OK(hipMemcpy(cnt.data(), c->d_bcount + fb, sizeof(int32_t) * nb, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(off.data(), c->d_boff + fb, sizeof(int32_t) * nb, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(bs.data(), c->d_borders + fb, sizeof(Border) * nb, hipMemcpyDeviceToHost));
+  }
+  size_t total = 0;
+  for (int b = 0; b < nb; b++) total += (size_t)cnt[b];
+  if (total > (size_t)max_points) { c->err = "mantis_get_contours: max_points too small"; return MANTIS_ERR_CAPACITY; }
+  std::vector<int32_t> pool(2 * (size_t)c->pool_cap);
+  HIP_OK(hipMemcpy(pool.data(), c->d_pool + 2 * (size_t)frame * c->pool_cap, sizeof(int32_t) * pool.size(),
+                   hipMemcpyDeviceToHost));
+  size_t k = 0;
+  for (int b = 0; b < nb; b++) {
+    counts[b] = cnt[b];
+    holes[b] = bs[b].hole;
+    if ((size_t)off[b] + cnt[b] > (size_t)c->pool_cap) { c->err = "mantis_get_contours: pool overflow"; return MANTIS_ERR_CAPACITY; }
+    std::memcpy(points + 2 * k, pool.data() + 2 * (size_t)off[b], sizeof(int32_t) * 2 * cnt[b]);
+    k += cnt[b];
+  }
+  return MANTIS_OK;
+}
 
 int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t max) {
   Ctx* c = (Ctx*)ctx;

@@ -1299,8 +1299,14 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
       b.start = key - 1; b.hole = 1; b.parent = py * Wp + X[pr];
     }
     const int idx = atomicAdd(&st[f].n_borders, 1);
-    if (idx < cap) borders[(size_t)f * cap + idx] = b;
-    else atomicOr(&st[f].overflow, 1);
+    if (idx < cap) {
+      borders[(size_t)f * cap + idx] = b;
+      // border index of the root run, above the labels (k_seg_plan; it checks the fit)
+      const int nruns = r[Hp];
+      if (2 * (size_t)nruns <= plane) L[nruns + id] = idx;
+    } else {
+      atomicOr(&st[f].overflow, 1);
+    }
   }
 }
 
@@ -1324,72 +1330,40 @@ __device__ inline void build_next_lut(uint8_t* lut, int tid, int nthreads) {
   }
 }
 
-// trace_border_nb_em (mk_contour.h, host-checked against the oracle) driven
-// by the table: the same point sequence.
-template <class NB, class EM>
-__device__ int trace_border_lut(const NB& nb, const uint8_t* lut, int sx, int sy, bool hole, EM& em,
-                                int* steps_max = nullptr) {
-  int steps = 0;
-  int x = sx, y = sy;
-  uint32_t m = nb(x, y);
-  const int s_end0 = hole ? 0 : 4;
-  int s = s_end0;
-  do {
-    s = (s - 1) & 7;
-  } while (!((m >> s) & 1u) && s != s_end0);
-  int px = sx - 1, py = sy - 1;
-  if (s == s_end0) {
-    em(px, py);
-    return 1;
-  }
-  const int x1 = sx + fdx(s), y1 = sy + fdy(s);
-  int n = 0;
-  int prev_s = s ^ 4;
-  uint32_t p9 = nb.row3(x, y - 1) | (nb.row3(x, y) << 3) | (nb.row3(x, y + 1) << 6);
-  for (;;) {
-    s = lut[(p9 << 3) | s];
-    if (s != prev_s) {
-      em(px, py);
-      n++;
-      prev_s = s;
-    }
-    const int dx = fdx(s), dy = fdy(s);
-    px += dx;
-    py += dy;
-    const int x4 = x + dx, y4 = y + dy;
-    if (x4 == sx && y4 == sy && x == x1 && y == y1) break;
-    x = x4;
-    y = y4;
-    p9 = nb.row3(x, y - 1) | (nb.row3(x, y) << 3) | (nb.row3(x, y + 1) << 6);
-    s = (s + 4) & 7;
-    steps++;
-  }
-  if (steps_max) atomicMax(steps_max, steps);
-  return n;
-}
-
 // Single-pass border tracing: points go to 64-point chunks handed out by an
 // LDS bump allocator; a wave per chunk then compacts them by border.
-constexpr int kChunk = 64;
+// 16-point chunks: a segmented walk (k_seg_plan) leaves one partial chunk per
+// segment, so the chunk storage (the pool's size in points) must hold the
+// points plus < 16 per segment (64-point chunks overflowed it on dense frames)
+constexpr int kChunk = 16;
+// Chunk c holds ccount[c] points that go to positions ordv[c] .. of its
+// owner's point list (owner = border; during segmented walks the segment,
+// k_seg_chain then adds the segment's offset in its border and maps the owner).
 struct ChunkEmit {
   int32_t* chunks;  // [chunk][64][2]
-  int32_t* owner;   // border of each chunk
-  int32_t* ordv;    // ordinal of the chunk within its border
+  int32_t* owner;   // border (or segment) of each chunk
+  int32_t* ordv;    // first point position of the chunk within its owner
+  int32_t* ccount;  // points in the chunk
   int32_t* counter; // LDS
   int max_chunks, border, cur, k, nch;
   bool ovf;
+  int n_pts = 0;  // the walk's point count (walk_segment_lds)
   __device__ void operator()(int px, int py) {
     if (cur < 0 || k == kChunk) {
       if (ovf) return;
+      if (cur >= 0) ccount[cur] = kChunk;
       const int c = atomicAdd(counter, 1);
       if (c >= max_chunks) { ovf = true; return; }
       cur = c;
       k = 0;
       owner[c] = border;
-      ordv[c] = nch++;
+      ordv[c] = kChunk * nch++;
     }
     *(int2*)(chunks + 2 * ((size_t)cur * kChunk + k)) = make_int2(px, py);  // one 8-byte store
     k++;
+  }
+  __device__ void flush() {
+    if (cur >= 0) ccount[cur] = k;
   }
 };
 
@@ -1544,6 +1518,7 @@ struct BitsTiled {
 struct Walk {
   uint32_t pos, spos, p1;  // current, start, and the start's last neighbour
   int s, prev_s, n, steps;
+  int first;               // the next step is the segment's first (never a checkpoint stop)
 };
 __device__ inline uint32_t wpos(int x, int y) { return (uint32_t)x | ((uint32_t)y << 16); }
 __device__ inline uint32_t wdelta(int s) { return (uint32_t)(fdx(s) + (fdy(s) << 16)); }
@@ -1569,16 +1544,99 @@ __device__ inline bool walk_start(const NB& nb, int sx, int sy, bool hole, EM& e
   w.s = s;
   return true;
 }
+// ------------------------------------------------ segmented border walks
+// A long border (the outer border of the grid's net, the large holes: 4.5k-
+// 9k steps, the frame's critical path) is walked as segments in parallel.
+// Checkpoints are fixed visits of the walk: in every row y = M k (padded
+// coordinates), each foreground run [a, b] gives the visit of pixel a whose
+// swept background arc holds its west neighbour and the visit of b whose arc
+// holds its east neighbour. Each such visit lies on exactly one border (the
+// one between the run's component and the background component on that side)
+// and occurs exactly once in that border's walk, and its walk state follows
+// from the 3x3 neighbourhood alone: the search start is the first foreground
+// direction clockwise from the arc's direction. So a segment starts at a
+// checkpoint with the state the whole walk would have there, emits exactly
+// the points the whole walk emits, and stops on arriving at the next
+// checkpoint visit (a local test: row y = M k and the arc about to be swept
+// holds west or east) or at its border's closing move. k_seg_chain then links
+// the segments of each border from its start in walk order: the point
+// sequence is findContours' (QuadDetection.h:216), bit for bit.
+constexpr int kSegRows = 512;     // sampled rows per frame (Hp <= 512 M)
+constexpr int kSegCap = 65536;    // segments per frame
+struct SegTab {
+  int32_t* rowbase;  // first checkpoint id of each sampled row (2 per foreground run)
+  int32_t *border, *pos, *sdir, *next, *cnt, *off;
+  int cap;
+};
+// in the scratch after the chunk planes (chunks 2 pc, owner / ordv / ccount 3 mc)
+__device__ inline SegTab seg_tab(int32_t* sc, int pool_cap) {
+  const long mc = pool_cap / kChunk;
+  int32_t* base = sc + 2 * (size_t)pool_cap + 3 * (size_t)mc;
+  const long avail = 4L * pool_cap - (2L * pool_cap + 3L * mc) - kSegRows;
+  SegTab t;
+  t.cap = (int)(avail / 6 < kSegCap ? avail / 6 : kSegCap);
+  t.rowbase = base;
+  int32_t* q = base + kSegRows;
+  t.border = q;
+  t.pos = q + t.cap;
+  t.sdir = q + 2 * (size_t)t.cap;
+  t.next = q + 3 * (size_t)t.cap;
+  t.cnt = q + 4 * (size_t)t.cap;
+  t.off = q + 5 * (size_t)t.cap;
+  return t;
+}
+// sdir codes of a segment: >= 0 checkpoint (search start), -1 unused (the
+// right visit of a one-pixel run that is its left visit), -2 start segment
+// aliased to the checkpoint at its border's start (next = that id), -3 start
+// segment walked from the border start, -4 isolated pixel (one point)
+constexpr int kSegUnused = -1, kSegAlias = -2, kSegStart = -3, kSegSingle = -4;
+// checkpoint id of the visit of pixel (x, y) on the west (side 0) / east (1)
+// arc: its foreground run in the row's run list (run 0 of a row is the
+// background ring, foreground runs have odd local indices)
+__device__ inline int seg_id_at(int x, int y, int side, int M, const int32_t* r, const uint16_t* X,
+                                const int32_t* rowbase) {
+  const int j0 = r[y];
+  const int j = j0 + run_at(X + j0, r[y + 1] - j0, x);
+  return rowbase[y / M - 1] + 2 * ((j - j0 - 1) >> 1) + side;
+}
+// does the arc swept from search start s to the found direction sn (both
+// exclusive, counter-clockwise) hold direction d
+__device__ inline bool arc_has(int s, int sn, int d) { return ((d - s - 1) & 7) < ((sn - s - 1) & 7); }
+// first foreground direction clockwise from d - 1 (the search start of the
+// visit whose arc holds d); d if there is none (an isolated pixel)
+__device__ inline int first_cw(uint32_t m, int d) {
+  int s = d;
+  do {
+    s = (s - 1) & 7;
+  } while (!((m >> s) & 1u) && s != d);
+  return s;
+}
+// the walk at a checkpoint visit
+template <class NB>
+__device__ inline void seg_begin(const NB& nb, const Border& b, int Wp, uint32_t pos, int sd, Walk& w) {
+  const int sx = b.start % Wp, sy = b.start / Wp;
+  const int s0 = first_cw(nb(sx, sy), b.hole ? 0 : 4);  // the border start's last neighbour (walk_start)
+  w.spos = wpos(sx, sy);
+  w.p1 = wpos(sx + fdx(s0), sy + fdy(s0));
+  w.pos = pos;
+  w.s = sd;
+  w.prev_s = (sd + 4) & 7;
+  w.n = 0;
+  w.steps = 0;
+  w.first = 1;
+}
 // one step of the follower on the tiled plane (BitsTiled layout, wpw32 = 32 *
-// words per row); false once the border closed
+// words per row); false once the segment ended: nx = the next segment's
+// checkpoint id, -1 when the border closed
 template <class EM>
-__device__ inline bool walk_step(const uint64_t* __restrict__ tb, int wpw32, const uint8_t* lut, EM& em, Walk& w) {
+__device__ inline bool walk_step(const uint64_t* __restrict__ tb, int wpw32, const uint8_t* lut, EM& em, Walk& w,
+                                 int M, const int32_t* r, const uint16_t* X, const int32_t* rowbase, int& nx) {
   const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
   const int xm = x - 1, col = xm & ~31, sh = xm & 31;
   const char* base = (const char*)tb;
-  const int r = y & 31, t0 = (y >> 5) * wpw32 + col, om = t0 + r;
-  const uint32_t off[3] = {(uint32_t)(r == 0 ? t0 - wpw32 + 31 : om - 1), (uint32_t)om,
-                           (uint32_t)(r == 31 ? t0 + wpw32 : om + 1)};
+  const int rr = y & 31, t0 = (y >> 5) * wpw32 + col, om = t0 + rr;
+  const uint32_t off[3] = {(uint32_t)(rr == 0 ? t0 - wpw32 + 31 : om - 1), (uint32_t)om,
+                           (uint32_t)(rr == 31 ? t0 + wpw32 : om + 1)};
   uint32_t p9 = 0;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -1586,83 +1644,311 @@ __device__ inline bool walk_step(const uint64_t* __restrict__ tb, int wpw32, con
     p9 |= ((uint32_t)(v >> sh) & 7u) << (3 * k);
   }
   const int s = lut[(p9 << 3) | w.s];
+  if (M > 0 && !w.first && y % M == 0) {
+    const bool west = arc_has(w.s, s, 4);
+    if (west || arc_has(w.s, s, 0)) {
+      nx = seg_id_at(x, y, west ? 0 : 1, M, r, X, rowbase);
+      return false;
+    }
+  }
+  w.first = 0;
   if (s != w.prev_s) {
     em(x - 1, y - 1);
     w.n++;
     w.prev_s = s;
   }
   const uint32_t np = w.pos + wdelta(s);
-  if (np == w.spos && w.pos == w.p1) return false;
+  if (np == w.spos && w.pos == w.p1) {
+    nx = -1;
+    return false;
+  }
   w.pos = np;
   w.s = (s + 4) & 7;
   w.steps++;
   return true;
 }
 
-// 1. follow every border once: one wave per frame (the tiled bit plane in
-// L2), each lane walking one border at a time and refilled from the frame's
-// border list once a quarter of the wave is idle, so a frame costs about its
-// longest walk (the outer border of the grid lines, ~5-9k steps) instead of
-// the sum over static batches of each batch's longest. Points go to 64-point
-// chunks handed out by a per-frame counter.
-__global__ __launch_bounds__(64) void k_trace_borders(const uint32_t* __restrict__ tbits, size_t tstride,
+// The frame's segments (before the walks; one block per frame): checkpoints
+// of the sampled rows with their border (the run's component, or the hole on
+// that side when the run's component encloses it: the hole's root run has the
+// component's run on its left, k_run_border's parent rule), search start and
+// kind; then one start segment per border, aliased to its start's checkpoint
+// when the start lies in a sampled row. M = 0, too many rows or segments, or
+// a label plane too full for the border-index map: borders walked whole.
+struct BitsRows {  // the padded bit plane, row-major (dbits)
+  const uint32_t* b;
+  int wpw;
+  __device__ uint32_t row3(int x, int y) const {
+    const uint32_t* p = b + (size_t)y * wpw + ((x - 1) >> 5);
+    const uint64_t v = ((uint64_t)p[1] << 32) | p[0];
+    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  }
+  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
+};
+__global__ __launch_bounds__(256) void k_seg_plan(const uint32_t* __restrict__ dbits, size_t dstride,
+                                                  const int32_t* __restrict__ rowb, size_t rstride,
+                                                  const uint16_t* __restrict__ rx, int32_t* lab, size_t plane,
+                                                  const Border* __restrict__ borders, FrameState* st,
+                                                  int32_t* __restrict__ scratch, int pool_cap, int Wp, int Hp,
+                                                  int border_cap, int M) {
+  __shared__ int32_t rb[kSegRows + 1];
+  __shared__ int32_t wsum[4];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
+  int32_t* L = lab + (size_t)f * plane;
+  const int nruns = r[Hp];
+  const int32_t* bidx = L + nruns;  // k_run_border: border index of each root run
+  int nb = st[f].n_borders;
+  if (nb > border_cap) nb = border_cap;
+  SegTab T = seg_tab(scratch + 4 * (size_t)f * pool_cap, pool_cap);
+  if (nb > T.cap) {  // a contour pool too small for one record per border
+    if (t == 0) atomicOr(&st[f].overflow, 2);
+    nb = T.cap;
+  }
+  const Border* bs = borders + (size_t)f * border_cap;
+  const int nsr = M > 0 ? (Hp - 2) / M : 0;  // sampled rows y = M, 2M, .. <= Hp - 2
+  bool split = M > 0 && nsr > 0 && nsr <= kSegRows && 2 * (size_t)nruns <= plane;
+  // checkpoint ids: 2 per foreground run of each sampled row
+  static_assert(kSegRows <= 512, "two passes of 256 sampled rows");
+  int carry = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    int v = 0;
+    const int k = pass * 256 + t;
+    if (split && k < nsr) {
+      const int y = (k + 1) * M;
+      v = 2 * ((r[y + 1] - r[y] - 1) >> 1);
+    }
+    const int inc = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int o = carry;
+    for (int q = 0; q < wave; q++) o += wsum[q];
+    if (k < kSegRows) rb[k] = o + inc - v;
+    carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  int NC = split ? carry : 0;
+  if (NC + nb > T.cap) {
+    split = false;
+    NC = 0;
+  }
+  if (t == 0) {
+    st[f].seg_nc = NC;
+    st[f].seg_m = split ? M : 0;
+  }
+  for (int k = t; k < nsr && split; k += 256) T.rowbase[k] = rb[k];
+  const BitsRows nbh{dbits + (size_t)f * dstride, dbits_wpw(Wp)};
+  if (split) {
+    for (int k = 0; k < nsr; k++) {
+      const int y = (k + 1) * M, j0 = r[y], nfg = (r[y + 1] - j0 - 1) >> 1;
+      for (int i = t; i < nfg; i += 256) {
+        const int g = j0 + 2 * i + 1;
+        const int x0 = X[g], x1 = (int)X[g + 1] - 1;
+        const int fr = uf_find_c(L, g);
+        const int id = rb[k] + 2 * i;
+        // west visit of x0: the border against the background run on the left
+        {
+          const int bg = uf_find_c(L, g - 1);
+          const int own = (bg != 0 && uf_find_c(L, bg - 1) == fr) ? bg : fr;
+          const uint32_t m = nbh(x0, y);
+          const int sd = first_cw(m, 4);
+          T.border[id] = bidx[own];
+          T.pos[id] = (int32_t)wpos(x0, y);
+          T.sdir[id] = sd == 4 ? kSegSingle : sd;
+          T.next[id] = -1;
+          T.cnt[id] = 0;
+        }
+        // east visit of x1 (for a one-pixel run, the west visit when its arc also holds east)
+        {
+          const int bg = uf_find_c(L, g + 1);
+          const int own = (bg != 0 && uf_find_c(L, bg - 1) == fr) ? bg : fr;
+          const uint32_t m = nbh(x1, y);
+          int sd = first_cw(m, 0);
+          if (sd == 0) {
+            sd = kSegUnused;  // isolated pixel: its west visit is the border
+          } else if (x1 == x0) {
+            const int sw = first_cw(m, 4);
+            const uint32_t rr = ((m | (m << 8)) >> (sw + 1)) & 0xffu;
+            if (arc_has(sw, (sw + 1 + __builtin_ctz(rr)) & 7, 0)) sd = kSegUnused;
+          }
+          T.border[id + 1] = bidx[own];
+          T.pos[id + 1] = (int32_t)wpos(x1, y);
+          T.sdir[id + 1] = sd;
+          T.next[id + 1] = -1;
+          T.cnt[id + 1] = 0;
+        }
+      }
+    }
+  }
+  __syncthreads();  // the checkpoints' kinds, for the aliases below
+  // start segments
+  for (int b = t; b < nb; b += 256) {
+    const Border bb = bs[b];
+    const int sx = bb.start % Wp, sy = bb.start / Wp, id = NC + b;
+    T.border[id] = b;
+    T.cnt[id] = 0;
+    T.pos[id] = (int32_t)wpos(sx, sy);
+    if (split && sy % M == 0 && sy <= Hp - 2) {
+      T.sdir[id] = kSegAlias;
+      int c = seg_id_at(sx, sy, bb.hole ? 1 : 0, M, r, X, rb);
+      if (T.sdir[c] == kSegUnused) c--;  // a one-pixel run whose west visit is also its east one
+      T.next[id] = c;
+    } else {
+      T.sdir[id] = kSegStart;
+      T.next[id] = -1;
+    }
+  }
+}
+
+// Per border, its segments in walk order from the start: offsets of their
+// points, the border's point count; then every chunk gets its border and
+// its points' positions in the border's list. A chain that does not close
+// within the frame's segment count, or that passes a segment planned for
+// another border, marks the frame overflowed (its quads are dropped).
+__global__ __launch_bounds__(256) void k_seg_chain(FrameState* st, int32_t* __restrict__ counts,
+                                                   int32_t* __restrict__ scratch, int pool_cap, int border_cap) {
+  const int f = blockIdx.x, t = threadIdx.x;
+  int nb = st[f].n_borders;
+  if (nb > border_cap) nb = border_cap;
+  int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
+  SegTab T = seg_tab(sc, pool_cap);
+  int32_t* cnt = counts + (size_t)f * border_cap;
+  for (int b = T.cap + t; b < nb; b += 256) cnt[b] = 0;  // past the segment table (overflow flagged)
+  if (nb > T.cap) nb = T.cap;
+  const int NC = st[f].seg_nc, NS = NC + nb;
+  for (int b = t; b < nb; b += 256) {
+    // from the start's segment until the walk is back at the start: a segment
+    // ends at the start checkpoint (aliased starts) or on the closing move (-1)
+    const int start = T.sdir[NC + b] == kSegAlias ? T.next[NC + b] : NC + b;
+    int cur = start, acc = 0, k = 0;
+    bool bad = false;
+    do {
+      if (++k > NS || T.border[cur] != b) {
+        bad = true;
+        break;
+      }
+      T.off[cur] = acc;
+      acc += T.cnt[cur];
+      cur = T.next[cur];
+    } while (cur >= 0 && cur != start);
+    cnt[b] = acc;
+    if (bad) atomicOr(&st[f].overflow, 2);
+  }
+  __syncthreads();
+  const int max_chunks = pool_cap / kChunk;
+  int nch = st[f].n_chunks;
+  if (nch > max_chunks) nch = max_chunks;
+  int32_t* owner = sc + 2 * (size_t)pool_cap;
+  int32_t* ordv = owner + max_chunks;
+  for (int c = t; c < nch; c += 256) {
+    const int sg = owner[c];
+    owner[c] = T.border[sg];
+    ordv[c] += T.off[sg];
+  }
+}
+
+// 1. follow every border once: MK_TB_WAVES waves per frame (the tiled bit
+// plane in L2), each lane walking one segment at a time (k_seg_plan; a whole
+// border when the frame is not split) and refilled from the frame's segment
+// list (an LDS counter) once a quarter of its wave is idle, so a frame costs
+// about its steps over its lanes instead of its longest border (the outer
+// border of the grid lines, ~5-9k steps). Points go to 16-point chunks handed
+// out by a per-frame counter; k_seg_chain orders them.
+#ifndef MK_TB_WAVES
+#define MK_TB_WAVES 4
+#endif
+__global__ __launch_bounds__(64 * MK_TB_WAVES) void k_trace_borders(const uint32_t* __restrict__ tbits, size_t tstride,
                                                       const Border* __restrict__ borders, FrameState* st,
-                                                      int32_t* __restrict__ counts, int32_t* __restrict__ scratch,
-                                                      int pool_cap, int Wp, int border_cap) {
+                                                      int32_t* __restrict__ scratch, int pool_cap, int Wp,
+                                                      int border_cap, const int32_t* __restrict__ rowb,
+                                                      size_t rstride, const uint16_t* __restrict__ rx, size_t plane) {
   const uint64_t t_start = wall_clock64();
   __shared__ uint8_t next_lut[512 * 8];
-  const int f = blockIdx.x, lane = threadIdx.x;
-  build_next_lut(next_lut, lane, 64);
+  __shared__ int32_t next_job;
+  const int f = blockIdx.x, lane = threadIdx.x & 63;
+  build_next_lut(next_lut, threadIdx.x, blockDim.x);
+  if (threadIdx.x == 0) next_job = 0;
   __syncthreads();
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
   const uint32_t* B = tbits + (size_t)f * tstride;
   const int wpw = dbits_wpw(Wp);
   const Border* bs = borders + (size_t)f * border_cap;
-  int32_t* cnt = counts + (size_t)f * border_cap;
   int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
   const int max_chunks = pool_cap / kChunk;
   int32_t* chunks = sc;                        // [0, 2 pool_cap)
   int32_t* owner = sc + 2 * (size_t)pool_cap;  // [2 pool_cap, + max_chunks)
   int32_t* ordv = owner + max_chunks;
+  int32_t* ccount = ordv + max_chunks;
+  const SegTab T = seg_tab(sc, pool_cap);
+  if (nb > T.cap) nb = T.cap;  // k_seg_plan flagged the frame
+  const int NC = st[f].seg_nc, M = st[f].seg_m, NS = NC + nb;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
   const BitsTiled nbh{(const uint64_t*)B, wpw};
   int32_t* smax = &st[f].trace_steps_max;
-  ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
+  ChunkEmit em{chunks, owner, ordv, ccount, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
   Walk w;
   int i = -1;
   bool act = false;
-  int next = 0;  // wave-uniform: the next border to hand out
+  bool exhausted = NS == 0;  // wave-uniform
   const uint64_t below = (1ull << lane) - 1;
+  const auto finish = [&](int nx) {
+    T.cnt[i] = w.n;
+    T.next[i] = nx;
+    em.flush();
+    if (em.ovf) atomicOr(&st[f].overflow, 2);
+    atomicMax(smax, w.steps);
+    atomicAdd(&st[f].trace_steps_sum, w.steps);
+  };
   for (;;) {
     const uint64_t idle = __ballot(!act);
     const int nidle = __popcll(idle);
-    if (next < nb && (nidle >= 16 || nidle == 64)) {
+    if (!exhausted && (nidle >= 16 || nidle == 64)) {
+      const int leader = __ffsll((unsigned long long)idle) - 1;
+      int next = 0;
+      if (lane == leader) next = atomicAdd(&next_job, nidle);
+      next = __shfl(next, leader);
+      if (next + nidle >= NS) exhausted = true;
       if (!act) {
-        const int bi = next + __popcll(idle & below);
-        if (bi < nb) {
-          i = bi;
-          const Border b = bs[i];
-          em.border = i; em.cur = -1; em.k = 0; em.nch = 0; em.ovf = false;
-          act = walk_start(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em, w);
-          if (!act) {
-            cnt[i] = w.n;
-            if (em.ovf) atomicOr(&st[f].overflow, 2);
+        const int j = next + __popcll(idle & below);
+        if (j < NS) {
+          const int sd = T.sdir[j];
+          if (sd != kSegUnused && sd != kSegAlias) {
+            i = j;
+            const Border b = bs[T.border[j]];
+            em.border = j; em.cur = -1; em.k = 0; em.nch = 0; em.ovf = false;
+            if (sd == kSegStart) {
+              act = walk_start(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em, w);
+              w.first = 0;
+              if (!act) finish(-1);
+            } else if (sd == kSegSingle) {
+              const uint32_t p = (uint32_t)T.pos[j];
+              em((int)(p & 0xffffu) - 1, (int)(p >> 16) - 1);
+              w.n = 1;
+              w.steps = 0;
+              finish(-1);
+            } else {
+              seg_begin(nbh, b, Wp, (uint32_t)T.pos[j], sd, w);
+              act = true;
+            }
           }
         }
       }
-      next += nidle;
       continue;
     }
-    if (nidle == 64) break;
-    if (act && !walk_step(nbh.b, 32 * wpw, next_lut, em, w)) {
+    if (nidle == 64) {
+      if (exhausted) break;
+      continue;
+    }
+    int nx = -1;
+    if (act && !walk_step(nbh.b, 32 * wpw, next_lut, em, w, M, r, X, T.rowbase, nx)) {
       act = false;
-      cnt[i] = w.n;
-      if (em.ovf) atomicOr(&st[f].overflow, 2);
-      atomicMax(smax, w.steps);
-      atomicAdd(&st[f].trace_steps_sum, w.steps);
+      finish(nx);
     }
   }
-  if (lane == 0) st[f].trace_ticks = (int32_t)(wall_clock64() - t_start);
+  if (lane == 0) atomicMax(&st[f].trace_ticks, (int32_t)(wall_clock64() - t_start));
 }
 
 // Latency variant of k_trace_borders for small batches: one 1024-thread block
@@ -1679,14 +1965,64 @@ struct BitsNBLds {
   }
   __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
+// one segment (k_seg_plan) on the LDS plane: the same walk as walk_step
+template <class NB, class EM>
+__device__ inline int walk_segment_lds(const NB& nb, const uint8_t* lut, EM& em, const Border& b, int Wp,
+                                       uint32_t pos, int sd, int M, const int32_t* r, const uint16_t* X,
+                                       const int32_t* rowbase, int& steps) {
+  Walk w;
+  if (sd == kSegStart) {
+    if (!walk_start(nb, b.start % Wp, b.start / Wp, b.hole != 0, em, w)) {
+      steps = 0;
+      return -1;
+    }
+    w.first = 0;
+  } else {
+    seg_begin(nb, b, Wp, pos, sd, w);
+  }
+  for (;;) {
+    const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
+    const uint32_t p9 = nb.row3(x, y - 1) | (nb.row3(x, y) << 3) | (nb.row3(x, y + 1) << 6);
+    const int s = lut[(p9 << 3) | w.s];
+    if (M > 0 && !w.first && y % M == 0) {
+      const bool west = arc_has(w.s, s, 4);
+      if (west || arc_has(w.s, s, 0)) {
+        steps = w.steps;
+        em.n_pts = w.n;
+        return seg_id_at(x, y, west ? 0 : 1, M, r, X, rowbase);
+      }
+    }
+    w.first = 0;
+    if (s != w.prev_s) {
+      em(x - 1, y - 1);
+      w.n++;
+      w.prev_s = s;
+    }
+    const uint32_t np = w.pos + wdelta(s);
+    if (np == w.spos && w.pos == w.p1) break;
+    w.pos = np;
+    w.s = (s + 4) & 7;
+    w.steps++;
+  }
+  steps = w.steps;
+  em.n_pts = w.n;
+  return -1;
+}
+// Latency path (small batches): one 1024-thread block per frame, the padded
+// bit plane in LDS (ds_read per step instead of an L2 round trip), threads
+// taking the frame's segments from an LDS counter (a frame's longest border,
+// ~5-9k steps, was the rig latency's walk; split it is a few hundred).
 __global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __restrict__ dbits, size_t dstride,
                                                             const Border* __restrict__ borders, FrameState* st,
-                                                            int32_t* __restrict__ counts,
                                                             int32_t* __restrict__ scratch, int pool_cap, int Wp,
-                                                            int Hp, int border_cap) {
+                                                            int Hp, int border_cap, const int32_t* __restrict__ rowb,
+                                                            size_t rstride, const uint16_t* __restrict__ rx,
+                                                            size_t plane) {
   __shared__ uint8_t next_lut[512 * 8];
+  __shared__ int32_t next_job;
   const int f = blockIdx.x;
   build_next_lut(next_lut, threadIdx.x, blockDim.x);
+  if (threadIdx.x == 0) next_job = 0;
   const int wpw = dbits_wpw(Wp);
   const uint32_t* B = dbits + (size_t)f * dstride;
   for (int k = threadIdx.x; k < wpw * Hp; k += blockDim.x) tb_lds[k] = B[k];
@@ -1694,18 +2030,38 @@ __global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __re
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
   const Border* bs = borders + (size_t)f * border_cap;
-  int32_t* cnt = counts + (size_t)f * border_cap;
   int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
   const int max_chunks = pool_cap / kChunk;
   int32_t* chunks = sc;
   int32_t* owner = sc + 2 * (size_t)pool_cap;
   int32_t* ordv = owner + max_chunks;
+  const SegTab T = seg_tab(sc, pool_cap);
+  if (nb > T.cap) nb = T.cap;  // k_seg_plan flagged the frame
+  const int NC = st[f].seg_nc, M = st[f].seg_m, NS = NC + nb;
+  const int32_t* r = rowb + (size_t)f * rstride;
+  const uint16_t* X = rx + (size_t)f * plane;
   const BitsNBLds nbh{wpw};
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-    const Border b = bs[i];
-    ChunkEmit em{chunks, owner, ordv, &st[f].n_chunks, max_chunks, i, -1, 0, 0, false};
-    cnt[i] = trace_border_lut(nbh, next_lut, b.start % Wp, b.start / Wp, b.hole != 0, em, &st[f].trace_steps_max);
+  for (;;) {
+    int j = 0;
+    j = atomicAdd(&next_job, 1);
+    if (j >= NS) break;
+    const int sd = T.sdir[j];
+    if (sd == kSegUnused || sd == kSegAlias) continue;
+    const Border b = bs[T.border[j]];
+    ChunkEmit em{chunks, owner, ordv, ordv + max_chunks, &st[f].n_chunks, max_chunks, j, -1, 0, 0, false};
+    int steps = 0, nx = -1;
+    if (sd == kSegSingle) {
+      const uint32_t p = (uint32_t)T.pos[j];
+      em((int)(p & 0xffffu) - 1, (int)(p >> 16) - 1);
+      em.n_pts = 1;
+    } else {
+      nx = walk_segment_lds(nbh, next_lut, em, b, Wp, (uint32_t)T.pos[j], sd, M, r, X, T.rowbase, steps);
+    }
+    T.cnt[j] = em.n_pts;
+    T.next[j] = nx;
+    em.flush();
     if (em.ovf) atomicOr(&st[f].overflow, 2);
+    atomicMax(&st[f].trace_steps_max, steps);
   }
 }
 
@@ -1794,13 +2150,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     return;
   }
   MK_TICK(2);
-  // 3. compact: one wave per chunk, one lane per point
+  // 3. compact: 64 / kChunk chunks per wave, one lane per point
   {
+    constexpr int CPW = 64 / kChunk;
     const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
-    for (int c = wave; c < nchunk; c += nwaves) {
-      const int b = owner[c], k = ordv[c] * kChunk + lane;
-      if (k < cnt[b]) {
-        const int32_t* sp = chunks + 2 * ((size_t)c * kChunk + lane);
+    const int32_t* ccount = ordv + max_chunks;
+    const int l = lane % kChunk;
+    for (int c0 = wave * CPW; c0 < nchunk; c0 += nwaves * CPW) {
+      const int c = c0 + lane / kChunk;
+      if (c < nchunk && l < ccount[c]) {
+        const int b = owner[c], k = ordv[c] + l;
+        const int32_t* sp = chunks + 2 * ((size_t)c * kChunk + l);
         int32_t* dp = pl + 2 * ((size_t)off[b] + k);
         dp[0] = sp[0];
         dp[1] = sp[1];

@@ -105,6 +105,8 @@ struct FrameState {
   int32_t n_chunks;         // 64-point chunks handed out by k_trace_borders
   int32_t trace_steps_sum;  // all border walks' steps of the frame
   int32_t trace_ticks;      // k_trace_borders wall-clock time of the frame (10 ns ticks)
+  int32_t seg_nc;           // border-walk checkpoint segments of the frame (k_seg_plan; 0: unsplit)
+  int32_t seg_m;            // checkpoint row spacing in use (0: borders walked whole)
 };
 
 // Gauss–Newton rig refinement (gn_impl.hip): one camera's inv(T_base_cam)

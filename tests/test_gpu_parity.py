@@ -109,6 +109,66 @@ def test_contour_borders_match_find_contours(mantis, frames):
         assert cnt[8] == 0, f"overflow flags {cnt[8]}"
         assert cnt[0] == len(cs), f"borders {cnt[0]} vs findContours {len(cs)}"
         assert cnt[1] == sum(len(c) for c in cs), f"points {cnt[1]} vs {sum(len(c) for c in cs)}"
+        _contours_equal(mantis, img)
+
+
+def _contours_equal(mt, img):
+    """Every border's point sequence from the library equals one of
+    findContours' (CCOMP, SIMPLE) exactly, start point and order included,
+    as a multiset over the frame."""
+    import collections
+
+    got = collections.Counter((h, tuple(map(tuple, p))) for p, h in mt.contours(0))
+    cs, holes = O.find_contours(O.detector_binary(O.canny(img)), 2)
+    want = collections.Counter((h, tuple(map(tuple, np.asarray(c).reshape(-1, 2)))) for c, h in zip(cs, holes))
+    assert got == want, f"{sum((got - want).values())} borders differ of {len(cs)}"
+
+
+@pytest.mark.parametrize("seg_m", ["0", "32", "8"])
+def test_segmented_border_walks_point_sequences(frames, seg_m):
+    """Border walks split at checkpoints (k_seg_plan: the visits of foreground
+    run ends in rows y = M k; MANTIS_SEG_M, 0 = whole borders) on the
+    large-batch walker: each border's chain points equal findContours' point
+    for point, on real frames and on blob-noise images with many nested
+    components, holes and one-pixel runs (a 16-point chunk per segment's
+    tail stays within the point pool)."""
+    import os
+
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    rng = np.random.default_rng(77)
+    imgs = [fr[0] for fr in frames[:2]]
+    for (w, h, cell) in [(1280, 720, 6), (640, 480, 1), (333, 97, 2)]:
+        base = (rng.random((h // cell + 2, w // cell + 2)) > 0.5).astype(np.float64) * 200 + 20
+        img = np.repeat(np.repeat(base, cell, 0), cell, 1)[:h, :w]
+        imgs.append(np.repeat(img[:, :, None], 3, 2).astype(np.uint8))
+    saved = {k: os.environ.get(k) for k in ("MANTIS_TRACE_LDS_FRAMES", "MANTIS_SEG_M")}
+    os.environ["MANTIS_TRACE_LDS_FRAMES"] = "0"
+    os.environ["MANTIS_SEG_M"] = seg_m
+    try:
+        mt = M.Mantis(max_cams=1, max_width=1280, max_height=720)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        for img in imgs:
+            try:
+                mt.detect_quads(M.make_image(img, K, D))
+            except M.MantisError:
+                pass  # the dense one-pixel noise can exceed the point pool; checked below
+            cnt = mt.frame_counters(0)
+            if cnt[8]:
+                assert img.shape[:2] == (480, 640), f"overflow flags {cnt[8]}"
+                continue
+            if seg_m != "0" and img.shape[:2] == (720, 1280):
+                assert cnt[22] > 0 and cnt[23] == int(seg_m), "frame walked unsplit"
+            _contours_equal(mt, img)
+    finally:
+        mt.close()
 
 
 def test_throughput_border_walks_match_find_contours(landmark_map):
