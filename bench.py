@@ -89,7 +89,7 @@ def parse():
                         "default 512)")
     p.add_argument("--frames", type=int, default=16, help="config 5: frames per step (16,200 hypotheses each)")
     p.add_argument("--distinct", type=int, default=128, help="distinct rendered rigs (cycled through the batch)")
-    p.add_argument("--contexts", type=int, default=4,
+    p.add_argument("--contexts", type=int, default=6,
                    help="config 3: library contexts per GPU, each driven by its own host thread (one ctx per "
                         "thread, include/mantis.h); the step's rigs are split evenly between them")
     p.add_argument("--contexts4", type=int, default=0,
@@ -361,13 +361,14 @@ def run_config3(a, rk, cpu):
                 if record and k == 0:
                     for name, ms in m.kernel_times():
                         stage_ms[name] = stage_ms.get(name, 0.0) + ms
-        for f in [pool.submit(worker, k) for k in range(nctx)]:
+        for f in [pool.submit(worker, k) for k in range(len(bs))]:
             f.result()
 
     def barrier_sync():
         rk.barrier()
         for mc in ctxs:
-            mc.synchronize()
+            if mc.h is not None:  # the host-ingest leg closes contexts past 4
+                mc.synchronize()
 
     run_steps(batches, a.warmup)
 
@@ -460,8 +461,8 @@ def run_config3(a, rk, cpu):
     prof_src = os.path.join("profiles", "r03_batch_launch_avg_default.json")
 
     def profiled(r, stage):
-        if r is None or stage not in stage_kernels or a.rigs != 4096 or nctx != 4:
-            return  # the committed profile is of the default command
+        if r is None or stage not in stage_kernels or a.rigs != 6144 or nctx != 6:
+            return  # the committed profile is of the default command (6 contexts x 1024 rigs)
         try:
             pj = json.load(open(os.path.join(ROOT, prof_src)))
         except (OSError, ValueError):
@@ -527,17 +528,24 @@ def run_config3(a, rk, cpu):
     for j in range(nd):
         m.d2h(host[j], dev + j * fb)
     himgs = [M.make_image(host[i % nd], K, D, T_base_cam=Tbc[i % nd]) for i in range(n_frames)]
+    # host frames need each context's staging buffer (max_cams x 3 W H, allocated
+    # on first use): beside the device planes of more than 4 contexts it would not
+    # fit in HBM, so the ingest leg runs on 4 of them (the others are closed)
+    nin = min(nctx, 4)
+    for k in range(nin, nctx):
+        ctxs[k].close()
     p50_host = p50_of(himgs[:CAMS])
     if a.ingest_steps > 0:
-        hb = [M.Batch(ctxs[k], himgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS], rigs_ctx) for k in range(nctx)]
+        hb = [M.Batch(ctxs[k], himgs[k * rigs_ctx * CAMS:(k + 1) * rigs_ctx * CAMS], rigs_ctx) for k in range(nin)]
         run_steps(hb, 1)  # one untimed pass over the host path
         barrier_sync()
         t0 = time.perf_counter()
         run_steps(hb, a.ingest_steps)
         barrier_sync()
         el = rk.max(time.perf_counter() - t0)
-        h2d_bytes = n_frames * fb * a.ingest_steps
-        ingest = {"value": round(a.rigs * a.ingest_steps * rk.world / el, 3), "unit": "rig poses/s",
+        h2d_bytes = nin * rigs_ctx * CAMS * fb * a.ingest_steps
+        ingest = {"value": round(nin * rigs_ctx * a.ingest_steps * rk.world / el, 3), "unit": "rig poses/s",
+                  "contexts": nin,
                   "ms_per_step": round(el / a.ingest_steps * 1e3, 3), "steps": a.ingest_steps,
                   "h2d_GBps_per_gpu": round(h2d_bytes / el / 1e9, 2),
                   "p50_latency_ms": round(p50_host, 3),

@@ -315,6 +315,9 @@ ScreenCam screen_cam_cached(Ctx* c, const Cam& cm) {
   return sc;
 }
 
+template <class T>
+mantis_status dalloc(Ctx* c, T** p, size_t count);
+
 // Stage the frames into the batch: device-resident contiguous inputs are
 // used in place; everything else is copied (pitch-converted) into d_bgr.
 mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int& H) {
@@ -335,6 +338,15 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
     if (im.mem_kind == 1 && im.step_bytes == 3 * W) {
       fd.bgr = im.bgr;
     } else {
+      if (!c->d_bgr) {
+        // the staging buffer only exists once a host (or pitched) frame arrives:
+        // device-resident callers keep its max_cams x 3 W H bytes of HBM
+        if (dalloc(c, &c->d_bgr, (size_t)c->F * c->Wmax * c->Hmax * 3) != MANTIS_OK) {
+          c->d_bgr = nullptr;
+          c->err = "hipMalloc of the frame staging buffer failed";
+          return MANTIS_ERR_OOM;
+        }
+      }
       uint8_t* dst = c->d_bgr + (size_t)i * fb;
       HIP_OK(hipMemcpy2DAsync(dst, 3 * W, im.bgr, im.step_bytes, 3 * W, H,
                               im.mem_kind == 1 ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->s));
@@ -843,7 +855,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   const int per = cfg.particles * cfg.iterations * 6;
   mantis_status st = MANTIS_OK;
   auto chk = [&](mantis_status s) { if (st == MANTIS_OK) st = s; };
-  chk(dalloc(c, &c->d_bgr, (size_t)F * c->Wmax * c->Hmax * 3));
   c->fstride = (c->plane + 3) & ~(size_t)3;  // the hysteresis flags take dword atomics at (root & ~3)
   chk(dalloc(c, &c->d_strong, (size_t)F * c->fstride));
   c->lstride = (c->plane + 1) & ~(size_t)1;  // even: the hysteresis views it as u32 run extents
