@@ -477,7 +477,7 @@ def run_config3(a, rk, cpu):
         ach = amount / (ms * 1e-3) / (1e9 if r["unit"] == "GB/s" else 1e12)
         r["profiled"] = {"source": prof_src, "kernel_sum_ms": round(ms, 4), "achieved": round(ach, 4),
                          "frac": round(ach / r["peak"], 5),
-                         "note": "sum of the stage kernels' rocprofv3 durations (batch launches, 4 contexts)"}
+                         "note": "sum of the stage kernels' rocprofv3 durations (batch launches of the default command)"}
 
     profiled(roof, dom)
     profiled(roof_front, "canny_nms")

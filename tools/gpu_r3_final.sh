@@ -1,0 +1,31 @@
+#!/bin/bash
+# GPU box, round-3 evidence. PART=a: GPU tests, smoke, default bench line (with
+# the CPU baseline); PART=b: rocprofv3 kernel trace + stats of the default
+# command, batch-launch averages (bench.py's profiled roofline reads them),
+# PMC traffic of the front end, and the config 2 / 5 / 4 legs.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=gpurun_out/r03_final; mkdir -p $O
+export TMPDIR=/tmp
+if [ "$PART" = "a" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1; tail -2 $O/gpu_tests.txt
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && tail -1 $O/smoke.txt || { echo smoke failed; tail -5 $O/smoke.txt; exit 1; }
+  timeout -k 10 700 python -u bench.py > $O/bench_default.log 2>&1 || { echo bench failed; tail -5 $O/bench_default.log; exit 1; }
+  grep '^{' $O/bench_default.log | tail -1 > $O/bench_default.json; cut -c1-200 $O/bench_default.json
+fi
+if [ "$PART" = "b" ]; then
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$R/$O/prof_default" -o run -- python3 "$R/bench.py" --no-cpu --steps 3 --warmup 1 --latency-iters 3 --ingest-steps 0 > "$R/$O/prof_default.log" 2>&1) || { echo prof failed; tail -5 $O/prof_default.log; exit 1; }
+  python3 tools/prof_summary.py $O/prof_default $O/rocprof_stats_default.md > /dev/null
+  python3 tools/kern_avg.py $O/prof_default/run_kernel_trace.csv 40 $O/batch_launch_avg_default.json > $O/batch_launch_avg_default.txt
+  python3 tools/trace_overlap.py $O/prof_default 18 > $O/trace_overlap_default.txt || true
+  head -12 $O/batch_launch_avg_default.txt
+  bash tools/pmc_traffic.sh > $O/pmc_traffic.txt 2>&1 && cp gpurun_out/pmc_traffic.json $O/pmc_traffic.json || { echo pmc failed; tail -5 $O/pmc_traffic.txt; exit 1; }
+  for leg in 2 5 4; do
+    case $leg in
+      2) args="--config 2" ;;
+      4) args="--config 4 --steps 5 --warmup 1 --latency-iters 3" ;;
+      5) args="--config 5 --steps 20 --warmup 3" ;;
+    esac
+    timeout -k 10 400 python -u bench.py $args > $O/bench_c$leg.log 2>&1 || { echo "bench $leg failed"; tail -5 $O/bench_c$leg.log; exit 1; }
+    grep '^{' $O/bench_c$leg.log | tail -1 > $O/bench_c$leg.json; cut -c1-160 $O/bench_c$leg.json
+  done
+fi
