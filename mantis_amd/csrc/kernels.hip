@@ -579,6 +579,235 @@ __global__ __launch_bounds__(256) void k_canny(const FrameDesc* __restrict__ fra
   }
 }
 
+// ------------------------------------------------ Canny as column strips
+// The same stages (gray, [84,89,84] blur with BORDER_REFLECT_101, Sobel with
+// BORDER_REPLICATE, L1 magnitude, NMS, weak / strong classes) without LDS or
+// barriers: a wave owns a strip of 64 x 4 columns and walks down the frame,
+// each lane keeping its 4 columns' last rows of every stage in registers
+// (the vertical taps) and taking the columns left and right of its own from
+// the neighbouring lanes by DPP (the horizontal taps). Lanes 0..55 produce
+// the strip's 224 columns (7 bit-plane words), lane 56 and lane 63 (the
+// column group left of the strip, reached by the wave rotation) are the
+// halo, lanes 57..62 idle. The stage outputs lag the input row: hblur(i),
+// blur(i-1), Sobel(i-2), NMS(i-3). At the frame's edges the neighbour values
+// are the border rules' (reflected gray, replicated blur, zero magnitude) in
+// the first / last column groups and rows. Every value is the same integer
+// as k_canny's (interior tiles), so the planes are identical.
+__device__ inline uint32_t dpp_from_left(uint32_t v) {  // lane l gets lane l-1's v (lane 0: lane 63's)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xf, 0xf, false);
+}
+__device__ inline uint32_t dpp_from_right(uint32_t v) {  // lane l gets lane l+1's v (lane 63: lane 0's)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x134, 0xf, 0xf, false);
+}
+__device__ inline uint32_t dpp_row_shr(uint32_t v, int n) {  // lane l gets lane l-n of its 16-lane row, 0 past the row's start
+  switch (n) {
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, true);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, true);
+    default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, true);
+  }
+}
+constexpr int kStripCols = 224;  // output columns per strip (7 words)
+// Per-wave state of a strip: three row slots per stage (row r in slot r % 3),
+// so the walk unrolled by three indexes registers with constants and moves
+// nothing between rows.
+struct StripRegs {
+  uint32_t hba[3], hbb[3];  // horizontal blur, 2 u16 pairs
+  uint32_t bl[3];           // blur, 4 bytes
+  uint32_t mga[3], mgb[3];  // L1 magnitude, 2 i16 pairs
+  uint32_t gxa[3], gxb[3], gya[3], gyb[3];  // Sobel gx / gy
+};
+struct StripWave {
+  const uint8_t* rowp;
+  uint32_t rstep;
+  int H, WW, lane;
+  bool left_edge, right_edge, inside, store_lane;
+  s16x2 LOW, HIGH;
+  uint32_t* cb;
+  uint32_t* sbp;
+  uint32_t n0, n1, n2;  // input row i (prefetched)
+};
+// Iteration i of the walk (S = i % 3): hblur(i), blur(i-1), Sobel(i-2), NMS(i-3).
+template <int S>
+__device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
+  constexpr int S1 = (S + 1) % 3, S2 = (S + 2) % 3;  // slots of rows i-2 / i+1, i-1
+  constexpr int SHIFT = 15;
+  constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
+  const u16x2 c84 = {84, 84}, c89 = {89, 89}, two = {2, 2};
+  const int H = w.H;
+  // ---- gray and horizontal blur of input row i
+  if (i < H) {
+    const uint32_t d0 = w.n0, d1 = w.n1, d2 = w.n2;
+    gu32* qn = gwords(w.rowp + (uint32_t)(i + 1 < H ? i + 1 : i) * w.rstep);  // next row (the last row again at the end)
+    w.n0 = qn[0];
+    w.n1 = qn[1];
+    w.n2 = qn[2];
+    const uint32_t g = gray4(d0, d1, d2);
+    uint32_t gl = dpp_from_left(g), gr = dpp_from_right(g);
+    if (w.left_edge) gl = g << 16;   // gray(-1) = gray(1)
+    if (w.right_edge) gr = g >> 16;  // gray(W) = gray(W-2)
+    const Taps4 tp = taps4(gl, g, gr);
+    const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
+    const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
+    R.hba[S] = upk(o01);
+    R.hbb[S] = upk(o23);
+  } else if (i == H) {  // row H = row H-2 (reflect), for the blur of row H-1
+    R.hba[S] = R.hba[S1];
+    R.hbb[S] = R.hbb[S1];
+  }
+  // ---- vertical blur of row j = i - 1 (hblur rows j-1, j, j+1 = slots S1, S2, S)
+  const int j = i - 1;
+  if (j >= 0 && j < H) {
+    const uint32_t aa = j == 0 ? R.hba[S] : R.hba[S1], ab = j == 0 ? R.hbb[S] : R.hbb[S1];  // row -1 = row 1
+    const uint32_t av[4] = {aa & 0xffffu, aa >> 16, ab & 0xffffu, ab >> 16};
+    const uint32_t bv[4] = {R.hba[S2] & 0xffffu, R.hba[S2] >> 16, R.hbb[S2] & 0xffffu, R.hbb[S2] >> 16};
+    const uint32_t cv[4] = {R.hba[S] & 0xffffu, R.hba[S] >> 16, R.hbb[S] & 0xffffu, R.hbb[S] >> 16};
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t r = (84u * (av[k] + cv[k]) + 89u * bv[k] + (1u << 15)) >> 16;
+      o |= (r > 255u ? 255u : r) << (8 * k);
+    }
+    R.bl[S2] = o;
+  } else if (j == H) {
+    R.bl[S2] = R.bl[S1];  // row H = row H-1 (replicate), for the Sobel of row H-1
+  }
+  // ---- Sobel of row k = i - 2 (blur rows k-1, k, k+1 = slots S, S1, S2)
+  const int k = i - 2;
+  if (k >= 0 && k < H) {
+    const uint32_t a = k == 0 ? R.bl[S1] : R.bl[S];  // row -1 = row 0
+    const uint32_t b = R.bl[S1], c = R.bl[S2];
+    const u16x2 A01 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c010c00u)), A23 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c030c02u));
+    const u16x2 B01 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c010c00u)), B23 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c030c02u));
+    const u16x2 C01 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c010c00u)), C23 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c030c02u));
+    const uint32_t vs01 = upk(A01 + C01 + B01 * two), vs23 = upk(A23 + C23 + B23 * two);
+    const uint32_t vd01 = upk(vpk<s16x2>(upk(C01)) - vpk<s16x2>(upk(A01)));
+    const uint32_t vd23 = upk(vpk<s16x2>(upk(C23)) - vpk<s16x2>(upk(A23)));
+    uint32_t VL = dpp_from_left(vs23), VR = dpp_from_right(vs01);
+    uint32_t DL = dpp_from_left(vd23), DR = dpp_from_right(vd01);
+    if (w.left_edge) { VL = vs01 << 16; DL = vd01 << 16; }    // blur(-1) = blur(0)
+    if (w.right_edge) { VR = vs23 >> 16; DR = vd23 >> 16; }   // blur(W) = blur(W-1)
+    const s16x2 S0v = vpk<s16x2>(__builtin_amdgcn_perm(vs01, VL, 0x05040302u));  // columns -1, 0
+    const s16x2 S1v = vpk<s16x2>(__builtin_amdgcn_perm(vs23, vs01, 0x05040302u)); // 1, 2
+    const s16x2 S2v = vpk<s16x2>(__builtin_amdgcn_perm(VR, vs23, 0x05040302u));   // 3, 4
+    const s16x2 D0 = vpk<s16x2>(__builtin_amdgcn_perm(vd01, DL, 0x05040302u));
+    const s16x2 D1 = vpk<s16x2>(__builtin_amdgcn_perm(vd23, vd01, 0x05040302u));
+    const s16x2 D2 = vpk<s16x2>(__builtin_amdgcn_perm(DR, vd23, 0x05040302u));
+    const s16x2 gx01 = S1v - S0v, gx23 = S2v - S1v;
+    const s16x2 gy01 = D0 + D1 + (vpk<s16x2>(vd01) << 1), gy23 = D1 + D2 + (vpk<s16x2>(vd23) << 1);
+    const s16x2 m01 = __builtin_elementwise_max(gx01, -gx01) + __builtin_elementwise_max(gy01, -gy01);
+    const s16x2 m23 = __builtin_elementwise_max(gx23, -gx23) + __builtin_elementwise_max(gy23, -gy23);
+    R.mga[S1] = upk(m01);
+    R.mgb[S1] = upk(m23);
+    R.gxa[S1] = upk(gx01);
+    R.gxb[S1] = upk(gx23);
+    R.gya[S1] = upk(gy01);
+    R.gyb[S1] = upk(gy23);
+  } else if (k == H) {
+    R.mga[S1] = 0;  // magnitude below the frame: zero
+    R.mgb[S1] = 0;
+  }
+  // ---- NMS of row n = i - 3 (magnitude rows n-1, n, n+1 = slots S2, S, S1)
+  const int n = i - 3;
+  if (n < 0) return;
+  const uint32_t ua = n == 0 ? 0u : R.mga[S2], ub = n == 0 ? 0u : R.mgb[S2];  // magnitude above the frame: zero
+  uint32_t P[3][3], Cw[3][2];
+  const uint32_t rwa[3] = {ua, R.mga[S], R.mga[S1]}, rwb[3] = {ub, R.mgb[S], R.mgb[S1]};
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    uint32_t Lw = dpp_from_left(rwb[r]), Rw = dpp_from_right(rwa[r]);
+    if (w.left_edge) Lw = 0u;
+    if (w.right_edge) Rw = 0u;
+    Cw[r][0] = rwa[r];
+    Cw[r][1] = rwb[r];
+    P[r][0] = __builtin_amdgcn_perm(rwa[r], Lw, 0x05040302u);
+    P[r][1] = __builtin_amdgcn_perm(rwb[r], rwa[r], 0x05040302u);
+    P[r][2] = __builtin_amdgcn_perm(Rw, rwb[r], 0x05040302u);
+  }
+  uint32_t push[2], strong[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const uint32_t gxp = h ? R.gxb[S] : R.gxa[S], gyp = h ? R.gyb[S] : R.gya[S];
+    const s16x2 X = vpk<s16x2>(gxp), Y = vpk<s16x2>(gyp);
+    const s16x2 AX = __builtin_elementwise_max(X, -X), AY = __builtin_elementwise_max(Y, -Y);
+    const uint32_t ax = upk(AX), ay = upk(AY);
+    const int ax0 = (int)(ax & 0xffffu), ax1 = (int)(ax >> 16);
+    const int ay0 = (int)(ay & 0xffffu) << SHIFT, ay1 = (int)(ay >> 16) << SHIFT;
+    const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
+    const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
+    const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);
+    const uint32_t UL = P[0][h], U = Cw[0][h], UR = P[0][h + 1];
+    const uint32_t L = P[1][h], Mm = Cw[1][h], Rr = P[1][h + 1];
+    const uint32_t DLw = P[2][h], Dd = Cw[2][h], DRw = P[2][h + 1];
+    const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
+    const uint32_t B = (HOR & Rr) | (~HOR & ((VER & Dd) | (~VER & ((NEG & DLw) | (~NEG & DRw)))));
+    const s16x2 Ms = vpk<s16x2>(Mm);
+    const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
+    const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
+    const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
+    const uint32_t HV = HOR | VER;
+    const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
+    const uint32_t GTL = upk((w.LOW - Ms) >> 15);
+    push[h] = GTA & BC & GTL;
+    strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
+  }
+  // nibbles (pixel 2h + t <-> bit t of half h) into 32-bit words of 8 lanes
+  const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
+  const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
+  uint32_t cw = w.inside ? ((xp | (xp >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
+  uint32_t sw = w.inside ? ((xs | (xs >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
+  cw |= dpp_row_shr(cw, 1);
+  sw |= dpp_row_shr(sw, 1);
+  cw |= dpp_row_shr(cw, 2);
+  sw |= dpp_row_shr(sw, 2);
+  cw |= dpp_row_shr(cw, 4);
+  sw |= dpp_row_shr(sw, 4);
+  if (w.store_lane) {
+    w.cb[(size_t)n * w.WW + (w.lane >> 3)] = cw;
+    w.sbp[(size_t)n * w.WW + (w.lane >> 3)] = sw;
+  }
+}
+__global__ __launch_bounds__(256) void k_canny_strip(const FrameDesc* __restrict__ frames, int low, int high,
+                                                     uint32_t* __restrict__ cbits, uint32_t* __restrict__ sbits,
+                                                     size_t bstride, int nstrip, int nwaves) {
+  // the wave index is wave-uniform: frame fields and row conditions stay scalar
+  const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (wv >= nwaves) return;
+  StripWave w;
+  w.lane = threadIdx.x & 63;
+  const int f = wv / nstrip, sidx = wv - f * nstrip;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w;
+  w.H = fd.h;
+  w.WW = bits::words(W);
+  const int base = sidx * kStripCols;
+  const int c0 = w.lane == 63 ? base - 4 : base + 4 * w.lane;      // this lane's first column
+  const int lc = c0 < 0 ? 0 : (c0 > W - 4 ? W - 4 : c0);            // loads stay inside the row
+  w.left_edge = c0 == 0;                                            // columns -1.. come from the border rules
+  w.right_edge = c0 == W - 4;
+  w.inside = c0 >= 0 && c0 <= W - 4;
+  const int lowc = low < -1 ? -1 : (low > 32767 ? 32767 : low);
+  const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
+  w.LOW = s16x2{(short)lowc, (short)lowc};
+  w.HIGH = s16x2{(short)highc, (short)highc};
+  w.rowp = fd.bgr + (uint32_t)lc * 3u;
+  w.rstep = (uint32_t)W * 3u;
+  w.cb = cbits + (size_t)f * bstride + (size_t)(base >> 5);
+  w.sbp = sbits + (size_t)f * bstride + (size_t)(base >> 5);
+  w.store_lane = (w.lane & 7) == 7 && w.lane < 56 && base + 4 * (w.lane & ~7) < W;
+  StripRegs R = {};
+  gu32* q = gwords(w.rowp);
+  w.n0 = q[0];
+  w.n1 = q[1];
+  w.n2 = q[2];
+  const int rows = w.H + 3;
+#pragma unroll 1
+  for (int i = 0; i < rows; i += 3) {
+    strip_step<0>(w, R, i);
+    if (i + 1 < rows) strip_step<1>(w, R, i + 1);
+    if (i + 2 < rows) strip_step<2>(w, R, i + 2);
+  }
+}
+
 // ------------------------------------------------ hysteresis: run CCL
 // Runs = maximal spans of candidates in a row, numbered in raster order per
 // frame (k_run_scan gives the row bases); 8-connected unions between

@@ -1,0 +1,75 @@
+// GPU check of k_canny_strip against k_canny (measurement tool): both on
+// the same frames (blob noise, gradients, random bytes; several sizes with
+// W % 4 == 0), candidate and strong bit planes compared word for word; the
+// first mismatching pixels are printed with both bits.
+// Build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize tools/check_canny_strip.hip -o tools/check_canny_strip
+#include "../mantis_amd/csrc/kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+using namespace mk;
+
+int main() {
+  const int sizes[][2] = {{1280, 720}, {640, 480}, {1000, 611}, {232, 40}, {8, 3}, {448, 17}};
+  int fails = 0;
+  std::mt19937 rng(5);
+  for (auto& sz : sizes) {
+    const int W = sz[0], H = sz[1];
+    for (int kind = 0; kind < 3; kind++) {
+      std::vector<uint8_t> img((size_t)W * H * 3);
+      for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+          for (int c = 0; c < 3; c++) {
+            uint8_t v;
+            if (kind == 0) v = (((x / 7) + (y / 5)) & 1) ? 210 : 25;
+            else if (kind == 1) v = (uint8_t)((x * 3 + y * 5 + c * 40) & 255);
+            else v = (uint8_t)(rng() & 255);
+            img[((size_t)y * W + x) * 3 + c] = v;
+          }
+      uint8_t* dimg;
+      hipMalloc(&dimg, img.size());
+      hipMemcpy(dimg, img.data(), img.size(), hipMemcpyHostToDevice);
+      FrameDesc fd{};
+      fd.bgr = dimg;
+      fd.w = W;
+      fd.h = H;
+      FrameDesc* dfd;
+      hipMalloc(&dfd, sizeof(FrameDesc));
+      hipMemcpy(dfd, &fd, sizeof(fd), hipMemcpyHostToDevice);
+      const int WW = bits::words(W);
+      const size_t B = (size_t)WW * H;
+      uint32_t *c1, *s1, *c2, *s2;
+      hipMalloc(&c1, B * 4); hipMalloc(&s1, B * 4); hipMalloc(&c2, B * 4); hipMalloc(&s2, B * 4);
+      hipMemset(c1, 0, B * 4); hipMemset(s1, 0, B * 4); hipMemset(c2, 0xff, B * 4); hipMemset(s2, 0xff, B * 4);
+      const int low = 30, high = 90;
+      const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
+      k_canny<<<tgx * tgy, 256>>>(dfd, low, high, 1, c1, s1, B, tgx, tgy);
+      const int ns = (W + kStripCols - 1) / kStripCols;
+      k_canny_strip<<<(ns + 3) / 4, 256>>>(dfd, low, high, c2, s2, B, ns, ns);
+      std::vector<uint32_t> h1(B), h2(B), g1(B), g2(B);
+      hipMemcpy(h1.data(), c1, B * 4, hipMemcpyDeviceToHost);
+      hipMemcpy(h2.data(), c2, B * 4, hipMemcpyDeviceToHost);
+      hipMemcpy(g1.data(), s1, B * 4, hipMemcpyDeviceToHost);
+      hipMemcpy(g2.data(), s2, B * 4, hipMemcpyDeviceToHost);
+      int bad = 0;
+      for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+          const size_t w = (size_t)y * WW + (x >> 5);
+          const int b = x & 31;
+          const int a1 = (h1[w] >> b) & 1, a2 = (h2[w] >> b) & 1, t1 = (g1[w] >> b) & 1, t2 = (g2[w] >> b) & 1;
+          if (a1 != a2 || t1 != t2) {
+            if (bad < 8) printf("  %dx%d kind %d: (%d, %d) cand %d/%d strong %d/%d\n", W, H, kind, x, y, a1, a2, t1, t2);
+            bad++;
+          }
+        }
+      printf("%dx%d kind %d: %d pixel mismatches\n", W, H, kind, bad);
+      fails += bad != 0;
+      hipFree(dimg); hipFree(dfd); hipFree(c1); hipFree(s1); hipFree(c2); hipFree(s2);
+    }
+  }
+  printf("check_canny_strip: %s\n", fails ? "FAIL" : "ok");
+  return fails ? 1 : 0;
+}
