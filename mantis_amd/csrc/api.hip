@@ -162,8 +162,8 @@ struct Ctx {
   int32_t* d_octl = nullptr;  // [2][2]: entries, next
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
-  int seg_m = 64;
-  int canny_strip = 1;  // k_canny_strip where the frames allow it (MANTIS_CANNY_STRIP=0: tiles)  // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
+  int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
+  int canny_strip = 1;  // k_canny_strip where the frames allow it (MANTIS_CANNY_STRIP=0: tiles)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -377,13 +377,13 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   }
   mark(c, "canny_nms");
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
-  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2};
-  dim3 gr4((H + 3) / 4, n);
-  k_hyst_count<<<gr4, 256, 0, c->s>>>(c->d_b1, B, hr, W, H);
-  k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, H);
-  k_hyst_runs<<<gr4, 256, 0, c->s>>>(c->d_b1, B, hr, W, H);
-  k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 2 * sizeof(uint32_t) * HB_ROWS * bits::words(W), c->s>>>(
-      c->d_b2, B, hr, c->d_eb, W, H);
+  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
+              HB_ROWS * ((W + 1) / 2)};
+  // list counters |A|, |B| of every frame (rowb[H + 1], rowb[H + 2])
+  HIP_OK(hipMemset2DAsync(c->d_rowb + H + 1, c->rstride * sizeof(int32_t), 0, 2 * sizeof(int32_t), n, c->s));
+  const int WWb = bits::words(W);
+  k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 3 * sizeof(uint32_t) * HB_ROWS * WWb, c->s>>>(
+      c->d_b1, c->d_b2, B, hr, c->d_eb, W, H);
   const int nseam = (H - 1) / HB_ROWS;
   if (nseam > 0) k_hyst_seam<<<dim3((nseam + 3) / 4, n), 256, 0, c->s>>>(hr, H);
   k_hyst_mark<<<dim3(8, n), 256, 0, c->s>>>(hr, H);
@@ -850,6 +850,14 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess)
       c->pf_mask_lds = ml;
   }
+  // hysteresis bands: edge, strong and candidate words of HB_ROWS rows in LDS
+  if (hipFuncSetAttribute((const void*)k_hyst_band, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(3 * sizeof(uint32_t) * HB_ROWS * bits::words(c->Wmax))) != hipSuccess) {
+    g_create_err = "max_width too large for the hysteresis band kernel";
+    (void)hipStreamDestroy(c->s);
+    delete c;
+    return MANTIS_ERR_ARG;
+  }
   c->morph_bh = morph_lds(c->Wmax, MB_BH) <= 160 * 1024 ? MB_BH : MB_BH_NARROW;
   if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -876,7 +884,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
   c->tstride = tbits_words(dbits_wpw(c->Wmax + 2), c->Hmax + 2);
   chk(dalloc(c, &c->d_tbits, (size_t)F * c->tstride));
-  c->rstride = (size_t)c->Hmax + 3;
+  c->rstride = (size_t)c->Hmax + 3 + (c->Hmax + HB_ROWS - 1) / HB_ROWS;  // + the hysteresis band run counts
   chk(dalloc(c, &c->d_rowb, (size_t)F * c->rstride));
   chk(dalloc(c, &c->d_mask, c->plane));
   chk(dalloc(c, &c->d_mbits, (size_t)F * c->bstride));

@@ -2,8 +2,7 @@
 //
 // Stage map (reference -> kernel):
 //   cvtColor+GaussianBlur+Canny NMS  QuadDetection.h:209-212        k_canny (candidate / strong bit planes)
-//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_count / k_run_scan / k_hyst_runs /
-//                                                                    k_hyst_band / _seam / _mark / _fix (run CCL)
+//   Canny hysteresis                 (OpenCV, [3P])                  k_hyst_band / _seam / _mark / _fix (run CCL)
 //   dilate x2 / erode x1             QuadDetection.h:213-214         k_morph (bit planes, LDS bands)
 //   cleanImageByEdge mask            HypothesisEvaluation.h:319-386  k_morph (same pass)
 //   findContours(CCOMP, SIMPLE)      QuadDetection.h:216             k_run_count/_scan/_emit/_band/_seam/_border
@@ -107,13 +106,13 @@ __device__ inline void lds_union(int* L, int a, int b) {
 // both) and cv::Canny's hysteresis stack walk, i.e. the 8-connected components
 // of the NMS candidates that hold a strong pixel. Nothing per-pixel reaches HBM
 // but bit planes:
-//   k_canny      per 128x16 tile: BGR (vector loads) -> classes in LDS ->
-//                candidate and strong bit planes (one ballot per 64 pixels)
-//   k_hyst_count / k_run_scan / k_hyst_runs   candidate runs per row, their
-//                ids (raster order), extents
-//   k_hyst_band  8-connected run unions inside 32-row bands in LDS; the edge
-//                words of every band component with a strong pixel; lists of
-//                the components that reach a band seam
+//   k_canny_strip / k_canny   column strips walked by one wave (DPP taps) /
+//                128x16 tiles (LDS): BGR -> classes -> candidate and strong bit
+//                planes
+//   k_hyst_band  per 32-row band: the two planes' words into LDS, candidate
+//                runs per row numbered inside the band, 8-connected run
+//                unions in LDS; the edge words of every band component with a
+//                strong pixel; lists of the components that reach a band seam
 //   k_hyst_seam  the same unions across band seams (global labels)
 //   k_hyst_mark  strong components at a seam mark their global root
 //   k_hyst_fix   weak components at a seam whose global root is marked: edges
@@ -617,7 +616,8 @@ struct StripRegs {
   uint32_t gxa[3], gxb[3], gya[3], gyb[3];  // Sobel gx / gy
 };
 struct StripWave {
-  const uint8_t* rowp;
+  const uint8_t* bgr;  // the frame (wave-uniform); lane offsets are 32-bit
+  uint32_t loff;       // this lane's first byte in a row
   uint32_t rstep;
   int H, WW, lane;
   bool left_edge, right_edge, inside, store_lane;
@@ -627,7 +627,11 @@ struct StripWave {
   uint32_t n0, n1, n2;  // input row i (prefetched)
 };
 // Iteration i of the walk (S = i % 3): hblur(i), blur(i-1), Sobel(i-2), NMS(i-3).
-template <int S>
+// ROWS: the frame's first / last rows may be among them (else all four rows
+// are inside the frame and no row rule applies: 6 <= i <= H - 1); EDGE: the
+// strip holds the frame's first or last column group (else no lane needs a
+// column rule).
+template <int S, bool ROWS, bool EDGE>
 __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
   constexpr int S1 = (S + 1) % 3, S2 = (S + 2) % 3;  // slots of rows i-2 / i+1, i-1
   constexpr int SHIFT = 15;
@@ -635,29 +639,30 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
   const u16x2 c84 = {84, 84}, c89 = {89, 89}, two = {2, 2};
   const int H = w.H;
   // ---- gray and horizontal blur of input row i
-  if (i < H) {
+  if (!ROWS || i < H) {
     const uint32_t d0 = w.n0, d1 = w.n1, d2 = w.n2;
-    gu32* qn = gwords(w.rowp + (uint32_t)(i + 1 < H ? i + 1 : i) * w.rstep);  // next row (the last row again at the end)
+    gu32* qn = gwords(w.bgr + (w.loff + (uint32_t)(i + 1 < H ? i + 1 : i) * w.rstep));  // next row (the last row again at the end)
     w.n0 = qn[0];
     w.n1 = qn[1];
     w.n2 = qn[2];
     const uint32_t g = gray4(d0, d1, d2);
     uint32_t gl = dpp_from_left(g), gr = dpp_from_right(g);
-    if (w.left_edge) gl = g << 16;   // gray(-1) = gray(1)
-    if (w.right_edge) gr = g >> 16;  // gray(W) = gray(W-2)
+    if (EDGE && w.left_edge) gl = g << 16;   // gray(-1) = gray(1)
+    if (EDGE && w.right_edge) gr = g >> 16;  // gray(W) = gray(W-2)
     const Taps4 tp = taps4(gl, g, gr);
     const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
     const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
     R.hba[S] = upk(o01);
     R.hbb[S] = upk(o23);
-  } else if (i == H) {  // row H = row H-2 (reflect), for the blur of row H-1
+  } else if (ROWS && i == H) {  // row H = row H-2 (reflect), for the blur of row H-1
     R.hba[S] = R.hba[S1];
     R.hbb[S] = R.hbb[S1];
   }
   // ---- vertical blur of row j = i - 1 (hblur rows j-1, j, j+1 = slots S1, S2, S)
   const int j = i - 1;
-  if (j >= 0 && j < H) {
-    const uint32_t aa = j == 0 ? R.hba[S] : R.hba[S1], ab = j == 0 ? R.hbb[S] : R.hbb[S1];  // row -1 = row 1
+  if (!ROWS || (j >= 0 && j < H)) {
+    const bool top = ROWS && j == 0;
+    const uint32_t aa = top ? R.hba[S] : R.hba[S1], ab = top ? R.hbb[S] : R.hbb[S1];  // row -1 = row 1
     const uint32_t av[4] = {aa & 0xffffu, aa >> 16, ab & 0xffffu, ab >> 16};
     const uint32_t bv[4] = {R.hba[S2] & 0xffffu, R.hba[S2] >> 16, R.hbb[S2] & 0xffffu, R.hbb[S2] >> 16};
     const uint32_t cv[4] = {R.hba[S] & 0xffffu, R.hba[S] >> 16, R.hbb[S] & 0xffffu, R.hbb[S] >> 16};
@@ -668,13 +673,13 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
       o |= (r > 255u ? 255u : r) << (8 * k);
     }
     R.bl[S2] = o;
-  } else if (j == H) {
+  } else if (ROWS && j == H) {
     R.bl[S2] = R.bl[S1];  // row H = row H-1 (replicate), for the Sobel of row H-1
   }
   // ---- Sobel of row k = i - 2 (blur rows k-1, k, k+1 = slots S, S1, S2)
   const int k = i - 2;
-  if (k >= 0 && k < H) {
-    const uint32_t a = k == 0 ? R.bl[S1] : R.bl[S];  // row -1 = row 0
+  if (!ROWS || (k >= 0 && k < H)) {
+    const uint32_t a = ROWS && k == 0 ? R.bl[S1] : R.bl[S];  // row -1 = row 0
     const uint32_t b = R.bl[S1], c = R.bl[S2];
     const u16x2 A01 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c010c00u)), A23 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c030c02u));
     const u16x2 B01 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c010c00u)), B23 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c030c02u));
@@ -684,8 +689,8 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
     const uint32_t vd23 = upk(vpk<s16x2>(upk(C23)) - vpk<s16x2>(upk(A23)));
     uint32_t VL = dpp_from_left(vs23), VR = dpp_from_right(vs01);
     uint32_t DL = dpp_from_left(vd23), DR = dpp_from_right(vd01);
-    if (w.left_edge) { VL = vs01 << 16; DL = vd01 << 16; }    // blur(-1) = blur(0)
-    if (w.right_edge) { VR = vs23 >> 16; DR = vd23 >> 16; }   // blur(W) = blur(W-1)
+    if (EDGE && w.left_edge) { VL = vs01 << 16; DL = vd01 << 16; }    // blur(-1) = blur(0)
+    if (EDGE && w.right_edge) { VR = vs23 >> 16; DR = vd23 >> 16; }   // blur(W) = blur(W-1)
     const s16x2 S0v = vpk<s16x2>(__builtin_amdgcn_perm(vs01, VL, 0x05040302u));  // columns -1, 0
     const s16x2 S1v = vpk<s16x2>(__builtin_amdgcn_perm(vs23, vs01, 0x05040302u)); // 1, 2
     const s16x2 S2v = vpk<s16x2>(__builtin_amdgcn_perm(VR, vs23, 0x05040302u));   // 3, 4
@@ -702,21 +707,22 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
     R.gxb[S1] = upk(gx23);
     R.gya[S1] = upk(gy01);
     R.gyb[S1] = upk(gy23);
-  } else if (k == H) {
+  } else if (ROWS && k == H) {
     R.mga[S1] = 0;  // magnitude below the frame: zero
     R.mgb[S1] = 0;
   }
   // ---- NMS of row n = i - 3 (magnitude rows n-1, n, n+1 = slots S2, S, S1)
   const int n = i - 3;
-  if (n < 0) return;
-  const uint32_t ua = n == 0 ? 0u : R.mga[S2], ub = n == 0 ? 0u : R.mgb[S2];  // magnitude above the frame: zero
+  if (ROWS && n < 0) return;
+  const bool first = ROWS && n == 0;
+  const uint32_t ua = first ? 0u : R.mga[S2], ub = first ? 0u : R.mgb[S2];  // magnitude above the frame: zero
   uint32_t P[3][3], Cw[3][2];
   const uint32_t rwa[3] = {ua, R.mga[S], R.mga[S1]}, rwb[3] = {ub, R.mgb[S], R.mgb[S1]};
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     uint32_t Lw = dpp_from_left(rwb[r]), Rw = dpp_from_right(rwa[r]);
-    if (w.left_edge) Lw = 0u;
-    if (w.right_edge) Rw = 0u;
+    if (EDGE && w.left_edge) Lw = 0u;
+    if (EDGE && w.right_edge) Rw = 0u;
     Cw[r][0] = rwa[r];
     Cw[r][1] = rwb[r];
     P[r][0] = __builtin_amdgcn_perm(rwa[r], Lw, 0x05040302u);
@@ -753,8 +759,9 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
   // nibbles (pixel 2h + t <-> bit t of half h) into 32-bit words of 8 lanes
   const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
   const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
-  uint32_t cw = w.inside ? ((xp | (xp >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
-  uint32_t sw = w.inside ? ((xs | (xs >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
+  // (outside the frame: lanes past the last column group of an edge strip)
+  uint32_t cw = !EDGE || w.inside ? ((xp | (xp >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
+  uint32_t sw = !EDGE || w.inside ? ((xs | (xs >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
   cw |= dpp_row_shr(cw, 1);
   sw |= dpp_row_shr(sw, 1);
   cw |= dpp_row_shr(cw, 2);
@@ -762,8 +769,34 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
   cw |= dpp_row_shr(cw, 4);
   sw |= dpp_row_shr(sw, 4);
   if (w.store_lane) {
-    w.cb[(size_t)n * w.WW + (w.lane >> 3)] = cw;
-    w.sbp[(size_t)n * w.WW + (w.lane >> 3)] = sw;
+    const uint32_t o = 4u * ((uint32_t)n * (uint32_t)w.WW + (uint32_t)(w.lane >> 3));  // byte offset
+    *(uint32_t*)((char*)w.cb + o) = cw;
+    *(uint32_t*)((char*)w.sbp + o) = sw;
+  }
+}
+// rows 0 .. H+2 in triples (row i in slot i % 3): the first two triples and
+// the last ones with the row rules, the triples between without
+template <bool EDGE>
+__device__ __forceinline__ void strip_walk(StripWave& w, StripRegs& R) {
+  const int rows = w.H + 3;
+  int i = 0;
+#pragma unroll 1
+  for (; i < 6 && i < rows; i += 3) {
+    strip_step<0, true, EDGE>(w, R, i);
+    if (i + 1 < rows) strip_step<1, true, EDGE>(w, R, i + 1);
+    if (i + 2 < rows) strip_step<2, true, EDGE>(w, R, i + 2);
+  }
+#pragma unroll 1
+  for (; i + 2 < w.H; i += 3) {
+    strip_step<0, false, EDGE>(w, R, i);
+    strip_step<1, false, EDGE>(w, R, i + 1);
+    strip_step<2, false, EDGE>(w, R, i + 2);
+  }
+#pragma unroll 1
+  for (; i < rows; i += 3) {
+    strip_step<0, true, EDGE>(w, R, i);
+    if (i + 1 < rows) strip_step<1, true, EDGE>(w, R, i + 1);
+    if (i + 2 < rows) strip_step<2, true, EDGE>(w, R, i + 2);
   }
 }
 __global__ __launch_bounds__(256) void k_canny_strip(const FrameDesc* __restrict__ frames, int low, int high,
@@ -789,23 +822,19 @@ __global__ __launch_bounds__(256) void k_canny_strip(const FrameDesc* __restrict
   const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
   w.LOW = s16x2{(short)lowc, (short)lowc};
   w.HIGH = s16x2{(short)highc, (short)highc};
-  w.rowp = fd.bgr + (uint32_t)lc * 3u;
+  w.bgr = fd.bgr;
+  w.loff = (uint32_t)lc * 3u;
   w.rstep = (uint32_t)W * 3u;
   w.cb = cbits + (size_t)f * bstride + (size_t)(base >> 5);
   w.sbp = sbits + (size_t)f * bstride + (size_t)(base >> 5);
   w.store_lane = (w.lane & 7) == 7 && w.lane < 56 && base + 4 * (w.lane & ~7) < W;
   StripRegs R = {};
-  gu32* q = gwords(w.rowp);
+  gu32* q = gwords(w.bgr + w.loff);
   w.n0 = q[0];
   w.n1 = q[1];
   w.n2 = q[2];
-  const int rows = w.H + 3;
-#pragma unroll 1
-  for (int i = 0; i < rows; i += 3) {
-    strip_step<0>(w, R, i);
-    if (i + 1 < rows) strip_step<1>(w, R, i + 1);
-    if (i + 2 < rows) strip_step<2>(w, R, i + 2);
-  }
+  if (sidx == 0 || sidx == nstrip - 1) strip_walk<true>(w, R);
+  else strip_walk<false>(w, R);
 }
 
 // ------------------------------------------------ hysteresis: run CCL
@@ -830,57 +859,6 @@ __device__ inline uint32_t span_mask(int w, int a, int b) {
   const uint32_t hi = w == (b >> 5) ? (0xffffffffu >> (31 - (b & 31))) : 0xffffffffu;
   return lo & hi;
 }
-struct HystRuns {  // per-frame planes (frame f at + f * stride)
-  uint32_t* x;     // run extents: start | end << 16
-  int32_t* lab;    // run labels
-  uint8_t* flag;   // per root: bit 2 = the global component holds a strong pixel (denser bands: bits 0 / 1
-                   // = strong / reaches a seam, per band root)
-  int32_t* rowb;   // row bases (H + 1), then the list counters |A|, |B|
-  size_t x_stride, lab_stride, flag_stride, rstride, half;
-};
-
-// wave per row: candidate runs of the row
-__global__ __launch_bounds__(256) void k_hyst_count(const uint32_t* __restrict__ cbits, size_t bstride, HystRuns hr,
-                                                    int W, int H) {
-  const int f = blockIdx.y, y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (y >= H) return;
-  const int WW = bits::words(W);
-  const uint32_t* row = cbits + (size_t)f * bstride + (size_t)y * WW;
-  int c = 0;
-  for (int w = lane; w < WW; w += 64) c += __popc(hb_starts(row, w));
-  c = wave_sum(c);
-  if (lane == 0) hr.rowb[(size_t)f * hr.rstride + y] = c;
-  if (y == 0 && lane == 0) {  // list counters (k_hyst_band): rowb[H + 1] = |A|, rowb[H + 2] = |B|
-    hr.rowb[(size_t)f * hr.rstride + H + 1] = 0;
-    hr.rowb[(size_t)f * hr.rstride + H + 2] = 0;
-  }
-}
-
-// wave per row: run extents. Runs of a row are disjoint, so its k-th start
-// bit and its k-th end bit bound run k: starts and ends are numbered by two
-// wave scans and written as the two 16-bit halves of the packed extent (no
-// search for the end).
-__global__ __launch_bounds__(256) void k_hyst_runs(const uint32_t* __restrict__ cbits, size_t bstride, HystRuns hr,
-                                                   int W, int H) {
-  const int f = blockIdx.y, y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (y >= H) return;
-  const int WW = bits::words(W);
-  const uint32_t* row = cbits + (size_t)f * bstride + (size_t)y * WW;
-  uint16_t* X16 = (uint16_t*)(hr.x + (size_t)f * hr.x_stride);  // extent j = start | end << 16
-  int bs = hr.rowb[(size_t)f * hr.rstride + y], be = bs;
-  for (int w0 = 0; w0 < WW; w0 += 64) {
-    const int w = w0 + lane;
-    uint32_t S = w < WW ? hb_starts(row, w) : 0u;
-    uint32_t E = w < WW ? hb_ends(row, w, WW) : 0u;
-    const int cs = __popc(S), ce = __popc(E);
-    const int is = wave_incl_scan(cs, lane), ie = wave_incl_scan(ce, lane);
-    for (int os = bs + is - cs; S; S &= S - 1, os++) X16[2 * (size_t)os] = (uint16_t)(32 * w + __ffs(S) - 1);
-    for (int oe = be + ie - ce; E; E &= E - 1, oe++) X16[2 * (size_t)oe + 1] = (uint16_t)(32 * w + __ffs(E) - 1);
-    bs += __shfl(is, 63);
-    be += __shfl(ie, 63);
-  }
-}
-
 // first run k of [0, n) whose end reaches v, n if none (packed extents)
 __device__ inline int hx_first_end(const uint32_t* x, int n, int v) {
   int lo = 0, hi = n;
@@ -907,6 +885,17 @@ __device__ inline bool run_strong(const uint32_t* srow, int a, int b) {
   return false;
 }
 
+struct HystRuns {  // per-frame planes (frame f at + f * stride)
+  uint32_t* x;     // run extents: start | end << 16 (seam rows, list B runs; every run of a dense band)
+  int32_t* lab;    // run labels
+  uint8_t* flag;   // per root: bit 2 = the global component holds a strong pixel (denser bands: bits 0 / 1
+                   // = strong / reaches a seam, per band root)
+  int32_t* rowb;   // per row: its first run's index inside the band; [H + 1], [H + 2] = |A|, |B|;
+                   // [H + 3 + b] = runs of band b
+  size_t x_stride, lab_stride, flag_stride, rstride, half;
+  int bs;          // run ids per band: run i of band b is b * bs + i (bs = band rows x ceil(W / 2))
+};
+
 // Per band of HB_ROWS rows: unions in LDS (labels = band roots, written to
 // the global labels for the seams), then the band's edge words: the runs of
 // band components holding a strong pixel are edges whatever the rest of the
@@ -923,6 +912,13 @@ __device__ inline bool run_strong(const uint32_t* srow, int a, int b) {
 #define MK_HB_THREADS 512
 #endif
 constexpr int HB_ROWS = MK_HB_ROWS, HB_CAP = 4096, HB_THREADS = MK_HB_THREADS, HB_WAVES = HB_THREADS / 64;
+// global id of row y's first run and the row's run count
+__device__ inline void hr_row(const int32_t* rb, int H, int bs, int y, int& g, int& cnt) {
+  const int b = y / HB_ROWS, s = rb[y];
+  const int e = (y + 1 < H && (y + 1) % HB_ROWS != 0) ? rb[y + 1] : rb[H + 3 + b];
+  g = b * bs + s;
+  cnt = e - s;
+}
 // band-local union-find on 16-bit labels in LDS (roots = smallest id); the
 // link is a 32-bit CAS on the dword holding the 16-bit slot
 __device__ inline int hb_find(const uint16_t* L, int x) {
@@ -957,97 +953,142 @@ __device__ inline void hyst_push(int32_t* list, int32_t* count, int v, bool push
     list[down ? top - 1 - k : k] = v;
   }
 }
-__global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __restrict__ sbits, size_t bstride, HystRuns hr,
-                                                   uint32_t* __restrict__ ebits, int W, int H) {
+// run extents of a band row (candidate words cw in LDS) from local index o:
+// its k-th start bit and k-th end bit bound run k (two wave scans, no search)
+template <class P>
+__device__ inline void hb_emit_runs(const uint32_t* cw, int WW, P* X16, int o, int lane) {
+  int bs = o, be = o;
+  for (int w0 = 0; w0 < WW; w0 += 64) {
+    const int w = w0 + lane;
+    uint32_t S = w < WW ? hb_starts(cw, w) : 0u;
+    uint32_t E = w < WW ? hb_ends(cw, w, WW) : 0u;
+    const int cs = __popc(S), ce = __popc(E);
+    const int is = wave_incl_scan(cs, lane), ie = wave_incl_scan(ce, lane);
+    for (int os = bs + is - cs; S; S &= S - 1, os++) X16[2 * os] = (uint16_t)(32 * w + __ffs(S) - 1);
+    for (int oe = be + ie - ce; E; E &= E - 1, oe++) X16[2 * oe + 1] = (uint16_t)(32 * w + __ffs(E) - 1);
+    bs += __shfl(is, 63);
+    be += __shfl(ie, 63);
+  }
+}
+// One block per band: the band's candidate and strong words into LDS, its
+// runs counted and numbered (band-local ids: no frame-wide scan), unions,
+// classes, edge words, lists. Global traffic: the two bit planes' words once,
+// the edge words once, labels / extents of the rows and runs later kernels read.
+__global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __restrict__ cbits,
+                                                          const uint32_t* __restrict__ sbits, size_t bstride, HystRuns hr,
+                                                          uint32_t* __restrict__ ebits, int W, int H) {
   __shared__ uint16_t Ll[HB_CAP];
   __shared__ uint32_t Xl[HB_CAP];
   __shared__ uint32_t Sl[HB_CAP / 4];  // per root byte: bit 0 strong, bit 1 reaches the band's edge rows
   __shared__ int32_t rbl[HB_ROWS + 1];
-  extern __shared__ uint32_t Ew[];     // the band's edge words (rows x WW), then its strong words
+  extern __shared__ uint32_t Ew[];     // the band's edge words (rows x WW), then its strong words, then its candidates
   const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int y0 = blockIdx.x * HB_ROWS;
+  const int band = blockIdx.x, y0 = band * HB_ROWS;
   if (y0 >= H) return;
   const int y1 = min(y0 + HB_ROWS, H), WW = bits::words(W), nr = y1 - y0;
-  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
-  int32_t* cnt = hr.rowb + (size_t)f * hr.rstride + H + 1;
-  const uint32_t* X = hr.x + (size_t)f * hr.x_stride;
-  const uint32_t* sb = sbits + (size_t)f * bstride;
+  int32_t* rb = hr.rowb + (size_t)f * hr.rstride;
+  int32_t* cnt = rb + H + 1;
+  uint32_t* X = hr.x + (size_t)f * hr.x_stride;
   int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
   int32_t* lists = L + hr.half;
   const size_t top = hr.lab_stride - hr.half;
   uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
   uint32_t* eb = ebits + (size_t)f * bstride + (size_t)y0 * WW;
-  const int g0 = r[y0], n = r[y1] - g0;
+  const int g0 = band * hr.bs;
+  uint32_t* Sw = Ew + nr * WW;
+  uint32_t* Cw = Sw + nr * WW;
+  const uint32_t* sb = sbits + (size_t)f * bstride + (size_t)y0 * WW;
+  const uint32_t* cb = cbits + (size_t)f * bstride + (size_t)y0 * WW;
+  for (int i = t; i < nr * WW; i += HB_THREADS) {
+    Ew[i] = 0u;
+    Sw[i] = sb[i];
+    Cw[i] = cb[i];
+  }
+  __syncthreads();
+  // runs per row (wave per row), then the band's row bases
+  for (int q = wave; q < nr; q += HB_WAVES) {
+    int c = 0;
+    for (int w = lane; w < WW; w += 64) c += __popc(hb_starts(Cw + q * WW, w));
+    c = wave_sum(c);
+    if (lane == 0) rbl[q + 1] = c;
+  }
+  __syncthreads();
+  if (t < 64) {
+    const int v = t < nr ? rbl[t + 1] : 0;
+    const int s = wave_incl_scan(v, t);
+    if (t < nr) {
+      rbl[t + 1] = s;
+      rb[y0 + t] = s - v;
+    }
+    if (t == 0) rbl[0] = 0;
+    if (t == nr - 1) rb[H + 3 + band] = s;
+  }
+  __syncthreads();
+  const int n = rbl[nr];
   // a row whose components may continue past the band: its first / last row inside the frame
-  const auto edge_row = [&](int y) { return (y == y0 && y0 > 0) || (y == y1 - 1 && y1 < H); };
+  const auto edge_row = [&](int q) { return (q == 0 && y0 > 0) || (q == nr - 1 && y1 < H); };
   if (n > HB_CAP) {
+    for (int q = wave; q < nr; q += HB_WAVES) hb_emit_runs(Cw + q * WW, WW, (uint16_t*)(X + g0), rbl[q], lane);
     for (int i = t; i < n; i += HB_THREADS) {
       L[g0 + i] = g0 + i;
       fl[g0 + i] = 0;
     }
-    for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = 0u;
     __syncthreads();
     const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
-    for (int y = y0 + 1 + wave; y < y1; y += HB_WAVES) hyst_row_union(X, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], lane, uni);
+    for (int q = 1 + wave; q < nr; q += HB_WAVES)
+      hyst_row_union(X, g0 + rbl[q - 1], rbl[q] - rbl[q - 1], g0 + rbl[q], rbl[q + 1] - rbl[q], lane, uni);
     __syncthreads();
-    for (int y = y0 + wave; y < y1; y += HB_WAVES)
-      for (int j = r[y] + lane; j < r[y + 1]; j += 64) {
+    for (int q = wave; q < nr; q += HB_WAVES)
+      for (int j = g0 + rbl[q] + lane; j < g0 + rbl[q + 1]; j += 64) {
         const int root = uf_find_c(L, j);
-        const uint32_t b = (run_strong(sb + (size_t)y * WW, X[j] & 0xffff, X[j] >> 16) ? 1u : 0u) | (edge_row(y) ? 2u : 0u);
+        const uint32_t b = (run_strong(Sw + q * WW, X[j] & 0xffff, X[j] >> 16) ? 1u : 0u) | (edge_row(q) ? 2u : 0u);
         if (b) atomicOr((uint32_t*)(fl + (root & ~3)), b << (8 * (root & 3)));
       }
     __syncthreads();
-    for (int y = y0 + wave; y < y1; y += HB_WAVES)
-      for (int j = r[y] + lane; j < r[y + 1]; j += 64) {
+    for (int q = wave; q < nr; q += HB_WAVES)
+      for (int j = g0 + rbl[q] + lane; j < g0 + rbl[q + 1]; j += 64) {
         const int root = uf_find_c(L, j);
         const int fb = fl[root] & 3;
         if (fb & 1) {
           const int a = X[j] & 0xffff, b = X[j] >> 16;
-          for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&eb[(y - y0) * WW + w], span_mask(w, a, b));
+          for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
         }
         hyst_push(lists, cnt + 1, j, fb == 2, true, top);
         hyst_push(lists, cnt, j, root == j && fb == 3, false, top);
       }
+    __syncthreads();
+    for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = Ew[i];
     return;
   }
-  for (int i = t; i <= nr; i += HB_THREADS) rbl[i] = r[y0 + i] - g0;
-  for (int i = t; i < n; i += HB_THREADS) {
-    Xl[i] = X[g0 + i];
-    Ll[i] = (uint16_t)i;
-  }
-  uint32_t* Sw = Ew + nr * WW;
+  for (int q = wave; q < nr; q += HB_WAVES) hb_emit_runs(Cw + q * WW, WW, (uint16_t*)Xl, rbl[q], lane);
+  for (int i = t; i < n; i += HB_THREADS) Ll[i] = (uint16_t)i;
   for (int i = t; i < (n + 3) / 4; i += HB_THREADS) Sl[i] = 0u;
-  for (int i = t; i < nr * WW; i += HB_THREADS) {
-    Ew[i] = 0u;
-    Sw[i] = sb[(size_t)y0 * WW + i];
-  }
   __syncthreads();
   uint16_t* Li = Ll;
   const auto uni = [Li](int a, int b) { hb_union(Li, a, b); };
-  for (int y = y0 + 1 + wave; y < y1; y += HB_WAVES) {
-    const int q = y - y0;
+  for (int q = 1 + wave; q < nr; q += HB_WAVES)
     hyst_row_union(Xl, rbl[q - 1], rbl[q] - rbl[q - 1], rbl[q], rbl[q + 1] - rbl[q], lane, uni);
-  }
   __syncthreads();
-  for (int y = y0 + wave; y < y1; y += HB_WAVES) {
-    const int q = y - y0;
+  for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = hb_find(Ll, j);
       Ll[j] = (uint16_t)root;
-      const uint32_t b = (run_strong(Sw + q * WW, Xl[j] & 0xffff, Xl[j] >> 16) ? 1u : 0u) | (edge_row(y) ? 2u : 0u);
+      const uint32_t b = (run_strong(Sw + q * WW, Xl[j] & 0xffff, Xl[j] >> 16) ? 1u : 0u) | (edge_row(q) ? 2u : 0u);
       if (b) atomicOr(&Sl[root >> 2], b << (8 * (root & 3)));
     }
   }
   __syncthreads();
-  for (int y = y0 + wave; y < y1; y += HB_WAVES) {
-    const int q = y - y0;
+  for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = Ll[j];
       const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
-      // global labels only where a later kernel looks: the band's first and
-      // last rows (seam unions), list B runs (fb == 2) and band roots (finds
-      // end there; their flag byte is what k_hyst_mark / k_hyst_fix use)
-      if (q == 0 || q == nr - 1 || fb == 2 || root == j) L[g0 + j] = g0 + root;
+      // global labels / extents only where a later kernel looks: the band's
+      // first and last rows (seam unions), list B runs (fb == 2: k_hyst_fix)
+      // and band roots (finds end there; their flag byte is what k_hyst_mark /
+      // k_hyst_fix use)
+      const bool seam_row = q == 0 || q == nr - 1;
+      if (seam_row || fb == 2 || root == j) L[g0 + j] = g0 + root;
+      if (seam_row || fb == 2) X[g0 + j] = Xl[j];
       if (root == j) fl[g0 + j] = 0;
       if (fb & 1) {
         const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
@@ -1066,10 +1107,13 @@ __global__ __launch_bounds__(256) void k_hyst_seam(HystRuns hr, int H) {
   const int f = blockIdx.y, lane = threadIdx.x & 63;
   const int y = (blockIdx.x * 4 + (threadIdx.x >> 6) + 1) * HB_ROWS;
   if (y >= H) return;
-  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
+  const int32_t* rb = hr.rowb + (size_t)f * hr.rstride;
   int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
   const auto uni = [L](int a, int b) { uf_union_c(L, a, b); };
-  hyst_row_union(hr.x + (size_t)f * hr.x_stride, r[y - 1], r[y] - r[y - 1], r[y], r[y + 1] - r[y], lane, uni);
+  int gp, np, gy, ny;
+  hr_row(rb, H, hr.bs, y - 1, gp, np);
+  hr_row(rb, H, hr.bs, y, gy, ny);
+  hyst_row_union(hr.x + (size_t)f * hr.x_stride, gp, np, gy, ny, lane, uni);
 }
 
 // list A: strong band components reaching a seam mark their global root (bit 2)
@@ -1089,8 +1133,8 @@ __global__ __launch_bounds__(256) void k_hyst_mark(HystRuns hr, int H) {
 __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restrict__ ebits, size_t bstride, int W,
                                                   int H) {
   const int f = blockIdx.y;
-  const int32_t* r = hr.rowb + (size_t)f * hr.rstride;
-  const int n = r[H + 2];
+  const int32_t* rb = hr.rowb + (size_t)f * hr.rstride;
+  const int n = rb[H + 2];
   int32_t* L = hr.lab + (size_t)f * hr.lab_stride;
   const int32_t* Bl = L + hr.lab_stride - 1;  // B[i] = Bl[-i]
   const uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
@@ -1099,10 +1143,11 @@ __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restr
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int j = Bl[-i];
     if (!(fl[uf_find_c(L, j)] & 4)) continue;
-    int lo = 0, hi = H - 1;  // row of run j: largest y with r[y] <= j
+    const int band = j / hr.bs, l = j - band * hr.bs;
+    int lo = band * HB_ROWS, hi = min(H, lo + HB_ROWS) - 1;  // row of run j: largest y of the band with rb[y] <= l
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (r[mid] <= j) lo = mid;
+      if (rb[mid] <= l) lo = mid;
       else hi = mid - 1;
     }
     const int a = X[j] & 0xffff, b = X[j] >> 16;

@@ -5,6 +5,8 @@ projection counts, integer error sums => identical fast errors); poses from
 identical decisions compared with an FP64 tolerance (1e-9 absolute) because
 device libm (atan/sin/cos/tan/sqrt) may differ from glibc by an ulp.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -65,6 +67,43 @@ def test_canny_bit_exact_odd_sizes_and_noise(mantis):
         got = mantis.canny(M.make_image(img, K, D))
         ref = O.canny(img)
         assert np.array_equal(got, ref), f"{w}x{h}: canny differs at {np.argwhere(got != ref)[:10]}"
+
+
+@pytest.mark.parametrize("strip", ["1", "0"])
+def test_canny_strip_and_tile_kernels_bit_exact(strip):
+    """Both Canny kernels (k_canny_strip: column strips walked by one wave,
+    DPP neighbour taps; k_canny: 128x32 LDS tiles; MANTIS_CANNY_STRIP picks)
+    against the oracle on widths that end a strip mid-word, the first / last
+    column groups at the frame edges, 3-row frames and blob noise."""
+    import mantis_amd as M
+
+    saved = os.environ.get("MANTIS_CANNY_STRIP")
+    os.environ["MANTIS_CANNY_STRIP"] = strip
+    try:
+        mt = M.Mantis(max_cams=1, max_width=1280, max_height=720)
+    finally:
+        if saved is None:
+            os.environ.pop("MANTIS_CANNY_STRIP")
+        else:
+            os.environ["MANTIS_CANNY_STRIP"] = saved
+    rng = np.random.default_rng(5)
+    K, D = synth.intrinsics()
+    try:
+        for (w, h) in [(1280, 720), (1000, 611), (232, 40), (448, 17), (8, 3), (224, 5), (12, 9)]:
+            base = rng.integers(0, 256, (h // 3 + 2, w // 3 + 2, 3)).astype(np.float64)
+            img = np.repeat(np.repeat(base, 3, 0), 3, 1)[:h, :w]
+            img = np.clip(img + rng.normal(0, 30, img.shape), 0, 255).astype(np.uint8)
+            got = mt.canny(M.make_image(img, K, D))
+            ref = O.canny(img)
+            assert np.array_equal(got, ref), f"{w}x{h}: canny differs at {np.argwhere(got != ref)[:10]}"
+        # i.i.d. noise: more than 4096 candidate runs per 32-row band (the
+        # hysteresis bands' global-label path)
+        img = rng.integers(0, 256, (720, 1280, 3)).astype(np.uint8)
+        got = mt.canny(M.make_image(img, K, D))
+        ref = O.canny(img)
+        assert np.array_equal(got, ref), f"noise: canny differs at {np.argwhere(got != ref)[:10]}"
+    finally:
+        mt.close()
 
 
 def test_detector_binary_and_mask_bit_exact(mantis, frames):

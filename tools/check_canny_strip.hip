@@ -8,11 +8,55 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
 using namespace mk;
 
-int main() {
+// time mode: N copies of one 1280x720 noise frame, both kernels timed with
+// HIP events (best of 5); for rocprofv3 --pmc passes on the kernels alone.
+static int time_mode(int N) {
+  const int W = 1280, H = 720;
+  const size_t fb = (size_t)W * H * 3;
+  std::vector<uint8_t> img(fb);
+  std::mt19937 rng(9);
+  for (size_t i = 0; i < fb; i++) img[i] = (uint8_t)((((i / 3) % W) / 6 + (i / 3 / W) / 6) & 1 ? 200 + (rng() & 31) : 30 + (rng() & 31));
+  uint8_t* dimg;
+  hipMalloc(&dimg, fb * N);
+  for (int f = 0; f < N; f++) hipMemcpy(dimg + fb * f, img.data(), fb, hipMemcpyHostToDevice);
+  std::vector<FrameDesc> fd(N);
+  for (int f = 0; f < N; f++) { fd[f] = FrameDesc{}; fd[f].bgr = dimg + fb * f; fd[f].w = W; fd[f].h = H; }
+  FrameDesc* dfd;
+  hipMalloc(&dfd, sizeof(FrameDesc) * N);
+  hipMemcpy(dfd, fd.data(), sizeof(FrameDesc) * N, hipMemcpyHostToDevice);
+  const size_t B = (size_t)bits::words(W) * H;
+  uint32_t *c, *s;
+  hipMalloc(&c, B * 4 * N);
+  hipMalloc(&s, B * 4 * N);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
+  const int ns = (W + kStripCols - 1) / kStripCols;
+  for (int kind = 0; kind < 2; kind++) {
+    float best = 1e9f;
+    for (int r = 0; r < 5; r++) {
+      hipEventRecord(e0);
+      if (kind == 0) k_canny<<<tgx * tgy * N, 256>>>(dfd, 30, 90, 1, c, s, B, tgx, tgy);
+      else k_canny_strip<<<(ns * N + 3) / 4, 256>>>(dfd, 30, 90, c, s, B, ns, ns * N);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      best = ms < best ? ms : best;
+    }
+    printf("%s: %d frames %.3f ms (%.3f ms per 4096 frames)\n", kind ? "k_canny_strip" : "k_canny", N, best, best * 4096.0 / N);
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "time") return time_mode(std::atoi(argv[2]));
   const int sizes[][2] = {{1280, 720}, {640, 480}, {1000, 611}, {232, 40}, {8, 3}, {448, 17}};
   int fails = 0;
   std::mt19937 rng(5);

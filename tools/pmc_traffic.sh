@@ -12,8 +12,7 @@ done
 python3 - "$R/gpurun_out" <<'P'
 import csv, glob, json, sys
 FR = 256
-kern = {"canny_nms": ["k_canny"], "hysteresis": ["k_hyst_count", "k_run_scan", "k_hyst_runs", "k_hyst_band",
-                                                 "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"]}
+kern = {"canny_nms": ["k_canny_strip", "k_canny"], "hysteresis": ["k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"]}
 out = {"stage": "canny_nms", "kernel": "k_canny", "frames_per_launch": FR}
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
