@@ -163,7 +163,7 @@ struct Ctx {
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
-  int canny_strip = 1;  // k_canny_strip where the frames allow it (MANTIS_CANNY_STRIP=0: tiles)
+  int canny_strip = 2;  // k_canny_strip: 2 = 8 columns per lane where W % 8 == 0, 1 = 4 columns; 0 = tiles (MANTIS_CANNY_STRIP)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -366,11 +366,16 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   mark(c, "start");
   const size_t B = c->bstride;
   const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
-  if (c->canny_strip && c->vec_ok && W >= 8 && H >= 3) {
-    // column strips walked by one wave each (W % 4 == 0, dword-aligned rows)
-    const int ns = (W + kStripCols - 1) / kStripCols, nw = ns * n;
-    k_canny_strip<<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
-                                                              c->d_b1, c->d_b2, B, ns, nw);
+  if (c->canny_strip >= 2 && c->vec_ok && W % 8 == 0 && W >= 16 && H >= 3) {
+    // column strips walked by one wave each, 8 columns per lane (W % 8 == 0)
+    const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols, nw = ns * n;
+    k_canny_strip<2><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
+                                                                 c->d_b1, c->d_b2, B, ns, nw);
+  } else if (c->canny_strip && c->vec_ok && W >= 8 && H >= 3) {
+    // 4 columns per lane (W % 4 == 0, dword-aligned rows)
+    const int ns = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols, nw = ns * n;
+    k_canny_strip<1><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
+                                                                 c->d_b1, c->d_b2, B, ns, nw);
   } else {
     k_canny<<<(unsigned)(tgx * tgy * n), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
                                                         c->vec_ok ? 1 : 0, c->d_b1, c->d_b2, B, tgx, tgy);
@@ -819,7 +824,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
-  if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = std::atoi(e);
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;

@@ -605,16 +605,30 @@ __device__ inline uint32_t dpp_row_shr(uint32_t v, int n) {  // lane l gets lane
     default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, true);
   }
 }
-constexpr int kStripCols = 224;  // output columns per strip (7 words)
+// K column groups of 4 per lane: K = 1 (W % 4 == 0) strips of 56 lanes x 4 =
+// 224 columns (7 words, halo lanes 56 / 63); K = 2 (W % 8 == 0) strips of 60
+// lanes x 8 = 480 columns (15 words, halo lanes 60 / 63): half the DPP,
+// border selects and nibble packing per column, 6 % idle lanes instead of 12 %.
+#ifndef MK_STRIP2_WAVES
+#define MK_STRIP2_WAVES 4
+#endif
+template <int K>
+struct StripGeom {
+  static constexpr int out_lanes = K == 1 ? 56 : 60;       // lanes producing the strip's columns
+  static constexpr int cols = out_lanes * 4 * K;            // columns per strip
+  static constexpr int lanes_per_word = 8 / K;
+};
 // Per-wave state of a strip: three row slots per stage (row r in slot r % 3),
 // so the walk unrolled by three indexes registers with constants and moves
 // nothing between rows.
+template <int K>
 struct StripRegs {
-  uint32_t hba[3], hbb[3];  // horizontal blur, 2 u16 pairs
-  uint32_t bl[3];           // blur, 4 bytes
-  uint32_t mga[3], mgb[3];  // L1 magnitude, 2 i16 pairs
-  uint32_t gxa[3], gxb[3], gya[3], gyb[3];  // Sobel gx / gy
+  uint32_t hba[3][K], hbb[3][K];  // horizontal blur, 2 u16 pairs per group
+  uint32_t bl[3][K];              // blur, 4 bytes per group
+  uint32_t mga[3][K], mgb[3][K];  // L1 magnitude, 2 i16 pairs per group
+  uint32_t gxa[3][K], gxb[3][K], gya[3][K], gyb[3][K];  // Sobel gx / gy
 };
+template <int K>
 struct StripWave {
   const uint8_t* bgr;  // the frame (wave-uniform); lane offsets are 32-bit
   uint32_t loff;       // this lane's first byte in a row
@@ -624,15 +638,26 @@ struct StripWave {
   s16x2 LOW, HIGH;
   uint32_t* cb;
   uint32_t* sbp;
-  uint32_t n0, n1, n2;  // input row i (prefetched)
+  uint32_t nx[K][3];  // input row i (prefetched)
 };
+template <int K>
+__device__ __forceinline__ void strip_load(StripWave<K>& w, int row) {
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    gu32* q = gwords(w.bgr + (w.loff + 12u * k + (uint32_t)row * w.rstep));
+    w.nx[k][0] = q[0];
+    w.nx[k][1] = q[1];
+    w.nx[k][2] = q[2];
+  }
+}
 // Iteration i of the walk (S = i % 3): hblur(i), blur(i-1), Sobel(i-2), NMS(i-3).
 // ROWS: the frame's first / last rows may be among them (else all four rows
 // are inside the frame and no row rule applies: 6 <= i <= H - 1); EDGE: the
 // strip holds the frame's first or last column group (else no lane needs a
-// column rule).
-template <int S, bool ROWS, bool EDGE>
-__device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
+// column rule). Group k's left / right neighbours are the lane's groups k-1 /
+// k+1, or the neighbouring lanes' last / first group by DPP.
+template <int K, int S, bool ROWS, bool EDGE>
+__device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int i) {
   constexpr int S1 = (S + 1) % 3, S2 = (S + 2) % 3;  // slots of rows i-2 / i+1, i-1
   constexpr int SHIFT = 15;
   constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
@@ -640,184 +665,227 @@ __device__ __forceinline__ void strip_step(StripWave& w, StripRegs& R, int i) {
   const int H = w.H;
   // ---- gray and horizontal blur of input row i
   if (!ROWS || i < H) {
-    const uint32_t d0 = w.n0, d1 = w.n1, d2 = w.n2;
-    gu32* qn = gwords(w.bgr + (w.loff + (uint32_t)(i + 1 < H ? i + 1 : i) * w.rstep));  // next row (the last row again at the end)
-    w.n0 = qn[0];
-    w.n1 = qn[1];
-    w.n2 = qn[2];
-    const uint32_t g = gray4(d0, d1, d2);
-    uint32_t gl = dpp_from_left(g), gr = dpp_from_right(g);
-    if (EDGE && w.left_edge) gl = g << 16;   // gray(-1) = gray(1)
-    if (EDGE && w.right_edge) gr = g >> 16;  // gray(W) = gray(W-2)
-    const Taps4 tp = taps4(gl, g, gr);
-    const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
-    const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
-    R.hba[S] = upk(o01);
-    R.hbb[S] = upk(o23);
+    uint32_t g[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) g[k] = gray4(w.nx[k][0], w.nx[k][1], w.nx[k][2]);
+    strip_load(w, i + 1 < H ? i + 1 : i);  // next row (the last row again at the end)
+    uint32_t gl = dpp_from_left(g[K - 1]), gr = dpp_from_right(g[0]);
+    if (EDGE && w.left_edge) gl = g[0] << 16;       // gray(-1) = gray(1)
+    if (EDGE && w.right_edge) gr = g[K - 1] >> 16;  // gray(W) = gray(W-2)
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const Taps4 tp = taps4(k ? g[k - 1] : gl, g[k], k + 1 < K ? g[k + 1] : gr);
+      const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
+      const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
+      R.hba[S][k] = upk(o01);
+      R.hbb[S][k] = upk(o23);
+    }
   } else if (ROWS && i == H) {  // row H = row H-2 (reflect), for the blur of row H-1
-    R.hba[S] = R.hba[S1];
-    R.hbb[S] = R.hbb[S1];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      R.hba[S][k] = R.hba[S1][k];
+      R.hbb[S][k] = R.hbb[S1][k];
+    }
   }
   // ---- vertical blur of row j = i - 1 (hblur rows j-1, j, j+1 = slots S1, S2, S)
   const int j = i - 1;
   if (!ROWS || (j >= 0 && j < H)) {
     const bool top = ROWS && j == 0;
-    const uint32_t aa = top ? R.hba[S] : R.hba[S1], ab = top ? R.hbb[S] : R.hbb[S1];  // row -1 = row 1
-    const uint32_t av[4] = {aa & 0xffffu, aa >> 16, ab & 0xffffu, ab >> 16};
-    const uint32_t bv[4] = {R.hba[S2] & 0xffffu, R.hba[S2] >> 16, R.hbb[S2] & 0xffffu, R.hbb[S2] >> 16};
-    const uint32_t cv[4] = {R.hba[S] & 0xffffu, R.hba[S] >> 16, R.hbb[S] & 0xffffu, R.hbb[S] >> 16};
-    uint32_t o = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t r = (84u * (av[k] + cv[k]) + 89u * bv[k] + (1u << 15)) >> 16;
-      o |= (r > 255u ? 255u : r) << (8 * k);
+    for (int k = 0; k < K; k++) {
+      const uint32_t aa = top ? R.hba[S][k] : R.hba[S1][k], ab = top ? R.hbb[S][k] : R.hbb[S1][k];  // row -1 = row 1
+      const uint32_t av[4] = {aa & 0xffffu, aa >> 16, ab & 0xffffu, ab >> 16};
+      const uint32_t bv[4] = {R.hba[S2][k] & 0xffffu, R.hba[S2][k] >> 16, R.hbb[S2][k] & 0xffffu, R.hbb[S2][k] >> 16};
+      const uint32_t cv[4] = {R.hba[S][k] & 0xffffu, R.hba[S][k] >> 16, R.hbb[S][k] & 0xffffu, R.hbb[S][k] >> 16};
+      uint32_t o = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t r = (84u * (av[b] + cv[b]) + 89u * bv[b] + (1u << 15)) >> 16;
+        o |= (r > 255u ? 255u : r) << (8 * b);
+      }
+      R.bl[S2][k] = o;
     }
-    R.bl[S2] = o;
   } else if (ROWS && j == H) {
-    R.bl[S2] = R.bl[S1];  // row H = row H-1 (replicate), for the Sobel of row H-1
+#pragma unroll
+    for (int k = 0; k < K; k++) R.bl[S2][k] = R.bl[S1][k];  // row H = row H-1 (replicate), for the Sobel of row H-1
   }
-  // ---- Sobel of row k = i - 2 (blur rows k-1, k, k+1 = slots S, S1, S2)
-  const int k = i - 2;
-  if (!ROWS || (k >= 0 && k < H)) {
-    const uint32_t a = ROWS && k == 0 ? R.bl[S1] : R.bl[S];  // row -1 = row 0
-    const uint32_t b = R.bl[S1], c = R.bl[S2];
-    const u16x2 A01 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c010c00u)), A23 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c030c02u));
-    const u16x2 B01 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c010c00u)), B23 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c030c02u));
-    const u16x2 C01 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c010c00u)), C23 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c030c02u));
-    const uint32_t vs01 = upk(A01 + C01 + B01 * two), vs23 = upk(A23 + C23 + B23 * two);
-    const uint32_t vd01 = upk(vpk<s16x2>(upk(C01)) - vpk<s16x2>(upk(A01)));
-    const uint32_t vd23 = upk(vpk<s16x2>(upk(C23)) - vpk<s16x2>(upk(A23)));
-    uint32_t VL = dpp_from_left(vs23), VR = dpp_from_right(vs01);
-    uint32_t DL = dpp_from_left(vd23), DR = dpp_from_right(vd01);
-    if (EDGE && w.left_edge) { VL = vs01 << 16; DL = vd01 << 16; }    // blur(-1) = blur(0)
-    if (EDGE && w.right_edge) { VR = vs23 >> 16; DR = vd23 >> 16; }   // blur(W) = blur(W-1)
-    const s16x2 S0v = vpk<s16x2>(__builtin_amdgcn_perm(vs01, VL, 0x05040302u));  // columns -1, 0
-    const s16x2 S1v = vpk<s16x2>(__builtin_amdgcn_perm(vs23, vs01, 0x05040302u)); // 1, 2
-    const s16x2 S2v = vpk<s16x2>(__builtin_amdgcn_perm(VR, vs23, 0x05040302u));   // 3, 4
-    const s16x2 D0 = vpk<s16x2>(__builtin_amdgcn_perm(vd01, DL, 0x05040302u));
-    const s16x2 D1 = vpk<s16x2>(__builtin_amdgcn_perm(vd23, vd01, 0x05040302u));
-    const s16x2 D2 = vpk<s16x2>(__builtin_amdgcn_perm(DR, vd23, 0x05040302u));
-    const s16x2 gx01 = S1v - S0v, gx23 = S2v - S1v;
-    const s16x2 gy01 = D0 + D1 + (vpk<s16x2>(vd01) << 1), gy23 = D1 + D2 + (vpk<s16x2>(vd23) << 1);
-    const s16x2 m01 = __builtin_elementwise_max(gx01, -gx01) + __builtin_elementwise_max(gy01, -gy01);
-    const s16x2 m23 = __builtin_elementwise_max(gx23, -gx23) + __builtin_elementwise_max(gy23, -gy23);
-    R.mga[S1] = upk(m01);
-    R.mgb[S1] = upk(m23);
-    R.gxa[S1] = upk(gx01);
-    R.gxb[S1] = upk(gx23);
-    R.gya[S1] = upk(gy01);
-    R.gyb[S1] = upk(gy23);
-  } else if (ROWS && k == H) {
-    R.mga[S1] = 0;  // magnitude below the frame: zero
-    R.mgb[S1] = 0;
+  // ---- Sobel of row m = i - 2 (blur rows m-1, m, m+1 = slots S, S1, S2)
+  const int m = i - 2;
+  if (!ROWS || (m >= 0 && m < H)) {
+    uint32_t vs01[K], vs23[K], vd01[K], vd23[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t a = ROWS && m == 0 ? R.bl[S1][k] : R.bl[S][k];  // row -1 = row 0
+      const uint32_t b = R.bl[S1][k], c = R.bl[S2][k];
+      const u16x2 A01 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c010c00u)), A23 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c030c02u));
+      const u16x2 B01 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c010c00u)), B23 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c030c02u));
+      const u16x2 C01 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c010c00u)), C23 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c030c02u));
+      vs01[k] = upk(A01 + C01 + B01 * two);
+      vs23[k] = upk(A23 + C23 + B23 * two);
+      vd01[k] = upk(vpk<s16x2>(upk(C01)) - vpk<s16x2>(upk(A01)));
+      vd23[k] = upk(vpk<s16x2>(upk(C23)) - vpk<s16x2>(upk(A23)));
+    }
+    uint32_t VL0 = dpp_from_left(vs23[K - 1]), VRK = dpp_from_right(vs01[0]);
+    uint32_t DL0 = dpp_from_left(vd23[K - 1]), DRK = dpp_from_right(vd01[0]);
+    if (EDGE && w.left_edge) { VL0 = vs01[0] << 16; DL0 = vd01[0] << 16; }                  // blur(-1) = blur(0)
+    if (EDGE && w.right_edge) { VRK = vs23[K - 1] >> 16; DRK = vd23[K - 1] >> 16; }        // blur(W) = blur(W-1)
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t VL = k ? vs23[k - 1] : VL0, VR = k + 1 < K ? vs01[k + 1] : VRK;
+      const uint32_t DL = k ? vd23[k - 1] : DL0, DR = k + 1 < K ? vd01[k + 1] : DRK;
+      const s16x2 S0v = vpk<s16x2>(__builtin_amdgcn_perm(vs01[k], VL, 0x05040302u));     // columns -1, 0
+      const s16x2 S1v = vpk<s16x2>(__builtin_amdgcn_perm(vs23[k], vs01[k], 0x05040302u)); // 1, 2
+      const s16x2 S2v = vpk<s16x2>(__builtin_amdgcn_perm(VR, vs23[k], 0x05040302u));      // 3, 4
+      const s16x2 D0 = vpk<s16x2>(__builtin_amdgcn_perm(vd01[k], DL, 0x05040302u));
+      const s16x2 D1 = vpk<s16x2>(__builtin_amdgcn_perm(vd23[k], vd01[k], 0x05040302u));
+      const s16x2 D2 = vpk<s16x2>(__builtin_amdgcn_perm(DR, vd23[k], 0x05040302u));
+      const s16x2 gx01 = S1v - S0v, gx23 = S2v - S1v;
+      const s16x2 gy01 = D0 + D1 + (vpk<s16x2>(vd01[k]) << 1), gy23 = D1 + D2 + (vpk<s16x2>(vd23[k]) << 1);
+      const s16x2 m01 = __builtin_elementwise_max(gx01, -gx01) + __builtin_elementwise_max(gy01, -gy01);
+      const s16x2 m23 = __builtin_elementwise_max(gx23, -gx23) + __builtin_elementwise_max(gy23, -gy23);
+      R.mga[S1][k] = upk(m01);
+      R.mgb[S1][k] = upk(m23);
+      R.gxa[S1][k] = upk(gx01);
+      R.gxb[S1][k] = upk(gx23);
+      R.gya[S1][k] = upk(gy01);
+      R.gyb[S1][k] = upk(gy23);
+    }
+  } else if (ROWS && m == H) {
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      R.mga[S1][k] = 0;  // magnitude below the frame: zero
+      R.mgb[S1][k] = 0;
+    }
   }
   // ---- NMS of row n = i - 3 (magnitude rows n-1, n, n+1 = slots S2, S, S1)
   const int n = i - 3;
   if (ROWS && n < 0) return;
   const bool first = ROWS && n == 0;
-  const uint32_t ua = first ? 0u : R.mga[S2], ub = first ? 0u : R.mgb[S2];  // magnitude above the frame: zero
-  uint32_t P[3][3], Cw[3][2];
-  const uint32_t rwa[3] = {ua, R.mga[S], R.mga[S1]}, rwb[3] = {ub, R.mgb[S], R.mgb[S1]};
+  uint32_t P[3][K][3], Cw[3][K][2];
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    uint32_t Lw = dpp_from_left(rwb[r]), Rw = dpp_from_right(rwa[r]);
-    if (EDGE && w.left_edge) Lw = 0u;
-    if (EDGE && w.right_edge) Rw = 0u;
-    Cw[r][0] = rwa[r];
-    Cw[r][1] = rwb[r];
-    P[r][0] = __builtin_amdgcn_perm(rwa[r], Lw, 0x05040302u);
-    P[r][1] = __builtin_amdgcn_perm(rwb[r], rwa[r], 0x05040302u);
-    P[r][2] = __builtin_amdgcn_perm(Rw, rwb[r], 0x05040302u);
-  }
-  uint32_t push[2], strong[2];
+    uint32_t rwa[K], rwb[K];
 #pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const uint32_t gxp = h ? R.gxb[S] : R.gxa[S], gyp = h ? R.gyb[S] : R.gya[S];
-    const s16x2 X = vpk<s16x2>(gxp), Y = vpk<s16x2>(gyp);
-    const s16x2 AX = __builtin_elementwise_max(X, -X), AY = __builtin_elementwise_max(Y, -Y);
-    const uint32_t ax = upk(AX), ay = upk(AY);
-    const int ax0 = (int)(ax & 0xffffu), ax1 = (int)(ax >> 16);
-    const int ay0 = (int)(ay & 0xffffu) << SHIFT, ay1 = (int)(ay >> 16) << SHIFT;
-    const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
-    const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
-    const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);
-    const uint32_t UL = P[0][h], U = Cw[0][h], UR = P[0][h + 1];
-    const uint32_t L = P[1][h], Mm = Cw[1][h], Rr = P[1][h + 1];
-    const uint32_t DLw = P[2][h], Dd = Cw[2][h], DRw = P[2][h + 1];
-    const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
-    const uint32_t B = (HOR & Rr) | (~HOR & ((VER & Dd) | (~VER & ((NEG & DLw) | (~NEG & DRw)))));
-    const s16x2 Ms = vpk<s16x2>(Mm);
-    const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
-    const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
-    const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
-    const uint32_t HV = HOR | VER;
-    const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
-    const uint32_t GTL = upk((w.LOW - Ms) >> 15);
-    push[h] = GTA & BC & GTL;
-    strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
+    for (int k = 0; k < K; k++) {
+      rwa[k] = r == 0 ? (first ? 0u : R.mga[S2][k]) : r == 1 ? R.mga[S][k] : R.mga[S1][k];  // above the frame: zero
+      rwb[k] = r == 0 ? (first ? 0u : R.mgb[S2][k]) : r == 1 ? R.mgb[S][k] : R.mgb[S1][k];
+    }
+    uint32_t Lw0 = dpp_from_left(rwb[K - 1]), RwK = dpp_from_right(rwa[0]);
+    if (EDGE && w.left_edge) Lw0 = 0u;
+    if (EDGE && w.right_edge) RwK = 0u;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t Lw = k ? rwb[k - 1] : Lw0, Rw = k + 1 < K ? rwa[k + 1] : RwK;
+      Cw[r][k][0] = rwa[k];
+      Cw[r][k][1] = rwb[k];
+      P[r][k][0] = __builtin_amdgcn_perm(rwa[k], Lw, 0x05040302u);
+      P[r][k][1] = __builtin_amdgcn_perm(rwb[k], rwa[k], 0x05040302u);
+      P[r][k][2] = __builtin_amdgcn_perm(Rw, rwb[k], 0x05040302u);
+    }
   }
-  // nibbles (pixel 2h + t <-> bit t of half h) into 32-bit words of 8 lanes
-  const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
-  const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
-  // (outside the frame: lanes past the last column group of an edge strip)
-  uint32_t cw = !EDGE || w.inside ? ((xp | (xp >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
-  uint32_t sw = !EDGE || w.inside ? ((xs | (xs >> 16)) & 0xfu) << (4 * (w.lane & 7)) : 0u;
+  uint32_t cw = 0, sw = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    uint32_t push[2], strong[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t gxp = h ? R.gxb[S][k] : R.gxa[S][k], gyp = h ? R.gyb[S][k] : R.gya[S][k];
+      const s16x2 X = vpk<s16x2>(gxp), Y = vpk<s16x2>(gyp);
+      const s16x2 AX = __builtin_elementwise_max(X, -X), AY = __builtin_elementwise_max(Y, -Y);
+      const uint32_t ax = upk(AX), ay = upk(AY);
+      const int ax0 = (int)(ax & 0xffffu), ax1 = (int)(ax >> 16);
+      const int ay0 = (int)(ay & 0xffffu) << SHIFT, ay1 = (int)(ay >> 16) << SHIFT;
+      const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
+      const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
+      const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);
+      const uint32_t UL = P[0][k][h], U = Cw[0][k][h], UR = P[0][k][h + 1];
+      const uint32_t L = P[1][k][h], Mm = Cw[1][k][h], Rr = P[1][k][h + 1];
+      const uint32_t DLw = P[2][k][h], Dd = Cw[2][k][h], DRw = P[2][k][h + 1];
+      const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
+      const uint32_t B = (HOR & Rr) | (~HOR & ((VER & Dd) | (~VER & ((NEG & DLw) | (~NEG & DRw)))));
+      const s16x2 Ms = vpk<s16x2>(Mm);
+      const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
+      const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
+      const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
+      const uint32_t HV = HOR | VER;
+      const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
+      const uint32_t GTL = upk((w.LOW - Ms) >> 15);
+      push[h] = GTA & BC & GTL;
+      strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
+    }
+    // nibble of group k (pixel 2h + t <-> bit t of half h)
+    const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
+    const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
+    cw |= ((xp | (xp >> 16)) & 0xfu) << (4 * k);
+    sw |= ((xs | (xs >> 16)) & 0xfu) << (4 * k);
+  }
+  // the lane's 4K bits into 32-bit words of 8 / K lanes (outside the frame:
+  // lanes past the last column group of an edge strip)
+  constexpr int LPW = StripGeom<K>::lanes_per_word;
+  const int sh = 4 * K * (w.lane & (LPW - 1));
+  cw = !EDGE || w.inside ? cw << sh : 0u;
+  sw = !EDGE || w.inside ? sw << sh : 0u;
   cw |= dpp_row_shr(cw, 1);
   sw |= dpp_row_shr(sw, 1);
   cw |= dpp_row_shr(cw, 2);
   sw |= dpp_row_shr(sw, 2);
-  cw |= dpp_row_shr(cw, 4);
-  sw |= dpp_row_shr(sw, 4);
+  if (LPW == 8) {
+    cw |= dpp_row_shr(cw, 4);
+    sw |= dpp_row_shr(sw, 4);
+  }
   if (w.store_lane) {
-    const uint32_t o = 4u * ((uint32_t)n * (uint32_t)w.WW + (uint32_t)(w.lane >> 3));  // byte offset
+    const uint32_t o = 4u * ((uint32_t)n * (uint32_t)w.WW + (uint32_t)(w.lane / LPW));  // byte offset
     *(uint32_t*)((char*)w.cb + o) = cw;
     *(uint32_t*)((char*)w.sbp + o) = sw;
   }
 }
 // rows 0 .. H+2 in triples (row i in slot i % 3): the first two triples and
 // the last ones with the row rules, the triples between without
-template <bool EDGE>
-__device__ __forceinline__ void strip_walk(StripWave& w, StripRegs& R) {
+template <int K, bool EDGE>
+__device__ __forceinline__ void strip_walk(StripWave<K>& w, StripRegs<K>& R) {
   const int rows = w.H + 3;
   int i = 0;
 #pragma unroll 1
   for (; i < 6 && i < rows; i += 3) {
-    strip_step<0, true, EDGE>(w, R, i);
-    if (i + 1 < rows) strip_step<1, true, EDGE>(w, R, i + 1);
-    if (i + 2 < rows) strip_step<2, true, EDGE>(w, R, i + 2);
+    strip_step<K, 0, true, EDGE>(w, R, i);
+    if (i + 1 < rows) strip_step<K, 1, true, EDGE>(w, R, i + 1);
+    if (i + 2 < rows) strip_step<K, 2, true, EDGE>(w, R, i + 2);
   }
 #pragma unroll 1
   for (; i + 2 < w.H; i += 3) {
-    strip_step<0, false, EDGE>(w, R, i);
-    strip_step<1, false, EDGE>(w, R, i + 1);
-    strip_step<2, false, EDGE>(w, R, i + 2);
+    strip_step<K, 0, false, EDGE>(w, R, i);
+    strip_step<K, 1, false, EDGE>(w, R, i + 1);
+    strip_step<K, 2, false, EDGE>(w, R, i + 2);
   }
 #pragma unroll 1
   for (; i < rows; i += 3) {
-    strip_step<0, true, EDGE>(w, R, i);
-    if (i + 1 < rows) strip_step<1, true, EDGE>(w, R, i + 1);
-    if (i + 2 < rows) strip_step<2, true, EDGE>(w, R, i + 2);
+    strip_step<K, 0, true, EDGE>(w, R, i);
+    if (i + 1 < rows) strip_step<K, 1, true, EDGE>(w, R, i + 1);
+    if (i + 2 < rows) strip_step<K, 2, true, EDGE>(w, R, i + 2);
   }
 }
-__global__ __launch_bounds__(256) void k_canny_strip(const FrameDesc* __restrict__ frames, int low, int high,
+// one wave per (frame, strip); needs W % (4K) == 0, W >= 8K, H >= 3
+template <int K>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 : MK_STRIP2_WAVES))) void k_canny_strip(const FrameDesc* __restrict__ frames, int low, int high,
                                                      uint32_t* __restrict__ cbits, uint32_t* __restrict__ sbits,
                                                      size_t bstride, int nstrip, int nwaves) {
   // the wave index is wave-uniform: frame fields and row conditions stay scalar
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wv >= nwaves) return;
-  StripWave w;
+  StripWave<K> w;
   w.lane = threadIdx.x & 63;
   const int f = wv / nstrip, sidx = wv - f * nstrip;
   const FrameDesc fd = frames[f];
   const int W = fd.w;
   w.H = fd.h;
   w.WW = bits::words(W);
-  const int base = sidx * kStripCols;
-  const int c0 = w.lane == 63 ? base - 4 : base + 4 * w.lane;      // this lane's first column
-  const int lc = c0 < 0 ? 0 : (c0 > W - 4 ? W - 4 : c0);            // loads stay inside the row
-  w.left_edge = c0 == 0;                                            // columns -1.. come from the border rules
-  w.right_edge = c0 == W - 4;
-  w.inside = c0 >= 0 && c0 <= W - 4;
+  constexpr int G = 4 * K;  // columns per lane
+  const int base = sidx * StripGeom<K>::cols;
+  const int c0 = w.lane == 63 ? base - G : base + G * w.lane;     // this lane's first column
+  const int lc = c0 < 0 ? 0 : (c0 > W - G ? W - G : c0);           // loads stay inside the row
+  w.left_edge = c0 == 0;                                           // columns -1.. come from the border rules
+  w.right_edge = c0 == W - G;
+  w.inside = c0 >= 0 && c0 <= W - G;
   const int lowc = low < -1 ? -1 : (low > 32767 ? 32767 : low);
   const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
   w.LOW = s16x2{(short)lowc, (short)lowc};
@@ -827,14 +895,13 @@ __global__ __launch_bounds__(256) void k_canny_strip(const FrameDesc* __restrict
   w.rstep = (uint32_t)W * 3u;
   w.cb = cbits + (size_t)f * bstride + (size_t)(base >> 5);
   w.sbp = sbits + (size_t)f * bstride + (size_t)(base >> 5);
-  w.store_lane = (w.lane & 7) == 7 && w.lane < 56 && base + 4 * (w.lane & ~7) < W;
-  StripRegs R = {};
-  gu32* q = gwords(w.bgr + w.loff);
-  w.n0 = q[0];
-  w.n1 = q[1];
-  w.n2 = q[2];
-  if (sidx == 0 || sidx == nstrip - 1) strip_walk<true>(w, R);
-  else strip_walk<false>(w, R);
+  constexpr int LPW = StripGeom<K>::lanes_per_word;
+  w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes &&
+                 base + G * (w.lane & ~(LPW - 1)) < W;
+  StripRegs<K> R = {};
+  strip_load(w, 0);
+  if (sidx == 0 || sidx == nstrip - 1) strip_walk<K, true>(w, R);
+  else strip_walk<K, false>(w, R);
 }
 
 // ------------------------------------------------ hysteresis: run CCL

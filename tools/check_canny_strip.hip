@@ -37,27 +37,28 @@ static int time_mode(int N) {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
-  const int ns = (W + kStripCols - 1) / kStripCols;
-  for (int kind = 0; kind < 2; kind++) {
+  const int ns1 = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols, ns2 = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols;
+  for (int kind = 0; kind < 3; kind++) {
     float best = 1e9f;
     for (int r = 0; r < 5; r++) {
       hipEventRecord(e0);
       if (kind == 0) k_canny<<<tgx * tgy * N, 256>>>(dfd, 30, 90, 1, c, s, B, tgx, tgy);
-      else k_canny_strip<<<(ns * N + 3) / 4, 256>>>(dfd, 30, 90, c, s, B, ns, ns * N);
+      else if (kind == 1) k_canny_strip<1><<<(ns1 * N + 3) / 4, 256>>>(dfd, 30, 90, c, s, B, ns1, ns1 * N);
+      else k_canny_strip<2><<<(ns2 * N + 3) / 4, 256>>>(dfd, 30, 90, c, s, B, ns2, ns2 * N);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
       hipEventElapsedTime(&ms, e0, e1);
       best = ms < best ? ms : best;
     }
-    printf("%s: %d frames %.3f ms (%.3f ms per 4096 frames)\n", kind ? "k_canny_strip" : "k_canny", N, best, best * 4096.0 / N);
+    printf("%s: %d frames %.3f ms (%.3f ms per 4096 frames)\n", kind == 2 ? "k_canny_strip<2>" : kind ? "k_canny_strip<1>" : "k_canny", N, best, best * 4096.0 / N);
   }
   return 0;
 }
 
 int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[1]) == "time") return time_mode(std::atoi(argv[2]));
-  const int sizes[][2] = {{1280, 720}, {640, 480}, {1000, 611}, {232, 40}, {8, 3}, {448, 17}};
+  const int sizes[][2] = {{1280, 720}, {640, 480}, {1000, 611}, {232, 40}, {8, 3}, {448, 17}, {1284, 33}, {16, 3}, {24, 5}, {488, 9}};
   int fails = 0;
   std::mt19937 rng(5);
   for (auto& sz : sizes) {
@@ -87,30 +88,39 @@ int main(int argc, char** argv) {
       const size_t B = (size_t)WW * H;
       uint32_t *c1, *s1, *c2, *s2;
       hipMalloc(&c1, B * 4); hipMalloc(&s1, B * 4); hipMalloc(&c2, B * 4); hipMalloc(&s2, B * 4);
-      hipMemset(c1, 0, B * 4); hipMemset(s1, 0, B * 4); hipMemset(c2, 0xff, B * 4); hipMemset(s2, 0xff, B * 4);
+      hipMemset(c1, 0, B * 4); hipMemset(s1, 0, B * 4);
       const int low = 30, high = 90;
       const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
       k_canny<<<tgx * tgy, 256>>>(dfd, low, high, 1, c1, s1, B, tgx, tgy);
-      const int ns = (W + kStripCols - 1) / kStripCols;
-      k_canny_strip<<<(ns + 3) / 4, 256>>>(dfd, low, high, c2, s2, B, ns, ns);
       std::vector<uint32_t> h1(B), h2(B), g1(B), g2(B);
       hipMemcpy(h1.data(), c1, B * 4, hipMemcpyDeviceToHost);
-      hipMemcpy(h2.data(), c2, B * 4, hipMemcpyDeviceToHost);
       hipMemcpy(g1.data(), s1, B * 4, hipMemcpyDeviceToHost);
-      hipMemcpy(g2.data(), s2, B * 4, hipMemcpyDeviceToHost);
-      int bad = 0;
-      for (int y = 0; y < H; y++)
-        for (int x = 0; x < W; x++) {
-          const size_t w = (size_t)y * WW + (x >> 5);
-          const int b = x & 31;
-          const int a1 = (h1[w] >> b) & 1, a2 = (h2[w] >> b) & 1, t1 = (g1[w] >> b) & 1, t2 = (g2[w] >> b) & 1;
-          if (a1 != a2 || t1 != t2) {
-            if (bad < 8) printf("  %dx%d kind %d: (%d, %d) cand %d/%d strong %d/%d\n", W, H, kind, x, y, a1, a2, t1, t2);
-            bad++;
-          }
+      for (int K = 1; K <= 2; K++) {
+        if (K == 2 && (W % 8 != 0 || W < 16)) continue;
+        hipMemset(c2, 0xff, B * 4); hipMemset(s2, 0xff, B * 4);
+        if (K == 1) {
+          const int ns = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols;
+          k_canny_strip<1><<<(ns + 3) / 4, 256>>>(dfd, low, high, c2, s2, B, ns, ns);
+        } else {
+          const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols;
+          k_canny_strip<2><<<(ns + 3) / 4, 256>>>(dfd, low, high, c2, s2, B, ns, ns);
         }
-      printf("%dx%d kind %d: %d pixel mismatches\n", W, H, kind, bad);
-      fails += bad != 0;
+        hipMemcpy(h2.data(), c2, B * 4, hipMemcpyDeviceToHost);
+        hipMemcpy(g2.data(), s2, B * 4, hipMemcpyDeviceToHost);
+        int bad = 0;
+        for (int y = 0; y < H; y++)
+          for (int x = 0; x < W; x++) {
+            const size_t w = (size_t)y * WW + (x >> 5);
+            const int b = x & 31;
+            const int a1 = (h1[w] >> b) & 1, a2 = (h2[w] >> b) & 1, t1 = (g1[w] >> b) & 1, t2 = (g2[w] >> b) & 1;
+            if (a1 != a2 || t1 != t2) {
+              if (bad < 8) printf("  %dx%d kind %d K %d: (%d, %d) cand %d/%d strong %d/%d\n", W, H, kind, K, x, y, a1, a2, t1, t2);
+              bad++;
+            }
+          }
+        printf("%dx%d kind %d K %d: %d pixel mismatches\n", W, H, kind, K, bad);
+        fails += bad != 0;
+      }
       hipFree(dimg); hipFree(dfd); hipFree(c1); hipFree(s1); hipFree(c2); hipFree(s2);
     }
   }
