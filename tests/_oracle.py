@@ -1,8 +1,8 @@
 """ctypes bindings for the ORACLE (test infrastructure only).
 
 Loads oracle/liboracle.so (CPU restatement of the reference mantis3 path) and,
-when present, oracle/_ref/libref_rpp.so (the reference's own RPP.cpp/Rpoly.cpp
-compiled in place against oracle/refshim).  Only tests/, __graft_entry__.smoke()
+when present, oracle/_ref/libref_rpoly.so (the reference's own Rpoly.cpp
+compiled in place; RPP.cpp needs OpenCV and is not built).  Only tests/, __graft_entry__.smoke()
 and bench.py's cpu_baseline use this module.
 """
 import ctypes as C
@@ -12,7 +12,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.environ.get("MANTIS_ORACLE_SO") or os.path.join(ROOT, "oracle", "liboracle.so")  # make sanitize: instrumented build
-REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_rpp.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_rpoly.so")
 
 ORC_MAX_QUADS = 256
 ORC_MAX_HYPS = 1024
@@ -82,11 +82,10 @@ def lib():
 
 
 def ref():
-    """The reference's own RPP/Rpoly (None when oracle/_ref was not built)."""
+    """The reference's own Rpoly (None when oracle/_ref was not built)."""
     global _ref
     if _ref is None and os.path.exists(REF_SO):
         R = C.CDLL(REF_SO)
-        R.ref_rpp.restype = C.c_int
         R.ref_rpoly.restype = C.c_int
         _ref = R
     return _ref
@@ -104,18 +103,6 @@ def rpp(model, iprts):
     st = lib().orc_rpp(_p(model, C.c_double), _p(iprts, C.c_double), n, _p(R, C.c_double), _p(t, C.c_double),
                        _p(e, C.c_double), C.byref(code))
     return st, R.reshape(3, 3), t, e, code.value
-
-
-def ref_rpp(model, iprts):
-    model = np.ascontiguousarray(model, np.float64)
-    iprts = np.ascontiguousarray(iprts, np.float64)
-    n = model.shape[1]
-    R = np.zeros(9)
-    t = np.zeros(3)
-    e = np.zeros(3)
-    st = ref().ref_rpp(_p(model, C.c_double), _p(iprts, C.c_double), C.c_int(n), _p(R, C.c_double),
-                       _p(t, C.c_double), _p(e, C.c_double))
-    return st, R.reshape(3, 3), t, e
 
 
 def rpoly(coef, ref_impl=False):

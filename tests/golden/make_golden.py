@@ -2,19 +2,21 @@
 """Generate the committed golden fixtures under tests/golden/.
 
 Run in the build container (it needs /root/reference for the in-place
-reference build and for test/grid1.jpg):
+Rpoly.cpp build and for test/grid1.jpg):
 
     make oracle ref && python tests/golden/make_golden.py
 
 Fixtures (data only — inputs and expected outputs):
-  rpp_golden.npz    4-point RPP problems -> outputs of the REFERENCE's own
-                    RPP.cpp/Rpoly.cpp (oracle/_ref/libref_rpp.so). Cases:
+  rpp_golden.npz    4-point RPP problems -> outputs of the ORACLE's RPP
+                    restatement (oracle/o_rpp.cpp; RPP.cpp itself needs
+                    OpenCV and is unbuildable here, so these are regression
+                    fixtures: the RPP pin is demo.cpp's known answer). Cases:
                     test/unit_test.cpp:144-203 (fisheye PnP, cv::RNG(10)
                     sigma 0.01 corner noise, GCC right-to-left draw order),
                     test/legacy/unit_test.cpp:49-76 (pinhole square), and
                     seeded random squares seen by a nadir-ish camera.
-  rpp_faults.npz    degenerate 4-point RPP problems -> the REFERENCE's outputs
-                    (same build): image points whose mean ray is the optical
+  rpp_faults.npz    degenerate 4-point RPP problems -> the ORACLE's outputs
+                    (regression fixtures, as above): image points whose mean ray is the optical
                     axis (a centred symmetric square), collinear, pairwise
                     repeated and coincident points -- Rpp() returns false there
                     (no 2nd-pose candidate: DecomposeR / RpyAng_X fail,
@@ -23,9 +25,10 @@ Fixtures (data only — inputs and expected outputs):
                     GetRotationbyVector, RPP.cpp:450-453, needs a mean ray the
                     rotation cannot map back; no image points with z = 1 reach
                     it -- tests/test_oracle_pins.py searches for it.)
-  rpp_demo.npz      demo.cpp:17-38 10-point problem -> reference output
-                    (plus the Matlab answer quoted in demo.cpp:28-38).
-  rpoly_golden.npz  quartics -> reference rpoly_ak1 roots (5 slots).
+  rpp_demo.npz      demo.cpp:17-38 10-point problem -> the oracle's output
+                    plus the Matlab answer quoted in demo.cpp:28-38 (the pin).
+  rpoly_golden.npz  quartics -> the REFERENCE's own rpoly_ak1 roots (5 slots;
+                    Rpoly.cpp compiled in place, oracle/_ref/libref_rpoly.so).
   grid1.npz         test/grid1.jpg decoded to BGR (PIL) + config-1 K/D, and
                     the ORACLE's quad corners / publish decision for it
                     (a plumbing golden: the reference itself cannot run here).
@@ -55,7 +58,7 @@ def rodrigues(rv):
 
 
 def ref_case(model, ip):
-    st, R, t, e = O.ref_rpp(model, ip)
+    st, R, t, e, _code = O.rpp(model, ip)
     return st, R, t, e
 
 
@@ -205,7 +208,7 @@ def grid1_case():
 
 def main():
     if O.ref() is None:
-        sys.exit("oracle/_ref/libref_rpp.so missing: run `make ref` first")
+        sys.exit("oracle/_ref/libref_rpoly.so missing: run `make ref` first")
     only = sys.argv[1:]  # e.g. `make_golden.py rpp_faults`: regenerate those fixtures only
     if only:
         for name in only:

@@ -647,7 +647,7 @@ def test_dense_batch_matches_per_frame(m720, landmark_map):
 
 def test_rpp_fault_golden_on_gpu(m720):
     """Fault injection, RPP: the degenerate problems of
-    tests/golden/rpp_faults.npz (outputs of the reference's own RPP.cpp) through
+    tests/golden/rpp_faults.npz (regression outputs of the oracle's RPP restatement) through
     the device RPP (mantis_rpp_batch): status 0 where Rpp() returns false (no
     2nd-pose candidate: the first ObjPose's pose is kept, RPP.cpp:13-64) and the
     reference's R, t and errors."""
