@@ -29,3 +29,10 @@ if [ "$PART" = "b" ]; then
     grep '^{' $O/bench_c$leg.log | tail -1 > $O/bench_c$leg.json; cut -c1-160 $O/bench_c$leg.json
   done
 fi
+if [ "$PART" = "c" ] || [ "$PART" = "b" ]; then
+  # one context: the kernels' own durations without the other contexts' blocks
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$R/$O/prof_c1" -o run -- python3 "$R/bench.py" --no-cpu --contexts 1 --steps 3 --warmup 1 --latency-iters 3 --ingest-steps 0 > "$R/$O/prof_c1.log" 2>&1) || { echo prof c1 failed; tail -5 $O/prof_c1.log; exit 1; }
+  python3 tools/prof_summary.py $O/prof_c1 $O/rocprof_stats_c1.md > /dev/null
+  python3 tools/kern_avg.py $O/prof_c1/run_kernel_trace.csv 40 $O/batch_launch_avg_c1.json > $O/batch_launch_avg_c1.txt
+  head -30 $O/batch_launch_avg_c1.txt
+fi

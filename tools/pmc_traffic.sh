@@ -13,7 +13,7 @@ python3 - "$R/gpurun_out" <<'P'
 import csv, glob, json, sys
 FR = 256
 kern = {"canny_nms": ["k_canny_strip", "k_canny"], "hysteresis": ["k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"]}
-out = {"stage": "canny_nms", "kernel": "k_canny", "frames_per_launch": FR}
+out = {"stage": "canny_nms", "kernel": "k_canny_strip", "frames_per_launch": FR}
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     f = glob.glob(f"{sys.argv[1]}/pmc_{c}/**/*counter_collection.csv", recursive=True)[0]
@@ -21,7 +21,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for stage, names in kern.items():
         tot = 0.0
         for k in names:
-            sel = [r for r in rows if r["Kernel_Name"].split("(")[0] == "mk::" + k]
+            sel = [r for r in rows if r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0] == "mk::" + k]
             if not sel:
                 continue
             g = max(int(r["Grid_Size"]) for r in sel)
@@ -38,7 +38,7 @@ out.update(per)
 out["canny_nms_hbm_bytes_per_frame"] = 2 * per["canny_nms_FETCH_SIZE_bytes_per_frame"] + per["canny_nms_WRITE_SIZE_bytes_per_frame"]
 out["hysteresis_hbm_bytes_per_frame"] = 2 * per["hysteresis_FETCH_SIZE_bytes_per_frame"] + per["hysteresis_WRITE_SIZE_bytes_per_frame"]
 out["hbm_bytes_per_frame"] = out["canny_nms_hbm_bytes_per_frame"]
-out["note"] = ("per 1280x720 frame; k_canny: FETCH_SIZE x 2 (calibrated on its 12-byte reads, tools/pmc_calib.hip) "
+out["note"] = ("per 1280x720 frame; k_canny_strip: FETCH_SIZE x 2 (calibrated on 12-byte reads, tools/pmc_calib.hip; the strip kernel reads 12 bytes per column group) "
                "+ WRITE_SIZE (= the 2 x W H / 8 bit-plane bytes); hysteresis: FETCH_SIZE x 2 + WRITE_SIZE "
                "(its access widths uncalibrated); algorithmic k_canny bytes: 3 W H + W H / 4 = 2,995,200")
 json.dump(out, open(f"{sys.argv[1]}/pmc_traffic.json", "w"), indent=1)

@@ -22,7 +22,7 @@ def main(d, steps=None):
         g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, g))
     ev.sort()
-    canny = [e for e in ev if e[2] == "mk::k_canny"]
+    canny = [e for e in ev if e[2] in ("mk::k_canny", "mk::k_canny_strip")]
     gmax = max(e[3] for e in canny)
     big = [e for e in canny if e[3] == gmax]
     k = steps if steps else max(1, len(big) // 2)
