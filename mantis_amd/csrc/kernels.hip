@@ -2458,27 +2458,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
   if (tid == 0) st[f].ticks[k] = (int32_t)(wall_clock64() - t0);
   if (tid == 0) { nraw = 0; total = 0; nlong = 0; nchunk = st[f].n_chunks; }
   __syncthreads();
-  MK_TICK(0);
+
   const int max_chunks = pool_cap / kChunk;
   int32_t* chunks = sc;                              // [0, 2 pool_cap), filled by k_trace_borders
   int32_t* owner = sc + 2 * (size_t)pool_cap;        // [2 pool_cap, + max_chunks)
   int32_t* ordv = owner + max_chunks;
-  MK_TICK(1);
-  // 2. exclusive scan of the point counts, blockDim at a time
-  for (int base = 0; base < nb; base += blockDim.x) {
-    int i = base + tid;
-    int v = i < nb ? cnt[i] : 0;
-    scan[tid] = v;
-    __syncthreads();
-    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-      int t = tid >= o ? scan[tid - o] : 0;
+
+  // 2. exclusive scan of the point counts, blockDim at a time: wave scans,
+  // then the wave totals (two barriers per chunk; the running total is kept
+  // by every thread in a register)
+  {
+    const int lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+    int run = 0;
+    for (int base = 0; base < nb; base += blockDim.x) {
+      const int i = base + tid;
+      const int v = i < nb ? cnt[i] : 0;
+      const int inc = wave_incl_scan(v, lane);
+      if (lane == 63) scan[wv] = inc;
       __syncthreads();
-      scan[tid] += t;
+      int pre = 0, tot = 0;
+      for (int k = 0; k < nwv; k++) {
+        const int s = scan[k];
+        pre += k < wv ? s : 0;
+        tot += s;
+      }
+      if (i < nb) off[i] = run + pre + inc - v;
+      run += tot;
       __syncthreads();
     }
-    if (i < nb) off[i] = total + scan[tid] - v;
-    __syncthreads();
-    if (tid == blockDim.x - 1) total += scan[tid];
+    if (tid == 0) total = run;
     __syncthreads();
   }
   if (total > pool_cap || nchunk > max_chunks) {
@@ -2490,7 +2498,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     }
     return;
   }
-  MK_TICK(2);
+  MK_TICK(0);  // scan
   // 3. compact: 64 / kChunk chunks per wave, one lane per point
   {
     constexpr int CPW = 64 / kChunk;
@@ -2509,34 +2517,110 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     }
   }
   __syncthreads();
-  MK_TICK(3);
+  MK_TICK(1);  // compaction
   // 4. approxPolyDP per border (eps = POLYGON_EPSILON, closed, quad early
-  // exit); long borders are deferred to whole waves
-  for (int i = tid; i < nb; i += blockDim.x) {
-    const int o = off[i], c = cnt[i];
-    if (c > kLongBorder) {
-      const int k = atomicAdd(&nlong, 1);
-      if (k < kMaxLong) { longs[k] = i; continue; }
-    }
-    int32_t* dst = sc + 4 * (size_t)o;
-    int32_t* stk = dst + 2 * (size_t)c;
-    int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
-    if (m == 4) emit_raw(i, dst);
-  }
+  // exit). Borders longer than kLongBorder points take a whole wave
+  // (approx_poly_wave); the others one lane each, ordered by length (counting
+  // sort on count / 4, longest first) so the 64 lanes of a wave trip walk
+  // borders of about one length instead of idling behind the longest of a
+  // random 64 (DP per lane is a serial loop; a trip lasts its longest lane).
+  // Waves take the long borders first, then 64 short ones at a time, from LDS
+  // counters. The result does not depend on the order: emit_raw's slots are
+  // re-ordered by CCOMP key below.
+  __shared__ int32_t hist[33], nshort, next_long, next_short;
+  if (tid < 33) hist[tid] = 0;
+  if (tid == 0) { next_long = 0; next_short = 0; }
   __syncthreads();
-  {
-    const int wave = tid >> 6, nwaves = blockDim.x >> 6;
-    const int nl = nlong < kMaxLong ? nlong : kMaxLong;
-    for (int k = wave; k < nl; k += nwaves) {
-      const int i = longs[k], o = off[i], c = cnt[i];
+  bool sorted = nb <= 1024;  // the order lives in scan[] (free after step 2)
+  if (sorted) {
+    for (int i = tid; i < nb; i += blockDim.x) {
+      const int c = cnt[i];
+      if (c > kLongBorder) {
+        const int k = atomicAdd(&nlong, 1);
+        if (k < kMaxLong) longs[k] = i;
+      } else {
+        atomicAdd(&hist[c >> 2], 1);
+      }
+    }
+    __syncthreads();
+    sorted = nlong <= kMaxLong;
+    if (sorted) {
+      if (tid == 0) {
+        int acc = 0;
+        for (int b = 32; b >= 0; b--) {
+          const int h = hist[b];
+          hist[b] = acc;
+          acc += h;
+        }
+        nshort = acc;
+      }
+      __syncthreads();
+      for (int i = tid; i < nb; i += blockDim.x) {
+        const int c = cnt[i];
+        if (c <= kLongBorder) scan[atomicAdd(&hist[c >> 2], 1)] = i;
+      }
+      __syncthreads();
+      const int lane = tid & 63;
+      for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&next_long, 1);
+        k = __shfl(k, 0);
+        if (k >= nlong) break;
+        const int i = longs[k], o = off[i], c = cnt[i];
+        int32_t* dst = sc + 4 * (size_t)o;
+        int32_t* stk = dst + 2 * (size_t)c;
+        const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
+        if (m == 4 && lane == 0) emit_raw(i, dst);
+      }
+      for (;;) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&next_short, 64);
+        k = __shfl(k, 0);
+        if (k >= nshort) break;
+        if (k + lane < nshort) {
+          const int i = scan[k + lane], o = off[i], c = cnt[i];
+          int32_t* dst = sc + 4 * (size_t)o;
+          int32_t* stk = dst + 2 * (size_t)c;
+          const int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
+          if (m == 4) emit_raw(i, dst);
+        }
+      }
+      __syncthreads();
+      MK_TICK(2);  // approx (sorted)
+    } else {
+      __syncthreads();
+      if (tid == 0) nlong = 0;
+      __syncthreads();
+    }
+  }
+  if (!sorted) {  // more than 1024 borders or kMaxLong long ones: borders in index order
+    for (int i = tid; i < nb; i += blockDim.x) {
+      const int o = off[i], c = cnt[i];
+      if (c > kLongBorder) {
+        const int k = atomicAdd(&nlong, 1);
+        if (k < kMaxLong) { longs[k] = i; continue; }
+      }
       int32_t* dst = sc + 4 * (size_t)o;
       int32_t* stk = dst + 2 * (size_t)c;
-      const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
-      if (m == 4 && (tid & 63) == 0) emit_raw(i, dst);
+      int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
+      if (m == 4) emit_raw(i, dst);
+    }
+    __syncthreads();
+    MK_TICK(2);  // short-border approx (threads)
+    {
+      const int wave = tid >> 6, nwaves = blockDim.x >> 6;
+      const int nl = nlong < kMaxLong ? nlong : kMaxLong;
+      for (int k = wave; k < nl; k += nwaves) {
+        const int i = longs[k], o = off[i], c = cnt[i];
+        int32_t* dst = sc + 4 * (size_t)o;
+        int32_t* stk = dst + 2 * (size_t)c;
+        const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
+        if (m == 4 && (tid & 63) == 0) emit_raw(i, dst);
+      }
     }
   }
   __syncthreads();
-  MK_TICK(4);
+  MK_TICK(3);  // long-border approx (waves)
   const int nq = nraw < kMaxQuads ? nraw : kMaxQuads;
   // position in the CCOMP output order (keys are distinct)
   for (int i = tid; i < nq; i += blockDim.x) {
@@ -2602,6 +2686,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     dbg[f].n_quads = n;
   }
   __syncthreads();
+  MK_TICK(4);  // CCOMP order, duplicates
   const FrameDesc fd = frames[f];
   for (int r = tid; r < nq; r += blockDim.x) {
     int k = kpos[r];
@@ -2624,7 +2709,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     for (int c = 0; c < 8; c++) { dbg[f].quads[k][c] = q.c[c]; dbg[f].test_pts[k][c] = q.tp[c]; }
   }
   __syncthreads();
-  MK_TICK(5);
+  MK_TICK(5);  // end
 #undef MK_TICK
 }
 

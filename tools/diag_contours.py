@@ -39,7 +39,7 @@ print("longest walk steps mean", C[:, 18].mean(), "max", C[:, 18].max())
 for j, nm in enumerate(names):
     print(f"{nm:8s} mean {C[:, j].mean():10.1f} max {C[:, j].max()}")
 T = C[:, 10:16].astype(float) * 0.01  # us
-ph = ["bitmap", "trace0", "scan", "trace1", "approx", "rest"]
+ph = ["scan", "compact", "approx_short", "approx_long", "dedup", "rest"]
 prev = np.zeros(n)
 for j, nm in enumerate(ph):
     d = T[:, j] - prev
