@@ -1810,7 +1810,11 @@ __device__ inline bool ccomp_before(int pa, int ha, int ka, int pb, int hb, int 
   return ka > kb;
 }
 
-constexpr int kLongBorder = 128;  // points; longer borders get a whole wave for approxPolyDP
+#ifndef MK_LONG_BORDER
+#define MK_LONG_BORDER 128
+#endif
+constexpr int kLongBorder = MK_LONG_BORDER;  // points; longer borders get a whole wave for approxPolyDP
+static_assert(kLongBorder <= 128, "k_frame_contours' length buckets (count / 4) hold counts up to 128");
 constexpr int kMaxLong = 512;
 
 struct RawQuad {
@@ -2499,21 +2503,33 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     return;
   }
   MK_TICK(0);  // scan
-  // 3. compact: 64 / kChunk chunks per wave, one lane per point
-  {
-    constexpr int CPW = 64 / kChunk;
+  // 3. compact: 64 / kChunk chunks per wave, one lane per point, kCU wave
+  // trips at once: every load of the kCU trips is issued (at a clamped, valid
+  // chunk) before any is used, so a trip's chain (chunk count / owner / order,
+  // then the border's offset, then the store) costs one round trip per kCU
+  // trips instead of per trip
+  if (nchunk > 0) {
+    constexpr int CPW = 64 / kChunk, kCU = 4;
     const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
     const int32_t* ccount = ordv + max_chunks;
     const int l = lane % kChunk;
-    for (int c0 = wave * CPW; c0 < nchunk; c0 += nwaves * CPW) {
-      const int c = c0 + lane / kChunk;
-      if (c < nchunk && l < ccount[c]) {
-        const int b = owner[c], k = ordv[c] + l;
-        const int32_t* sp = chunks + 2 * ((size_t)c * kChunk + l);
-        int32_t* dp = pl + 2 * ((size_t)off[b] + k);
-        dp[0] = sp[0];
-        dp[1] = sp[1];
+    typedef __attribute__((aligned(8))) int2 pt2;
+    for (int c0 = wave * CPW * kCU; c0 < nchunk; c0 += nwaves * CPW * kCU) {
+      int cc[kCU], b[kCU], k[kCU], o[kCU];
+      pt2 v[kCU];
+#pragma unroll
+      for (int u = 0; u < kCU; u++) {
+        const int c = min(c0 + u * CPW + lane / kChunk, nchunk - 1);
+        cc[u] = c0 + u * CPW + lane / kChunk < nchunk ? ccount[c] : 0;
+        b[u] = owner[c];
+        k[u] = ordv[c] + l;
+        v[u] = *(const pt2*)(chunks + 2 * ((size_t)c * kChunk + l));
       }
+#pragma unroll
+      for (int u = 0; u < kCU; u++) o[u] = off[b[u]];
+#pragma unroll
+      for (int u = 0; u < kCU; u++)
+        if (l < cc[u]) *(pt2*)(pl + 2 * ((size_t)o[u] + k[u])) = v[u];
     }
   }
   __syncthreads();
