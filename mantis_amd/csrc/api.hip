@@ -410,7 +410,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   const size_t P = c->plane;
   const int Wp = W + 2, Hp = H + 2;
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
-  dim3 grow((Hp + 3) / 4, n);
+  dim3 grow((Hp + 4 * RUN_RPW - 1) / (4 * RUN_RPW), n);  // k_run_count / emit / border: RUN_RPW rows per wave
   uint16_t* rx = c->d_lroot;  // free after hysteresis: run starts (u16, one run per pixel at most)
   k_run_count<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, Wp, Hp);
   k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);

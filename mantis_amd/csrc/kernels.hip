@@ -1438,17 +1438,26 @@ __device__ inline uint32_t run_starts(const uint32_t* row, int w) {
   return cur ^ ((cur << 1) | (prv >> 31));
 }
 
+// The per-row kernels of the run CCL (count, emit, border) take RUN_RPW rows
+// per wave (a block = 4 waves = 4 RUN_RPW rows): a row is a few dozen runs,
+// so with one row per wave the grid was 181 blocks per 720p frame (741k per
+// 4096-frame batch) and the launches were bound by workgroup dispatch
+#ifndef MK_RUN_RPW
+#define MK_RUN_RPW 8
+#endif
+constexpr int RUN_RPW = MK_RUN_RPW;
 __global__ __launch_bounds__(256) void k_run_count(const uint32_t* __restrict__ dbits, size_t dstride,
                                                    int32_t* __restrict__ rowb, size_t rstride, int Wp, int Hp) {
-  const int f = blockIdx.y;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (y >= Hp) return;
-  const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+  const int f = blockIdx.y, lane = threadIdx.x & 63;
+  const int ya = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN_RPW, yb = min(ya + RUN_RPW, Hp);
   const int nw = (Wp + 31) / 32;
-  int c = 0;
-  for (int w = lane; w < nw; w += 64) c += __popc(run_starts(row, w));
-  c = wave_sum(c);
-  if (lane == 0) rowb[(size_t)f * rstride + y] = c + 1;
+  for (int y = ya; y < yb; y++) {
+    const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+    int c = 0;
+    for (int w = lane; w < nw; w += 64) c += __popc(run_starts(row, w));
+    c = wave_sum(c);
+    if (lane == 0) rowb[(size_t)f * rstride + y] = c + 1;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_run_scan(int32_t* __restrict__ rowb, size_t rstride, FrameState* st,
@@ -1482,30 +1491,31 @@ __global__ __launch_bounds__(256) void k_run_emit(const uint32_t* __restrict__ d
                                                   const int32_t* __restrict__ rowb, size_t rstride,
                                                   uint16_t* __restrict__ rx, int32_t* __restrict__ lab, size_t plane,
                                                   int Wp, int Hp) {
-  const int f = blockIdx.y;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (y >= Hp) return;
-  const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+  const int f = blockIdx.y, lane = threadIdx.x & 63;
+  const int ya = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN_RPW, yb = min(ya + RUN_RPW, Hp);
   uint16_t* X = rx + (size_t)f * plane;
   int32_t* L = lab + (size_t)f * plane;
   const int nw = (Wp + 31) / 32;
-  int base = rowb[(size_t)f * rstride + y];
-  if (lane == 0) { X[base] = 0; L[base] = base; }
-  base++;
-  for (int w0 = 0; w0 < nw; w0 += 64) {
-    const int w = w0 + lane;
-    uint32_t T = w < nw ? run_starts(row, w) : 0u;
-    const int c = __popc(T);
-    const int inc = wave_incl_scan(c, lane);
-    int o = base + inc - c;
-    while (T) {
-      const int b = __ffs(T) - 1;
-      T &= T - 1;
-      X[o] = (uint16_t)(32 * w + b);
-      L[o] = o;
-      o++;
+  for (int y = ya; y < yb; y++) {
+    const uint32_t* row = dbits + (size_t)f * dstride + (size_t)y * dbits_wpw(Wp);
+    int base = rowb[(size_t)f * rstride + y];
+    if (lane == 0) { X[base] = 0; L[base] = base; }
+    base++;
+    for (int w0 = 0; w0 < nw; w0 += 64) {
+      const int w = w0 + lane;
+      uint32_t T = w < nw ? run_starts(row, w) : 0u;
+      const int c = __popc(T);
+      const int inc = wave_incl_scan(c, lane);
+      int o = base + inc - c;
+      while (T) {
+        const int b = __ffs(T) - 1;
+        T &= T - 1;
+        X[o] = (uint16_t)(32 * w + b);
+        L[o] = o;
+        o++;
+      }
+      base += __shfl(inc, 63);
     }
-    base += __shfl(inc, 63);
   }
 }
 
@@ -1613,12 +1623,12 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
                                                     const uint16_t* __restrict__ rx, int32_t* lab, size_t plane,
                                                     Border* __restrict__ borders, FrameState* st, int Wp, int Hp,
                                                     int cap) {
-  const int f = blockIdx.y;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (y >= Hp) return;
+  const int f = blockIdx.y, lane = threadIdx.x & 63;
+  const int ya = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN_RPW, yb = min(ya + RUN_RPW, Hp);
   const int32_t* r = rowb + (size_t)f * rstride;
   const uint16_t* X = rx + (size_t)f * plane;
   int32_t* L = lab + (size_t)f * plane;
+  for (int y = ya; y < yb; y++) {
   const int by = r[y], ny = r[y + 1] - by;
   for (int j = lane; j < ny; j += 64) {
     const int id = by + j;
@@ -1648,6 +1658,7 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
     } else {
       atomicOr(&st[f].overflow, 1);
     }
+  }
   }
 }
 
