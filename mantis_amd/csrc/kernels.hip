@@ -988,9 +988,11 @@ __device__ inline void hr_row(const int32_t* rb, int H, int bs, int y, int& g, i
 }
 // band-local union-find on 16-bit labels in LDS (roots = smallest id); the
 // link is a 32-bit CAS on the dword holding the 16-bit slot
+// (bits 12..13 of a root's slot hold its band flags once the unions are done,
+// MK_HB_LFLAGS: ids are < HB_CAP = 4096, so the low 12 bits are the link)
 __device__ inline int hb_find(const uint16_t* L, int x) {
   int p;
-  while ((p = L[x]) != x) x = p;
+  while ((p = L[x] & 0xfff) != x) x = p;
   return x;
 }
 __device__ inline void hb_union(uint16_t* L, int a, int b) {
@@ -1046,7 +1048,12 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
                                                           uint32_t* __restrict__ ebits, int W, int H) {
   __shared__ uint16_t Ll[HB_CAP];
   __shared__ uint32_t Xl[HB_CAP];
+#ifndef MK_HB_LFLAGS
+#define MK_HB_LFLAGS 1
+#endif
+#if !MK_HB_LFLAGS
   __shared__ uint32_t Sl[HB_CAP / 4];  // per root byte: bit 0 strong, bit 1 reaches the band's edge rows
+#endif
   __shared__ int32_t rbl[HB_ROWS + 1];
   extern __shared__ uint32_t Ew[];     // the band's edge words (rows x WW), then its strong words, then its candidates
   const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1129,7 +1136,9 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   }
   for (int q = wave; q < nr; q += HB_WAVES) hb_emit_runs(Cw + q * WW, WW, (uint16_t*)Xl, rbl[q], lane);
   for (int i = t; i < n; i += HB_THREADS) Ll[i] = (uint16_t)i;
+#if !MK_HB_LFLAGS
   for (int i = t; i < (n + 3) / 4; i += HB_THREADS) Sl[i] = 0u;
+#endif
   __syncthreads();
   uint16_t* Li = Ll;
   const auto uni = [Li](int a, int b) { hb_union(Li, a, b); };
@@ -1139,16 +1148,29 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = hb_find(Ll, j);
-      Ll[j] = (uint16_t)root;
       const uint32_t b = (run_strong(Sw + q * WW, Xl[j] & 0xffff, Xl[j] >> 16) ? 1u : 0u) | (edge_row(q) ? 2u : 0u);
+#if MK_HB_LFLAGS
+      // the band flags go to bits 12..13 of the root's own slot (its link
+      // bits stay == root, so concurrent finds still stop there); a root
+      // never stores its own slot, which would drop flags already set
+      if (root != j) Ll[j] = (uint16_t)root;
+      if (b) atomicOr((uint32_t*)(Ll + (root & ~1)), (b << 12) << (16 * (root & 1)));
+#else
+      Ll[j] = (uint16_t)root;
       if (b) atomicOr(&Sl[root >> 2], b << (8 * (root & 3)));
+#endif
     }
   }
   __syncthreads();
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
+#if MK_HB_LFLAGS
+      const int root = Ll[j] & 0xfff;
+      const int fb = (Ll[root] >> 12) & 3;
+#else
       const int root = Ll[j];
       const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
+#endif
       // global labels / extents only where a later kernel looks: the band's
       // first and last rows (seam unions), list B runs (fb == 2: k_hyst_fix)
       // and band roots (finds end there; their flag byte is what k_hyst_mark /
