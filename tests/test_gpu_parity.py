@@ -504,3 +504,59 @@ def test_screen_off_equals_screen_on(frames, landmark_map):
     finally:
         mx.close()
         ms.close()
+
+
+def _disc_frame(rows, cols, pitch=26, r=5, squares=True):
+    """Gray frame with a rows x cols lattice of dark discs (each becomes a
+    small hole of the dilated edge net: a border whose approxPolyDP is not a
+    quad) and, when `squares`, three large dark squares on the right (quads)."""
+    H, W = 720, 1280
+    img = np.full((H, W, 3), 200, np.uint8)
+    yy, xx = np.mgrid[0:H, 0:W]
+    for i in range(rows):
+        for j in range(cols):
+            cy, cx = 20 + pitch * i, 20 + pitch * j
+            img[(yy - cy) ** 2 + (xx - cx) ** 2 <= r * r] = 40
+    if squares:
+        for k, (y0, x0) in enumerate([(60, 1000), (300, 1060), (520, 980)]):
+            img[y0:y0 + 110 + 10 * k, x0:x0 + 120] = 30
+    return img
+
+
+@pytest.mark.parametrize("lds_frames", [None, "0"])
+def test_many_borders_approx_paths(landmark_map, lds_frames):
+    """k_frame_contours' approxPolyDP on frames with 906 and 2,366 borders:
+    the length-ordered path (<= 1024 borders) and the index-order fallback
+    (more), in the latency shape (1024-thread blocks, LDS walks) and, with
+    MANTIS_TRACE_LDS_FRAMES=0, the throughput shape (256-thread blocks, L2
+    walks): quads, raw quad count and border / point counts against the oracle."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    seq = [_disc_frame(18, 25), _disc_frame(30, 40, pitch=24)]  # 906 / 2,366 borders
+    old = os.environ.get("MANTIS_TRACE_LDS_FRAMES")
+    if lds_frames is not None:
+        os.environ["MANTIS_TRACE_LDS_FRAMES"] = lds_frames
+    try:
+        m = M.Mantis(max_cams=2, max_width=1280, max_height=720)
+    finally:
+        if old is None:
+            os.environ.pop("MANTIS_TRACE_LDS_FRAMES", None)
+        else:
+            os.environ["MANTIS_TRACE_LDS_FRAMES"] = old
+    try:
+        m.set_map(*landmark_map)
+        m.rng_state = 1
+        m.process([M.make_image(x, K, D) for x in seq], rigs=2)
+        orc = O.Oracle(*landmark_map, seed=1)
+        nbs = []
+        for i, x in enumerate(seq):
+            o = orc.process(x, K, D)
+            g = m.frame_debug(i)
+            nbs.append(int(m.frame_counters(i)[0]))
+            assert g.n_raw_quads == o.n_raw_quads and g.n_quads == o.n_quads and o.n_quads > 0, (i, g.n_quads, o.n_quads)
+            n = g.n_quads
+            assert np.array_equal(np.array(g.quads)[:n], np.array(o.quads)[:n]), i
+        assert nbs[0] <= 1024 < nbs[1], nbs  # both approx paths ran
+    finally:
+        m.close()
