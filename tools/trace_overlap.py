@@ -26,13 +26,18 @@ def main(d, steps=None):
     gmax = max(e[3] for e in canny)
     big = [e for e in canny if e[3] == gmax]
     k = steps if steps else max(1, len(big) // 2)
-    t0 = big[-k][0]
-    t1 = max(e[1] for e in ev)
-    win = [e for e in ev if e[1] > t0]
+    # window: from the k-th last big Canny before the isolated step (bench.py
+    # runs context 0 alone for one step after the timed ones: its Canny is the
+    # last big one) to that step's start, so the isolated step and the latency
+    # calls after it do not count as idle time of the timed steps
+    t0 = big[-k - 1][0] if len(big) > k else big[0][0]
+    t1 = big[-1][0]
+    win = [e for e in ev if e[1] > t0 and e[0] < t1]
     # sweep line
     pts = []
     for s, e, n, _ in win:
         s = max(s, t0)
+        e = min(e, t1)
         pts.append((s, 1, n))
         pts.append((e, -1, n))
     pts.sort(key=lambda p: (p[0], p[1]))
@@ -58,7 +63,7 @@ def main(d, steps=None):
     dur = collections.Counter()
     cnt = collections.Counter()
     for s, e, n, _ in win:
-        dur[n] += e - max(s, t0)
+        dur[n] += min(e, t1) - max(s, t0)
         cnt[n] += 1
     print(f"window {span / 1e6:.1f} ms from the last {k} big k_canny dispatches; busy {busy / span:.3f}, "
           f"mean kernels in flight {area / max(busy, 1):.2f}")
