@@ -15,11 +15,11 @@ CSRC = mantis_amd/csrc
 all: product tools oracle
 
 product: mantis_amd/libmantis_amd.so
-mantis_amd/libmantis_amd.so: $(CSRC)/api.hip $(CSRC)/kernels.hip $(CSRC)/gn_impl.hip $(CSRC)/dense_impl.hip $(wildcard $(CSRC)/*.h) include/mantis.h include/mantis_ros.h
+mantis_amd/libmantis_amd.so: $(CSRC)/api.hip $(CSRC)/kernels.hip $(CSRC)/gn_impl.hip $(CSRC)/dense_impl.hip $(wildcard $(CSRC)/*.h) $(CSRC)/mk_rpp_np.inc $(CSRC)/markov_impl.hip include/mantis.h include/mantis_ros.h
 	$(HIPCC) $(HIPFLAGS) -shared -pthread -o $@ $(CSRC)/api.hip -lrccl
 
 tools: build/libmantis_hostcheck.so tools/libmantis_synth.so
-build/libmantis_hostcheck.so: $(CSRC)/hostcheck.cpp $(wildcard $(CSRC)/mk_*.h)
+build/libmantis_hostcheck.so: $(CSRC)/hostcheck.cpp $(wildcard $(CSRC)/mk_*.h) $(CSRC)/mk_rpp_np.inc
 	mkdir -p build
 	g++ -O2 -std=c++17 -fPIC -ffp-contract=off -shared -o $@ $(CSRC)/hostcheck.cpp
 tools/libmantis_synth.so: tools/synth_host.cpp $(CSRC)/synth.h
@@ -40,7 +40,7 @@ SAN_ORACLE_SRC = oracle/o_imgproc.cpp oracle/o_rpp.cpp oracle/o_mantis3.cpp orac
 build/san/liboracle.so: $(SAN_ORACLE_SRC) $(wildcard oracle/*.hpp) oracle/oracle.h
 	mkdir -p build/san
 	g++ $(SANFLAGS) -shared -o $@ $(SAN_ORACLE_SRC)
-build/san/libmantis_hostcheck.so: $(CSRC)/hostcheck.cpp $(wildcard $(CSRC)/mk_*.h)
+build/san/libmantis_hostcheck.so: $(CSRC)/hostcheck.cpp $(wildcard $(CSRC)/mk_*.h) $(CSRC)/mk_rpp_np.inc
 	mkdir -p build/san
 	g++ $(SANFLAGS) -shared -o $@ $(CSRC)/hostcheck.cpp
 sanitize: build/san/liboracle.so build/san/libmantis_hostcheck.so tools/libmantis_synth.so product

@@ -234,6 +234,18 @@ def make_ctx(M, rk, **cfg):
         die(rk, f"cannot create a library context on device {rk.local} ({e}); this needs an MI355X per rank")
 
 
+def lib_sha16():
+    """First 16 hex digits of the running product library's SHA-256: PMC
+    summaries record it, and the bench line uses a summary only when it
+    matches (a stale profile of another build is never mixed in)."""
+    import hashlib
+
+    try:
+        return hashlib.sha256(open(os.path.join(ROOT, "mantis_amd", "libmantis_amd.so"), "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def cpu_model():
     try:
         for ln in open("/proc/cpuinfo"):
@@ -298,7 +310,9 @@ def cpu_baseline(a, W, H, cams_per_rig):
         res = list(ex.map(lambda k: stream(k, a.cpu_seconds), range(P)))
         tall = time.perf_counter() - t0
     nall = sum(n for n, _ in res)
-    return {"value": round(nall / tall, 4), "unit": "rig poses/s", "cores": P, "kind": "port",
+    # cores = the CPUs the P threads could actually use: the visible CPUs capped by the cgroup quota
+    cores = P if quota is None else max(1, min(P, int(quota)))
+    return {"value": round(nall / tall, 4), "unit": "rig poses/s", "cores": cores, "threads": P, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus_visible": avail, "cgroup_cpu_quota": quota,
             "single_core": {"value": round(n1 / t1, 4), "p50_rig_ms": round(t1 / n1 * 1e3, 1), "rigs": n1},
             "sample": f"oracle/liboracle.so (C++17 -O3, full mantis3 callback per camera) on {len(rigs)} distinct "
@@ -350,7 +364,7 @@ def run_config3(a, rk, cpu):
     from concurrent.futures import ThreadPoolExecutor
 
     pool = ThreadPoolExecutor(max_workers=nctx)
-    stage_ms = {}
+    stage_ms, kern_ms = {}, {}
 
     def run_steps(bs, k_steps, record=False):
         """k_steps steps: every context's host thread runs its share of each step
@@ -359,8 +373,12 @@ def run_config3(a, rk, cpu):
             for _ in range(k_steps):
                 bs[k].run()
                 if record and k == 0:
-                    for name, ms in m.kernel_times():
-                        stage_ms[name] = stage_ms.get(name, 0.0) + ms
+                    for name, ms in m.kernel_times():  # "stage" or "stage/kernel" (hot stages: one event per kernel)
+                        st = name.split("/", 1)[0]
+                        stage_ms[st] = stage_ms.get(st, 0.0) + ms
+                        if "/" in name:
+                            kn = name.split("/", 1)[1]
+                            kern_ms[kn] = kern_ms.get(kn, 0.0) + ms
         for f in [pool.submit(worker, k) for k in range(len(bs))]:
             f.result()
 
@@ -372,14 +390,20 @@ def run_config3(a, rk, cpu):
 
     run_steps(batches, a.warmup)
 
-    # ---- timed region: stage events on context 0's stream
+    # ---- timed region: stage / kernel events on context 0's stream; host CPU
+    # time of this process (every context's host thread, the cv::RNG draw
+    # threads, the driver's) over the same region
     m.set_profiling(True)
     barrier_sync()
+    cpu0 = os.times()
     t0 = time.perf_counter()
     run_steps(batches, a.steps, record=True)
     barrier_sync()
-    elapsed = rk.max(time.perf_counter() - t0)
+    el_local = time.perf_counter() - t0
+    cpu1 = os.times()
+    elapsed = rk.max(el_local)
     m.set_profiling(False)
+    host_cpu_s = (cpu1.user - cpu0.user) + (cpu1.system - cpu0.system)
     value = a.rigs * a.steps * rk.world / elapsed
     ms_per_step = elapsed / a.steps * 1e3
     # every step processes the same frames: the last step's records describe each step
@@ -401,8 +425,13 @@ def run_config3(a, rk, cpu):
     s_fast = LANDMARKS * fast_per_frame
     s_slow = 3700.0 * slow_per_frame
 
-    # ---- roofline of the dominant stage (per launch = per step on context 0)
+    # ---- roofline of the dominant stage (per launch = per step on context 0).
+    # Durations are HIP events around each kernel of the stage on the stream it
+    # is launched on (the hot stages are marked per kernel), averaged over the
+    # timed steps: dispatch to completion under the other contexts' load, what
+    # rocprofv3 reports per dispatch of the same command.
     avg = {k: v / a.steps for k, v in stage_ms.items()}
+    kavg = {k: v / a.steps for k, v in kern_ms.items()}
     work = {
         # BGR read once; candidate and strong-root bit planes written
         "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
@@ -415,33 +444,41 @@ def run_config3(a, rk, cpu):
         "contours_quads": ("hbm", frames_step * ((W + 2) * (H + 2) // 8)),
         "rpp_first": ("fp64", iters[0] * FLOPS_PER_OBJPOSE_ITER),
         "rpp_cand": ("fp64", iters[1] * FLOPS_PER_OBJPOSE_ITER),
-        "score_pf_yaw": ("fp64", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
+        "score_pf_yaw": ("valu", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
+    stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_final"),
+                     "canny_nms": ("k_canny_strip<2>", "k_canny_strip<1>", "k_canny"),
+                     "hysteresis": ("k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
+                     "morph": ("k_morph",)}
+    digest = lib_sha16()
 
-    def roofline(stage, avg=avg):
+    def pmc_for(path):
+        """A committed PMC summary, only when it was collected on this very
+        library build (its lib_sha16 = the running libmantis_amd.so's)."""
+        try:
+            pj = json.load(open(os.path.join(ROOT, path)))
+        except (OSError, ValueError):
+            return None
+        return pj if pj.get("lib_sha16") == digest else None
+
+    def roofline(stage, avg=avg, kavg=kavg):
         if stage not in avg or stage not in work:
             return None
         kind, amount = work[stage]
         dur_s = avg[stage] * 1e-3
+        ks = {k: round(kavg[k], 4) for k in stage_kernels.get(stage, ()) if k in kavg}
+        r = {"kernel": stage, "kernels_ms": ks or None, "avg_launch_ms": round(avg[stage], 4), "traffic": None}
         if kind == "hbm":
             achieved = amount / dur_s / 1e9
-            traffic = None
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                try:
-                    tj = json.load(open(pmc))
-                    if tj.get("stage") == stage and tj.get("hbm_bytes_per_frame"):
-                        traffic = int(tj["hbm_bytes_per_frame"] * frames_step)
-                except Exception:
-                    traffic = None
-            return {"bound": "hbm", "kernel": stage, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "alg_bytes_per_launch": int(amount), "avg_launch_ms": round(avg[stage], 4)}
+            r.update({"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(achieved / HBM_PEAK_GBS, 5), "alg_bytes_per_launch": int(amount)})
+            return r
         achieved = amount / dur_s / 1e12
-        return {"bound": "fp64_valu", "kernel": stage, "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
-                "alg_flops_per_launch": int(amount), "avg_launch_ms": round(avg[stage], 4)}
+        r.update({"bound": "fp64" if kind == "fp64" else "valu", "achieved": round(achieved, 4),
+                  "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+                  "alg_flops_per_launch": int(amount)})
+        return r
 
     kern = [k for k in avg if k in work]
     dom = max(kern, key=avg.get) if kern else None  # dominant kernel stage by event time
@@ -449,50 +486,40 @@ def run_config3(a, rk, cpu):
     if roof is not None:
         roof["stages_ms"] = {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}
         roof["objpose_iterations_per_launch"] = iters
+        roof["duration_source"] = ("HIP events around each kernel of the stage on context 0's stream over the timed "
+                                   "steps (sum of kernels_ms)")
     roof_front = roofline("canny_nms")
+    # HBM traffic and VALU issue from PMC summaries of this same build
+    # (tools/pmc_score.sh / tools/pmc_traffic.sh write lib_sha16): per launch =
+    # per-frame counters x frames_step; null when no summary matches the build
+    pj = pmc_for(os.path.join("profiles", "r04_pmc.json"))
+    pmc_k = {} if pj is None else pj["kernels"]
+    pmc_fr = None if pj is None else pj["frames_per_launch"]
 
-    # ---- the same rooflines from kernel durations (rocprofv3 batch-launch
-    # averages of this command, committed under profiles/): the event spans
-    # above also hold the queue waits between a stage's kernels
-    stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_final"),
-                     "canny_nms": ("k_canny_strip", "k_canny"),
-                     "hysteresis": ("k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
-                     "morph": ("k_morph",)}
-    prof_src = os.path.join("profiles", "r03_batch_launch_avg_default.json")
-
-    def profiled(r, stage):
-        if r is None or stage not in stage_kernels or a.rigs != 6144 or nctx != 6:
-            return  # the committed profile is of the default command (6 contexts x 1024 rigs)
-        try:
-            pj = json.load(open(os.path.join(ROOT, prof_src)))
-        except (OSError, ValueError):
+    def pmc_stage(r, stage):
+        """traffic (HBM bytes per launch: FETCH_SIZE x 2 + WRITE_SIZE) and VALU
+        issue of the stage's kernels, scaled from the summary's launch size"""
+        if r is None or not pmc_k or not pmc_fr:
             return
-        ms = 0.0
-        for k in stage_kernels[stage]:
-            hit = [v["avg_ms"] for name, v in pj.items() if ("::" + k + "<") in name or name.endswith("::" + k)]
-            ms += hit[0] if hit else 0.0  # kernels the profiled build did not launch
-        if ms == 0.0:
+        kk = [k.split("<")[0] for k in stage_kernels.get(stage, ())]
+        kk = [k for k in dict.fromkeys(kk) if k in pmc_k and "FETCH_SIZE_bytes" in pmc_k[k]]
+        if not kk:
             return
-        amount = work[stage][1]
-        ach = amount / (ms * 1e-3) / (1e9 if r["unit"] == "GB/s" else 1e12)
-        r["profiled"] = {"source": prof_src, "kernel_sum_ms": round(ms, 4), "achieved": round(ach, 4),
-                         "frac": round(ach / r["peak"], 5),
-                         "note": "sum of the stage kernels' rocprofv3 durations (batch launches of the default command)"}
+        sc = frames_step / pmc_fr
+        r["traffic"] = int(sum(2 * pmc_k[k]["FETCH_SIZE_bytes"] + pmc_k[k].get("WRITE_SIZE_bytes", 0) for k in kk) * sc)
+        vi = sum(pmc_k[k].get("SQ_INSTS_VALU", 0) for k in kk) * sc
+        if vi:
+            r["valu_instructions_per_launch"] = int(vi)
+            # wave64 VALU instruction = 2 cycles on a SIMD-32 (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
+            r["valu_issue_frac"] = round(vi * 2 / (1024 * 2.4e9 * r["avg_launch_ms"] * 1e-3), 4)
+        r["pmc_source"] = "profiles/r04_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step)"
 
-    profiled(roof, dom)
-    profiled(roof_front, "canny_nms")
-    # HBM reads of the scoring kernels (FETCH_SIZE, kB per launch of 1024 frames,
-    # tools/pmc_score.sh; no write counter in that pass set), per this launch
-    if roof is not None and dom == "score_pf_yaw" and roof.get("traffic") is None:
-        try:
-            pj = json.load(open(os.path.join(ROOT, "profiles", "r03_pmc_score_screen.json")))
-            fk = sum(v["FETCH_SIZE"] for k, v in pj.items() if "k_score_" in k)
-            roof["traffic"] = int(fk * 1024 / 1024 * frames_step)
-            roof["traffic_note"] = ("HBM read bytes from FETCH_SIZE of k_score_init/pf/final "
-                                    "(profiles/r03_pmc_score_screen.json, 1024-frame launches, scaled per frame); "
-                                    "the stage is FP64-issue / gather-latency bound, not HBM-bound")
-        except (OSError, ValueError, KeyError):
-            pass
+    if roof is not None and dom == "score_pf_yaw":
+        roof["bound_note"] = ("FP32 screen + exact FP64 fallback on the VALU, gathers from L2/MALL: frac counts the "
+                              "reference's 51 algorithmic FP64 flops per landmark projection against the FP64 vector "
+                              "peak; valu_issue_frac is the VALU issue occupancy from SQ_INSTS_VALU")
+    pmc_stage(roof, dom)
+    pmc_stage(roof_front, "canny_nms")
 
     # ---- the same stages with context 0 running alone (one step, after the
     # timed region): the timed-region launch durations above include the
@@ -500,13 +527,23 @@ def run_config3(a, rk, cpu):
     if nctx > 1 and roof is not None:
         m.set_profiling(True)
         ctxs[0].process(per_ctx[0], rigs_ctx)
-        iso = {k: v for k, v in m.kernel_times()}
+        iso_raw = m.kernel_times()
         m.set_profiling(False)
+        iso, kiso = {}, {}
+        for name, ms in iso_raw:
+            st = name.split("/", 1)[0]
+            iso[st] = iso.get(st, 0.0) + ms
+            if "/" in name:
+                kiso[name.split("/", 1)[1]] = ms
         for r, stg in ((roof, dom), (roof_front, "canny_nms")):
-            ri = roofline(stg, iso) if r is not None else None
+            ri = roofline(stg, iso, kiso) if r is not None else None
             if ri is not None:
-                r["isolated"] = {"avg_launch_ms": ri["avg_launch_ms"], "achieved": ri["achieved"], "frac": ri["frac"],
+                r["isolated"] = {"avg_launch_ms": ri["avg_launch_ms"], "kernels_ms": ri["kernels_ms"],
+                                 "achieved": ri["achieved"], "frac": ri["frac"],
                                  "note": "context 0 alone, one step after the timed region"}
+                if "valu_instructions_per_launch" in r:
+                    r["isolated"]["valu_issue_frac"] = round(
+                        r["valu_instructions_per_launch"] * 2 / (1024 * 2.4e9 * ri["avg_launch_ms"] * 1e-3), 4)
         roof["stages_ms_isolated"] = {k: round(v, 4) for k, v in sorted(iso.items(), key=lambda kv: -kv[1])}
     path_bytes = n_frames * (6 * W * H + 3 * (s_fast + s_slow))
 
@@ -574,6 +611,11 @@ def run_config3(a, rk, cpu):
             "camera_frames_per_s": round(value * CAMS, 2),
             "published_frac": round(published / max(1, a.rigs * a.steps), 4),
             "path_alg_GBps": round(path_bytes * a.steps / elapsed / 1e9, 3),
+            "host_cpu_s_per_step": round(host_cpu_s / a.steps, 4),
+            "host_cpu_note": ("process user+system CPU seconds per step over the timed region (os.times: every "
+                              "context's host thread incl. the cv::RNG gaussian draws); / ms_per_step = cores busy"),
+            "host_cores_busy": round(host_cpu_s / el_local, 3),
+            "lib_sha16": digest,
             "host_ingest": ingest,
             "roofline": roof,
             "roofline_frontend": roof_front,

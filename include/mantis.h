@@ -264,6 +264,15 @@ mantis_status mantis_score_hypotheses(void* ctx, const mantis_image* img, const 
  * -1 rotation check failed = the reference's exit(1)). */
 mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* obj_pts, int32_t n, double* R,
                                double* t, double* errs, int32_t* rpp_status);
+/* RPP::Rpp(model, iprts, ...) (RPP.h:92-93, RPP.cpp:13-64) on n problems of n_points points each,
+ * 4 <= n_points <= 12 (the reference accepts any count; demo.cpp:17-38 solves 10): img_pts
+ * n x n_points x 2 normalized (the homogeneous row is 1, as demo.cpp's Mat::ones), obj_pts
+ * n x n_points x 3. Outputs as mantis_rpp_batch plus iterations (n, nullable: the reference's
+ * `iterations` out-parameter). One device lane per problem; mantis_rpp_batch is the throughput
+ * entry for 4-point problems (same arithmetic, bit-identical results). */
+mantis_status mantis_rpp_solve(void* ctx, const double* img_pts, const double* obj_pts, int32_t n_points,
+                               int32_t n, double* R, double* t, double* errs, int32_t* rpp_status,
+                               int32_t* iterations);
 
 /* Per-quad Gauss-Newton after RPP (new stage; legacy analogue
  * cv::solvePnP ITERATIVE, include/legacy/mantis2/PoseEstimator.h:91-153): n

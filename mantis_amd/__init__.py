@@ -106,6 +106,8 @@ _SIGS = {
                                           C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_rpp_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    "mantis_rpp_solve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mantis_quad_gn": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,
                                  C.c_void_p, C.c_void_p]),
     "mantis_get_rig_weights": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -521,6 +523,29 @@ class Mantis:
                                          t.ctypes.data, e.ctypes.data, s.ctypes.data), "rpp_batch")
         return R.reshape(n, 3, 3), t, e, s
 
+    def rpp_solve(self, model, iprts):
+        """RPP::Rpp(model, iprts) (RPP.cpp:13-64) on the device for any point
+        count 4..12 (mantis_rpp_solve): model 3 x n (or k x 3 x n), iprts 3 x n
+        homogeneous with a unit third row (demo.cpp:41-53's layout). Returns
+        (R [k,3,3], t [k,3], errs [k,2] = obj_err, img_err, status [k], iterations [k])."""
+        m = np.asarray(model, np.float64)
+        q = np.asarray(iprts, np.float64)
+        if m.ndim == 2:
+            m, q = m[None], q[None]
+        k, _, npts = m.shape
+        if not np.all(q[:, 2, :] == 1.0):
+            raise ValueError("rpp_solve: image points must be homogeneous with z = 1")
+        obj = np.ascontiguousarray(np.transpose(m, (0, 2, 1)))      # k x n x 3
+        img = np.ascontiguousarray(np.transpose(q[:, :2, :], (0, 2, 1)))  # k x n x 2
+        R = np.zeros((k, 9))
+        t = np.zeros((k, 3))
+        e = np.zeros((k, 2))
+        s = np.zeros(k, np.int32)
+        it = np.zeros(k, np.int32)
+        self._chk(lib().mantis_rpp_solve(self.h, img.ctypes.data, obj.ctypes.data, int(npts), int(k), R.ctypes.data,
+                                         t.ctypes.data, e.ctypes.data, s.ctypes.data, it.ctypes.data), "rpp_solve")
+        return R.reshape(k, 3, 3), t, e, s, it
+
     def rig_weights(self, rig, cams_per_rig=None):
         """Legacy rig weighting record of rig `rig` (mantis_get_rig_weights):
         (weights[C+1], c2w[C+1, C, 12], sums[C+1, C, 2], chosen slot or -1);
@@ -636,6 +661,15 @@ class Mantis:
         ms = (C.c_float * 64)()
         n = lib().mantis_kernel_times(self.h, names, ms, 64)
         return [(names[i].decode(), ms[i]) for i in range(n)]
+
+    def stage_times(self):
+        """kernel_times() summed per stage: a mark named "stage/kernel" (the
+        hot stages are marked per kernel) counts toward "stage"."""
+        out = {}
+        for name, ms in self.kernel_times():
+            st = name.split("/", 1)[0]
+            out[st] = out.get(st, 0.0) + ms
+        return list(out.items())
 
 
 def argmin_pick(pairs):

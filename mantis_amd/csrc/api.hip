@@ -242,22 +242,30 @@ struct Ctx {
 // ncclAllReduce (max of a failure flag, 4 bytes), so every rank returns
 // together -- the failing rank its own error, the others MANTIS_ERR_COMM --
 // instead of leaving them blocked in an all-gather.
-mantis_status agree(Ctx* c, mantis_status local) {
+// `count` (>= 0): a size every rank must pass identically (the frame count of a
+// batched exchange); ranks that disagree all fail with MANTIS_ERR_ARG instead
+// of issuing collectives of different sizes.
+mantis_status agree(Ctx* c, mantis_status local, int32_t count = -1) {
   c->agreed_fail = false;
   if (!c->comm || !c->d_agree) return local;
-  int32_t flag = local != MANTIS_OK ? 1 : 0;
-  if (hipMemcpyAsync(c->d_agree, &flag, sizeof(flag), hipMemcpyHostToDevice, c->s) != hipSuccess ||
-      ncclAllReduce(c->d_agree, c->d_agree, 1, ncclInt32, ncclMax, (ncclComm_t)c->comm, c->s) != ncclSuccess ||
-      hipMemcpyAsync(&flag, c->d_agree, sizeof(flag), hipMemcpyDeviceToHost, c->s) != hipSuccess ||
+  int32_t v[3] = {local != MANTIS_OK ? 1 : 0, count, -count};  // max of each: flag, max count, -min count
+  if (hipMemcpyAsync(c->d_agree, v, sizeof(v), hipMemcpyHostToDevice, c->s) != hipSuccess ||
+      ncclAllReduce(c->d_agree, c->d_agree, 3, ncclInt32, ncclMax, (ncclComm_t)c->comm, c->s) != ncclSuccess ||
+      hipMemcpyAsync(v, c->d_agree, sizeof(v), hipMemcpyDeviceToHost, c->s) != hipSuccess ||
       hipStreamSynchronize(c->s) != hipSuccess) {
     c->err = "agreement all-reduce failed";
     return MANTIS_ERR_COMM;
   }
-  c->agreed_fail = flag != 0;
+  const bool mismatch = v[1] != -v[2];
+  c->agreed_fail = v[0] != 0 || mismatch;
   if (local != MANTIS_OK) return local;
-  if (flag) {
+  if (v[0]) {
     c->err = "another rank of the communicator failed before this exchange (see its mantis_last_error)";
     return MANTIS_ERR_COMM;
+  }
+  if (mismatch) {
+    c->err = "ranks passed different frame counts to a batched exchange (every rank must pass the same n_frames)";
+    return MANTIS_ERR_ARG;
   }
   return MANTIS_OK;
 }
@@ -303,9 +311,9 @@ Cam cam_from(const mantis_image& im) {
   return m;
 }
 
-// FP32 screen constants of a camera (mk_screen.h screen_cam_from samples the
-// distortion curve: ~0.1 ms), memoised per context on the intrinsics: the
-// frames of a batch share a few cameras
+// FP32 screen constants of a camera (mk_screen.h screen_cam_from bounds the
+// distortion curve over 4096 pieces: ~0.1 ms), memoised per context on the
+// intrinsics: the frames of a batch share a few cameras
 ScreenCam screen_cam_cached(Ctx* c, const Cam& cm) {
   for (const auto& e : c->scam_cache)
     if (std::memcmp(&e.first, &cm, sizeof(Cam)) == 0) return e.second;
@@ -371,16 +379,18 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols, nw = ns * n;
     k_canny_strip<2><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
                                                                  c->d_b1, c->d_b2, B, ns, nw);
+    mark(c, "canny_nms/k_canny_strip<2>");
   } else if (c->canny_strip && c->vec_ok && W >= 8 && H >= 3) {
     // 4 columns per lane (W % 4 == 0, dword-aligned rows)
     const int ns = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols, nw = ns * n;
     k_canny_strip<1><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
                                                                  c->d_b1, c->d_b2, B, ns, nw);
+    mark(c, "canny_nms/k_canny_strip<1>");
   } else {
     k_canny<<<(unsigned)(tgx * tgy * n), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
                                                         c->vec_ok ? 1 : 0, c->d_b1, c->d_b2, B, tgx, tgy);
+    mark(c, "canny_nms/k_canny");
   }
-  mark(c, "canny_nms");
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
   HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
               HB_ROWS * ((W + 1) / 2)};
@@ -389,19 +399,22 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const int WWb = bits::words(W);
   k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 3 * sizeof(uint32_t) * HB_ROWS * WWb, c->s>>>(
       c->d_b1, c->d_b2, B, hr, c->d_eb, W, H);
+  mark(c, "hysteresis/k_hyst_band");
   const int nseam = (H - 1) / HB_ROWS;
   if (nseam > 0) k_hyst_seam<<<dim3((nseam + 3) / 4, n), 256, 0, c->s>>>(hr, H);
+  mark(c, "hysteresis/k_hyst_seam");
   k_hyst_mark<<<dim3(8, n), 256, 0, c->s>>>(hr, H);
+  mark(c, "hysteresis/k_hyst_mark");
   k_hyst_fix<<<dim3(8, n), 256, 0, c->s>>>(hr, c->d_eb, B, W, H);
   if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
-  mark(c, "hysteresis");
+  mark(c, "hysteresis/k_hyst_fix");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   dim3 gm((H + c->morph_bh - 1) / c->morph_bh, n);
   k_morph<<<gm, MB_THREADS, morph_lds(W, c->morph_bh), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
                                                               c->morph_bh);
   if (det_bytes) k_bits_to_bytes<<<blocks_for((size_t)(W + 2) * (H + 2)), 256, 0, c->s>>>(c->d_dbits, c->d_det, W + 2, H + 2,
                                                                                           dbits_wpw(W + 2));
-  mark(c, "morph");
+  mark(c, "morph/k_morph");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -584,6 +597,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   Landmarks L = lmk_of(c);
   k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
                                               c->d_dbg, c->d_sst, zc ? c->h_gauss : nullptr, c->d_gauss, per);
+  mark(c, "score_pf_yaw/k_score_init");
   // particle filter: 16 waves per frame, each task one particle over a
   // 1/kPfSplit slice of the landmarks (the integer partial sums combine
   // exactly); the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0:
@@ -597,9 +611,10 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
     k_score_pf<kPfThreads, kPfSplit, false><<<n, kPfThreads, 0, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
         c->cfg.iterations);
+  mark(c, "score_pf_yaw/k_score_pf");
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
                                                c->d_sst, c->cfg.grid_spacing, 9);
-  mark(c, "score_pf_yaw");
+  mark(c, "score_pf_yaw/k_score_final");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -720,6 +735,23 @@ mantis_status dalloc(Ctx* c, T** p, size_t count) {
   }
   return MANTIS_OK;
 }
+// device scratch of one C-ABI call, freed on every return path
+struct DevScratch {
+  Ctx* c;
+  std::vector<void*> p;
+  explicit DevScratch(Ctx* ctx) : c(ctx) {}
+  template <class T>
+  bool get(T** q, size_t count) {  // true on failure (c->err set), like dalloc
+    *q = nullptr;
+    if (dalloc(c, q, count)) return true;
+    p.push_back((void*)*q);
+    return false;
+  }
+  ~DevScratch() {
+    if (!p.empty()) (void)hipStreamSynchronize(c->s);
+    for (void* q : p) (void)hipFree(q);
+  }
+};
 template <class T>
 mantis_status halloc(Ctx* c, T** p, size_t count) {
   if (hipHostMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1), hipHostMallocDefault) != hipSuccess) {
@@ -1344,24 +1376,26 @@ mantis_status mantis_shard_gauss_offsets(void* ctx, const int32_t* pairs, int32_
   if ((int64_t)per_frame * n_global > INT32_MAX) { c->err = "per_frame x n_global exceeds 2^31"; return MANTIS_ERR_ARG; }
   for (int i = 0; i < n_local; i++)
     if (gidx[i] < 0 || gidx[i] >= n_global) { c->err = "gidx outside [0, n_global)"; return MANTIS_ERR_ARG; }
+  // the host rule (mk_shard.h offsets_from_pairs) rejects a gather naming a
+  // frame >= n_global; so does the kernel (total -1), checked below as well
+  for (int i = 0; i < npairs; i++)
+    if (pairs[2 * i] >= n_global) { c->err = "pair index outside [0, n_global)"; return MANTIS_ERR_ARG; }
   int32_t *d_pairs = nullptr, *d_flags = nullptr, *d_gidx = nullptr, *d_total = nullptr;
-  struct Free {
-    std::vector<void*> p;
-    ~Free() { for (void* q : p) (void)hipFree(q); }
-  } fr;
-  if (dalloc(c, &d_pairs, (size_t)2 * npairs) || dalloc(c, &d_flags, (size_t)2 * n_global) ||
-      dalloc(c, &d_gidx, (size_t)n_local) || dalloc(c, &d_total, 1))
+  FrameState* d_st = nullptr;  // scratch frame states: the context's (last batch) are left alone
+  DevScratch ds(c);
+  if (ds.get(&d_pairs, (size_t)2 * npairs) || ds.get(&d_flags, (size_t)2 * n_global) ||
+      ds.get(&d_gidx, (size_t)n_local) || ds.get(&d_total, 1) || ds.get(&d_st, (size_t)std::max(1, n_local)))
     return MANTIS_ERR_OOM;
-  fr.p = {d_pairs, d_flags, d_gidx, d_total};
   if (npairs) HIP_OK(hipMemcpyAsync(d_pairs, pairs, sizeof(int32_t) * 2 * npairs, hipMemcpyHostToDevice, c->s));
   if (n_local) HIP_OK(hipMemcpyAsync(d_gidx, gidx, sizeof(int32_t) * n_local, hipMemcpyHostToDevice, c->s));
-  k_gauss_offsets_global<<<1, 1024, 0, c->s>>>(d_pairs, npairs, d_flags, n_global, c->d_st, d_gidx, n_local, per_frame,
+  k_gauss_offsets_global<<<1, 1024, 0, c->s>>>(d_pairs, npairs, d_flags, n_global, d_st, d_gidx, n_local, per_frame,
                                                d_total);
   HIP_OK(hipGetLastError());
   std::vector<FrameState> st(std::max(1, n_local));
-  if (n_local) HIP_OK(hipMemcpyAsync(st.data(), c->d_st, sizeof(FrameState) * n_local, hipMemcpyDeviceToHost, c->s));
+  if (n_local) HIP_OK(hipMemcpyAsync(st.data(), d_st, sizeof(FrameState) * n_local, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipMemcpyAsync(total, d_total, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
+  if (*total < 0) { c->err = "pair index outside [0, n_global)"; return MANTIS_ERR_ARG; }
   for (int i = 0; i < n_local; i++) offsets[i] = st[i].gauss_offset;
   return MANTIS_OK;
 }
@@ -1649,6 +1683,46 @@ mantis_status mantis_rpp_batch(void* ctx, const double* img_pts, const double* o
   }
   void* ps[] = {d_ip, d_op, d_it, d_rf, d_out, d_j0, d_j1, d_q};
   for (void* p : ps) (void)hipFree(p);
+  return MANTIS_OK;
+}
+
+mantis_status mantis_rpp_solve(void* ctx, const double* img_pts, const double* obj_pts, int32_t n_points,
+                               int32_t n, double* R, double* t, double* errs, int32_t* rpp_status,
+                               int32_t* iterations) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !img_pts || !obj_pts || n <= 0 || !R || !t || !errs || !rpp_status) return MANTIS_ERR_ARG;
+  if (n_points < 4 || n_points > 12) {
+    c->err = "mantis_rpp_solve: n_points must be in [4, 12]";
+    return MANTIS_ERR_ARG;
+  }
+  double *d_ip, *d_op;
+  RppOut* d_out;
+  DevScratch ds(c);
+  if (ds.get(&d_ip, (size_t)2 * n_points * n) || ds.get(&d_op, (size_t)3 * n_points * n) || ds.get(&d_out, (size_t)n))
+    return MANTIS_ERR_OOM;
+  HIP_OK(hipMemcpyAsync(d_ip, img_pts, sizeof(double) * 2 * n_points * n, hipMemcpyHostToDevice, c->s));
+  HIP_OK(hipMemcpyAsync(d_op, obj_pts, sizeof(double) * 3 * n_points * n, hipMemcpyHostToDevice, c->s));
+  const unsigned g = (unsigned)((n + 63) / 64);
+  switch (n_points) {
+#define MK_RPP_LAUNCH(k) \
+    case k: k_rpp_solve<k><<<g, 64, 0, c->s>>>(d_ip, d_op, n, d_out); break;
+    MK_RPP_LAUNCH(4)
+    MK_RPP_INSTANCES(MK_RPP_LAUNCH)
+#undef MK_RPP_LAUNCH
+  }
+  HIP_OK(hipGetLastError());
+  std::vector<RppOut> h(n);
+  HIP_OK(hipMemcpyAsync(h.data(), d_out, sizeof(RppOut) * n, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 9; k++) R[9 * i + k] = h[i].R[k];
+    for (int k = 0; k < 3; k++) t[3 * i + k] = h[i].t[k];
+    errs[2 * i] = h[i].obj_err;
+    errs[2 * i + 1] = h[i].img_err;
+    rpp_status[i] = h[i].error == 1 ? -1 : h[i].status;
+    if (iterations) iterations[i] = h[i].iterations;
+  }
   return MANTIS_OK;
 }
 

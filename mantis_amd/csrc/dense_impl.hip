@@ -119,29 +119,39 @@ mantis_status score_argmin_impl(void* ctx, const mantis_image* img, const uint8_
   Ctx* c = (Ctx*)ctx;
   if (c) bind_device(c);
   if (!c || !img || !c2w || n < 0 || !best_err || !best_idx) return MANTIS_ERR_ARG;
-  if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
   if (use_comm && !c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
-  int W, H;
-  mantis_status st = stage_frames(c, img, 1, W, H);
+  // every rank-local failure from here to the exchange is agreed on first
+  // (agree(), api.hip), so no rank is left alone in the all-gather
+  const auto prepare = [&]() -> mantis_status {
+    if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
+    if (use_comm && (c->nranks < 1 || c->nranks > 63)) { c->err = "argmin exchange supports 1..63 ranks"; return MANTIS_ERR_ARG; }
+    int W, H;
+    mantis_status st = stage_frames(c, img, 1, W, H);
+    if (st != MANTIS_OK) return st;
+    const size_t cap = (size_t)(n > 0 ? n : 1);
+    if (cap > c->dense_cap) {
+      (void)hipFree(c->d_dense_c2w);
+      (void)hipFree(c->d_dense_err);
+      (void)hipFree(c->d_dense_np);
+      c->d_dense_c2w = nullptr;
+      c->d_dense_err = nullptr;
+      c->d_dense_np = nullptr;
+      c->dense_cap = 0;
+      if (dalloc(c, &c->d_dense_c2w, 12 * cap) != MANTIS_OK || dalloc(c, &c->d_dense_err, cap) != MANTIS_OK ||
+          dalloc(c, &c->d_dense_np, cap) != MANTIS_OK)
+        return MANTIS_ERR_OOM;
+      c->dense_cap = cap;
+    }
+    if (!c->d_pairs) {
+      if (dalloc(c, &c->d_pairs, (size_t)2 * 64) != MANTIS_OK) return MANTIS_ERR_OOM;
+      c->dense_pairs_cap = 128;
+    }
+    return MANTIS_OK;
+  };
+  mantis_status st = prepare();
+  if (use_comm) st = agree(c, st, 1);
   if (st != MANTIS_OK) return st;
-  const size_t cap = (size_t)(n > 0 ? n : 1);
-  if (cap > c->dense_cap) {
-    (void)hipFree(c->d_dense_c2w);
-    (void)hipFree(c->d_dense_err);
-    (void)hipFree(c->d_dense_np);
-    c->d_dense_c2w = nullptr;
-    c->d_dense_err = nullptr;
-    c->d_dense_np = nullptr;
-    c->dense_cap = 0;
-    if (dalloc(c, &c->d_dense_c2w, 12 * cap) != MANTIS_OK || dalloc(c, &c->d_dense_err, cap) != MANTIS_OK ||
-        dalloc(c, &c->d_dense_np, cap) != MANTIS_OK)
-      return MANTIS_ERR_OOM;
-    c->dense_cap = cap;
-  }
-  if (!c->d_pairs) {
-    if (dalloc(c, &c->d_pairs, (size_t)2 * 64) != MANTIS_OK) return MANTIS_ERR_OOM;
-    c->dense_pairs_cap = 128;
-  }
+  const int W = img->width, H = img->height;
   const uint8_t* d_mask = nullptr;
   const double* d_c2w = c->d_dense_c2w;
   if (dev) {
@@ -166,9 +176,7 @@ mantis_status score_argmin_impl(void* ctx, const mantis_image* img, const uint8_
   HIP_OK(hipGetLastError());
   int nr = 1;
   if (use_comm) {
-    const int cnt = c->nranks;  // checked against ncclCommCount in mantis_comm_init
-    if (cnt < 1 || cnt > 63) { c->err = "argmin exchange supports 1..63 ranks"; return MANTIS_ERR_ARG; }
-    nr = cnt;
+    nr = c->nranks;  // checked against ncclCommCount in mantis_comm_init, range checked above
     ncclResult_t r = ncclAllGather(c->d_pairs, c->d_pairs + 2, 2, ncclFloat64, (ncclComm_t)c->comm, c->s);
     if (r != ncclSuccess) { c->err = std::string("ncclAllGather: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
     mark(c, "allgather");
@@ -191,53 +199,63 @@ mantis_status mantis_score_argmin_batch(void* ctx, const mantis_image* imgs, int
   if (c) bind_device(c);
   if (!c || !imgs || n_frames <= 0 || !c2w_dev || !n_hyps || !index_base || !best_err || !best_idx)
     return MANTIS_ERR_ARG;
-  if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
   if (use_comm && !c->comm) { c->err = "comm not initialised (mantis_comm_init)"; return MANTIS_ERR_STATE; }
-  if (use_comm && (c->nranks < 1 || c->nranks > 63)) { c->err = "argmin exchange supports 1..63 ranks"; return MANTIS_ERR_ARG; }
-  int W, H;
-  mantis_status st = stage_frames(c, imgs, n_frames, W, H);
-  if (st != MANTIS_OK) return st;
   std::vector<DenseJob> jobs(n_frames);
-  size_t tot = 0;
   int maxn = 0;
-  for (int f = 0; f < n_frames; f++) {
-    if (n_hyps[f] < 0 || (n_hyps[f] > 0 && !c2w_dev[f])) return MANTIS_ERR_ARG;
-    jobs[f] = DenseJob{masks_dev ? masks_dev[f] : nullptr, c2w_dev[f], n_hyps[f], (int32_t)tot, index_base[f]};
-    tot += (size_t)n_hyps[f];
-    maxn = std::max(maxn, n_hyps[f]);
-  }
-  if (tot > (size_t)INT32_MAX) return MANTIS_ERR_ARG;
-  const size_t cap = std::max<size_t>(tot, 1);
-  if (cap > c->dense_cap) {
-    (void)hipFree(c->d_dense_err);
-    (void)hipFree(c->d_dense_np);
-    (void)hipFree(c->d_dense_c2w);
-    c->d_dense_err = c->d_dense_c2w = nullptr;
-    c->d_dense_np = nullptr;
-    c->dense_cap = 0;
-    if (dalloc(c, &c->d_dense_c2w, 12 * cap) != MANTIS_OK || dalloc(c, &c->d_dense_err, cap) != MANTIS_OK ||
-        dalloc(c, &c->d_dense_np, cap) != MANTIS_OK)
-      return MANTIS_ERR_OOM;
-    c->dense_cap = cap;
-  }
-  // at least the single-frame call's 64 pairs (mantis_score_argmin shares d_pairs)
-  const size_t pair_cap = std::max<size_t>((size_t)2 * n_frames * (use_comm ? c->nranks + 1 : 1), 128);
-  if (pair_cap > c->dense_pairs_cap) {
-    (void)hipFree(c->d_pairs);
-    c->d_pairs = nullptr;
-    c->dense_pairs_cap = 0;
-    if (dalloc(c, &c->d_pairs, pair_cap) != MANTIS_OK) return MANTIS_ERR_OOM;
-    c->dense_pairs_cap = pair_cap;
-  }
-  // the job table has its own capacity: d_pairs may already be large enough
-  // (single-frame call) when the first batch arrives
-  if ((size_t)n_frames > c->dense_jobs_cap) {
-    (void)hipFree(c->d_dense_jobs);
-    c->d_dense_jobs = nullptr;
-    c->dense_jobs_cap = 0;
-    if (dalloc(c, (DenseJob**)&c->d_dense_jobs, (size_t)n_frames) != MANTIS_OK) return MANTIS_ERR_OOM;
-    c->dense_jobs_cap = (size_t)n_frames;
-  }
+  // every rank-local failure up to the exchange (a rejected image, a bad
+  // hypothesis block, an allocation) and the frame count are agreed on with
+  // the other ranks first (agree(), api.hip): ranks fail together instead of
+  // leaving the others in an all-gather, and never all-gather different sizes
+  const auto prepare = [&]() -> mantis_status {
+    if (!c->d_lm) { c->err = "map not set"; return MANTIS_ERR_STATE; }
+    if (use_comm && (c->nranks < 1 || c->nranks > 63)) { c->err = "argmin exchange supports 1..63 ranks"; return MANTIS_ERR_ARG; }
+    int W, H;
+    mantis_status st = stage_frames(c, imgs, n_frames, W, H);
+    if (st != MANTIS_OK) return st;
+    size_t tot = 0;
+    for (int f = 0; f < n_frames; f++) {
+      if (n_hyps[f] < 0 || (n_hyps[f] > 0 && !c2w_dev[f])) { c->err = "bad hypothesis block"; return MANTIS_ERR_ARG; }
+      jobs[f] = DenseJob{masks_dev ? masks_dev[f] : nullptr, c2w_dev[f], n_hyps[f], (int32_t)tot, index_base[f]};
+      tot += (size_t)n_hyps[f];
+      maxn = std::max(maxn, n_hyps[f]);
+    }
+    if (tot > (size_t)INT32_MAX) { c->err = "too many hypotheses in one batch"; return MANTIS_ERR_ARG; }
+    const size_t cap = std::max<size_t>(tot, 1);
+    if (cap > c->dense_cap) {
+      (void)hipFree(c->d_dense_err);
+      (void)hipFree(c->d_dense_np);
+      (void)hipFree(c->d_dense_c2w);
+      c->d_dense_err = c->d_dense_c2w = nullptr;
+      c->d_dense_np = nullptr;
+      c->dense_cap = 0;
+      if (dalloc(c, &c->d_dense_c2w, 12 * cap) != MANTIS_OK || dalloc(c, &c->d_dense_err, cap) != MANTIS_OK ||
+          dalloc(c, &c->d_dense_np, cap) != MANTIS_OK)
+        return MANTIS_ERR_OOM;
+      c->dense_cap = cap;
+    }
+    // at least the single-frame call's 64 pairs (mantis_score_argmin shares d_pairs)
+    const size_t pair_cap = std::max<size_t>((size_t)2 * n_frames * (use_comm ? c->nranks + 1 : 1), 128);
+    if (pair_cap > c->dense_pairs_cap) {
+      (void)hipFree(c->d_pairs);
+      c->d_pairs = nullptr;
+      c->dense_pairs_cap = 0;
+      if (dalloc(c, &c->d_pairs, pair_cap) != MANTIS_OK) return MANTIS_ERR_OOM;
+      c->dense_pairs_cap = pair_cap;
+    }
+    // the job table has its own capacity: d_pairs may already be large enough
+    // (single-frame call) when the first batch arrives
+    if ((size_t)n_frames > c->dense_jobs_cap) {
+      (void)hipFree(c->d_dense_jobs);
+      c->d_dense_jobs = nullptr;
+      c->dense_jobs_cap = 0;
+      if (dalloc(c, (DenseJob**)&c->d_dense_jobs, (size_t)n_frames) != MANTIS_OK) return MANTIS_ERR_OOM;
+      c->dense_jobs_cap = (size_t)n_frames;
+    }
+    return MANTIS_OK;
+  };
+  mantis_status st = prepare();
+  if (use_comm) st = agree(c, st, n_frames);
+  if (st != MANTIS_OK) return st;
   DenseJob* d_jobs = (DenseJob*)c->d_dense_jobs;
   HIP_OK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(DenseJob) * n_frames, hipMemcpyHostToDevice, c->s));
   Landmarks L = lmk_of(c);

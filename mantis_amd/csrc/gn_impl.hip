@@ -373,7 +373,7 @@ mantis_status mantis_comm_init(void* ctx, const void* id128, int32_t nranks, int
   }
   // the failure flag of the sharded call's agreement steps (agree(), api.hip):
   // allocated here so agreeing never needs an allocation
-  if (!c->d_agree && dalloc(c, &c->d_agree, 1) != MANTIS_OK) {
+  if (!c->d_agree && dalloc(c, &c->d_agree, 4) != MANTIS_OK) {
     (void)ncclCommDestroy(comm);
     return MANTIS_ERR_OOM;
   }

@@ -36,6 +36,26 @@ int hc_rpp(const double* model, const double* iprts, double* R, double* t, doubl
   return r.status;
 }
 
+// RPP::Rpp on n points (4..12) through the per-count instances mantis_rpp_solve runs
+int hc_rpp_n(const double* model, const double* iprts, int n, double* R, double* t, double* errs, int* err_code) {
+  mk::rpp::Result r;
+  switch (n) {
+    case 4: r = mk::rpp::solve(model, iprts); break;
+#define MK_HC_RPP(k) \
+    case k: r = mk::rpp::n##k::solve(model, iprts); break;
+    MK_RPP_INSTANCES(MK_HC_RPP)
+#undef MK_HC_RPP
+    default: return -100;
+  }
+  std::memcpy(R, r.R, sizeof(r.R));
+  std::memcpy(t, r.t, sizeof(r.t));
+  errs[0] = r.obj_err;
+  errs[1] = r.img_err;
+  errs[2] = r.iterations;
+  *err_code = r.error;
+  return r.status;
+}
+
 // first ObjPose (stage1a): R[9], t[3], obj_err, img_err, iterations, Q after (12)
 void hc_first_objpose(const double* model, const double* iprts, double* R, double* t, double* errs, int32_t* it,
                       double* Qout) {
@@ -256,6 +276,24 @@ void hc_distort(const double* xyz, int n, const double* K, const double* D, doub
 void hc_undistort(const double* px, int n, const double* K, const double* D, double* out) {
   mk::Cam cm{(double)(float)K[0], (double)(float)K[4], (double)(float)K[2], (double)(float)K[5], {D[0], D[1], D[2], D[3]}};
   for (int i = 0; i < n; i++) mk::undistort(cm, px[2 * i], px[2 * i + 1], out + 2 * i, out + 2 * i + 1);
+}
+
+// screen constants (mk_screen.h screen_cam_from / screen_bounds): out = sens,
+// crel, S (per unit focal length), M; returns the bound's admissibility
+int hc_screen_consts(const double* K, const double* D, int pieces, double* out) {
+  mk::Cam cm;
+  cm.fx = (double)(float)K[0];
+  cm.fy = (double)(float)K[4];
+  cm.cx = (double)(float)K[2];
+  cm.cy = (double)(float)K[5];
+  for (int k = 0; k < 4; k++) cm.k[k] = D[k];
+  const mk::ScreenCam sc = mk::screen_cam_from(cm);
+  const mk::ScreenBounds b = mk::screen_bounds(cm.k, pieces);
+  out[0] = sc.sens;
+  out[1] = sc.crel;
+  out[2] = b.S;
+  out[3] = b.M;
+  return b.ok ? 1 : 0;
 }
 
 // FP32 projection screen (mk_screen.h) against the exact projection on n

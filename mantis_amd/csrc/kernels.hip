@@ -3125,6 +3125,49 @@ __global__ __launch_bounds__(256) void k_rpp_merge(const RppItem* __restrict__ i
   R.iterations = r.iterations;
 }
 
+// mantis_rpp_solve: RPP::Rpp (RPP.cpp:13-64) on N-point problems, the whole
+// solve on one lane (stage1 + candidate ObjPoses + merge, the same functions
+// the 4-point queues run in pieces). Off the per-frame path: it exists so any
+// point count the reference accepts runs the device code, e.g. demo.cpp:17-38's
+// 10-point known answer. img: n x N x 2 normalized (homogeneous z = 1, as
+// demo.cpp's Mat::ones and CoPlanarPoseEstimator.cpp:19-34 pack them), obj:
+// n x N x 3.
+template <int N> struct RppN;
+template <> struct RppN<4> {
+  static __device__ rpp::Result solve(const double* m, const double* q) { return rpp::solve(m, q); }
+};
+#define MK_RPP_SOLVE_N(k)                                                                         \
+  template <> struct RppN<k> {                                                                    \
+    static __device__ rpp::Result solve(const double* m, const double* q) { return rpp::n##k::solve(m, q); } \
+  };
+MK_RPP_INSTANCES(MK_RPP_SOLVE_N)
+#undef MK_RPP_SOLVE_N
+template <int N>
+__global__ __launch_bounds__(64) void k_rpp_solve(const double* __restrict__ img, const double* __restrict__ obj,
+                                                  int n, RppOut* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double model[3 * N], ip[3 * N];
+  for (int k = 0; k < N; k++) {
+    const size_t p = (size_t)i * N + k;
+    model[k] = obj[3 * p];
+    model[N + k] = obj[3 * p + 1];
+    model[2 * N + k] = obj[3 * p + 2];
+    ip[k] = img[2 * p];
+    ip[N + k] = img[2 * p + 1];
+    ip[2 * N + k] = 1.0;
+  }
+  const rpp::Result r = RppN<N>::solve(model, ip);
+  RppOut& R = out[i];
+  for (int k = 0; k < 9; k++) R.R[k] = r.R[k];
+  for (int k = 0; k < 3; k++) R.t[k] = r.t[k];
+  R.img_err = r.img_err;
+  R.obj_err = r.obj_err;
+  R.status = r.status;
+  R.error = r.error;
+  R.iterations = r.iterations;
+}
+
 // stage entry mantis_quad_gn: one lane per problem
 __global__ __launch_bounds__(256) void k_quad_gn(const double* __restrict__ img, const double* __restrict__ obj, int n,
                                                  double* __restrict__ R, double* __restrict__ t, int its,
@@ -3353,12 +3396,15 @@ __global__ __launch_bounds__(1024) void k_gauss_offsets_global(const int32_t* __
                                                                const int32_t* __restrict__ gidx, int n_local,
                                                                int per_frame, int32_t* total) {
   __shared__ int wsum[16];
+  __shared__ int bad;  // a pair names a frame >= ng: mk_shard.h offsets_from_pairs rejects the gather (-1)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) bad = 0;
   for (int i = t; i < ng; i += 1024) flags[i] = 0;
   __syncthreads();
   for (int i = t; i < npairs; i += 1024) {
     const int g = pairs[2 * i];
-    if (g >= 0 && g < ng) flags[g] = pairs[2 * i + 1];
+    if (g >= ng) bad = 1;
+    else if (g >= 0) flags[g] = pairs[2 * i + 1];
   }
   __syncthreads();
   const int chunk = (ng + 1023) / 1024;
@@ -3379,7 +3425,7 @@ __global__ __launch_bounds__(1024) void k_gauss_offsets_global(const int32_t* __
     flags[ng + f] = acc;
     if (flags[f]) acc += per_frame;
   }
-  if (t == 1023) *total = base + incl;
+  if (t == 1023) *total = bad ? -1 : base + incl;
   __syncthreads();
   for (int f = t; f < n_local; f += 1024) st[f].gauss_offset = flags[ng + gidx[f]];
 }

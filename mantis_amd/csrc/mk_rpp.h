@@ -877,240 +877,8 @@ MK_HD Mt<3, C> norm_rv(const Mt<3, C>& R) {
   return o;
 }
 
-constexpr int NP = 4;  // points per problem (a square's 4 corners)
-typedef Mt<3, NP> M34;
 typedef Mt<3, 3> M33;
 typedef Mt<3, 1> M31;
-
-// AbsKernel (RPP.cpp:229-332): overwrites P (re-centred) and Q (F_i q_i) in place
-#ifndef MK_OP_STAMP
-#define MK_OP_STAMP(k)
-#endif
-MK_HD void abs_kernel(M34& P, M34& Q, const M33* F, const M33& G, M33& R, M31& t, M34& Qout, double& err2) {
-  MK_OP_STAMP(0);
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    M31 q = mm(F[i], col(Q, i));
-#pragma unroll
-    for (int r = 0; r < 3; r++) Q(r, i) = q.a[r];
-  }
-  M31 pbar = scl(rowsum(P), 1.0 / NP);
-#pragma unroll
-  for (int i = 0; i < NP; i++)
-#pragma unroll
-    for (int r = 0; r < 3; r++) P(r, i) -= pbar.a[r];
-  M33 M = zeros<3, 3>();
-#pragma unroll
-  for (int i = 0; i < NP; i++)
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-      for (int b = 0; b < 3; b++) M(a, b) += P(a, i) * Q(b, i);
-  M33 U, V;
-  MK_OP_STAMP(1);
-  svd3(M, U, V);
-  MK_OP_STAMP(2);
-  M33 Ut = tr(U);
-  // ref: RPP.cpp:296-318. det(V U^T) > 0: try R = V U^T, and if t_z < 0
-  // flip V's 3rd column and take R = -(V U^T). Otherwise flip first, take
-  // R = V U^T and, if t_z < 0, R = -(V U^T). One EstimateT call site.
-  const bool pos = sgn(det3(mm(V, Ut))) == 1;
-  if (!pos) {
-#pragma unroll
-    for (int r = 0; r < 3; r++) V(r, 2) = -V(r, 2);
-  }
-  R = mm(V, Ut);
-#pragma unroll 1
-  for (int pass = 0; pass < 2; pass++) {
-    M31 sum = zeros<3, 1>();
-#pragma unroll
-    for (int i = 0; i < NP; i++) sum = add(sum, mm(mm(F[i], R), col(P, i)));
-    t = mm(G, sum);
-    if (pass == 1 || !(t.a[2] < 0)) break;
-    if (pos) {
-#pragma unroll
-      for (int r = 0; r < 3; r++) V(r, 2) = -V(r, 2);
-    }
-    R = mm(V, Ut, -1.0);
-  }
-  M33 I = eye3();
-  err2 = 0;
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    double x = P(0, i), y = P(1, i), z = P(2, i);
-    M31 qo;
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-      qo.a[r] = R(r, 0) * x + R(r, 1) * y + R(r, 2) * z + t.a[r];
-      Qout(r, i) = qo.a[r];
-    }
-    err2 += sqnorm3(mm(sub(I, F[i]), qo));
-  }
-  MK_OP_STAMP(3);
-}
-
-// ObjPose (RPP.cpp:66-208) as a resumable state machine: op_setup (everything
-// before the loop), op_step (one trip of the reference's do-while: the stop
-// test, then one AbsKernel), op_finish (obj_err, img_err, t re-centring). A GPU
-// lane can then hold one job, retire it when op_step reports done and pick up
-// the next (k_objpose_q); obj_pose below runs the same three functions in a
-// plain loop, so host checks and device kernels share every operation.
-constexpr double kObjTol = 1E-5, kObjEps = 1E-8;  // RPP.cpp:7-8
-constexpr int kObjCap = 100000;                    // the reference loop is unbounded
-struct OpState {
-  M34 P;          // model points, re-centred (AbsKernel re-centres them again every call)
-  M34 Qi;         // current projections (AbsKernel input and output)
-  double F6[NP][6];  // F_i = v v^T / (v^T v), symmetric: xx xy xz yy yz zz
-  M33 G;          // tFactor
-  M33 R;
-  M31 t, pbar;
-  double old_err, new_err;
-  double qx0, qy0;  // Qp(0,0), Qp(1,0) for img_err (Q2: column 0 only)
-  int it;
-  int init_pass, first;
-};
-MK_HD M33 f_full(const double* f) {
-  M33 F;
-  F.a[0] = f[0]; F.a[1] = f[1]; F.a[2] = f[2];
-  F.a[3] = f[1]; F.a[4] = f[3]; F.a[5] = f[4];
-  F.a[6] = f[2]; F.a[7] = f[4]; F.a[8] = f[5];
-  return F;
-}
-// Qp is rewritten to F_i q_i when there is no initial rotation (the first
-// AbsKernel runs on Qp itself, RPP.cpp:105-110); the caller keeps that copy.
-MK_HD void op_setup(const M34& P0, M34& Qp, const M33* initR, OpState& s) {
-  s.P = P0;
-  s.it = 0;
-  s.pbar = scl(rowsum(s.P), 1.0 / NP);
-#pragma unroll
-  for (int i = 0; i < NP; i++)
-#pragma unroll
-    for (int r = 0; r < 3; r++) s.P(r, i) -= s.pbar.a[r];
-  M33 F[NP];
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    M31 V = col(Qp, i);
-    double ret = mm(tr(V), V).a[0];
-    F[i] = mm(V, tr(V), 1.0 / ret);  // symmetric bit for bit (v_a v_b == v_b v_a)
-    s.F6[i][0] = F[i].a[0]; s.F6[i][1] = F[i].a[1]; s.F6[i][2] = F[i].a[2];
-    s.F6[i][3] = F[i].a[4]; s.F6[i][4] = F[i].a[5]; s.F6[i][5] = F[i].a[8];
-  }
-  M33 sumF = zeros<3, 3>();
-#pragma unroll
-  for (int i = 0; i < NP; i++) sumF = add(sumF, F[i]);
-  M33 I = eye3();
-  s.G = scl(inv3(sub(I, scl(sumF, 1.0 / NP))), 1.0 / NP);
-  s.old_err = 0;
-  s.init_pass = initR == nullptr;
-  if (initR) {
-    s.R = *initR;
-    M31 sm = zeros<3, 1>();
-#pragma unroll
-    for (int i = 0; i < NP; i++) sm = mmc(mm(sub(F[i], I), s.R), col(s.P, i), sm);
-    s.t = mm(s.G, sm);
-#pragma unroll
-    for (int i = 0; i < NP; i++) {
-      double x = s.P(0, i), y = s.P(1, i), z = s.P(2, i);
-      M31 qo;
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        qo.a[r] = s.R(r, 0) * x + s.R(r, 1) * y + s.R(r, 2) * z + s.t.a[r];
-        s.Qi(r, i) = qo.a[r];
-      }
-      s.old_err += sqnorm3(mm(sub(I, F[i]), qo));
-    }
-  } else {
-    s.Qi = Qp;
-    // what the first AbsKernel leaves in Qp: F_i q_i, computed as it does
-#pragma unroll
-    for (int i = 0; i < NP; i++) {
-      M31 q = mm(F[i], col(Qp, i));
-#pragma unroll
-      for (int r = 0; r < 3; r++) Qp(r, i) = q.a[r];
-    }
-  }
-  s.qx0 = Qp(0, 0);
-  s.qy0 = Qp(1, 0);
-  // the reference computes one AbsKernel before testing the stop rule
-  s.new_err = s.old_err;
-  s.first = 1;
-}
-// one loop trip; returns 0 while running, 1 converged, 2 iteration cap
-MK_HD int op_step(OpState& s) {
-  if (!s.first) {
-    if (!(fabs((s.old_err - s.new_err) / s.old_err) > kObjTol && (s.new_err > kObjEps))) return 1;
-    if (s.it >= kObjCap) return 2;
-    s.old_err = s.new_err;
-  }
-  M33 F[NP];
-#pragma unroll
-  for (int i = 0; i < NP; i++) F[i] = f_full(s.F6[i]);
-  abs_kernel(s.P, s.Qi, F, s.G, s.R, s.t, s.Qi, s.new_err);
-  s.it = s.it + 1;
-  if (s.init_pass) {
-    s.init_pass = 0;
-    s.old_err = s.new_err;
-  } else {
-    s.first = 0;
-  }
-  return 0;
-}
-MK_HD void op_finish(const OpState& s, M33& R, M31& t, double& obj_err, double& img_err) {
-  R = s.R;
-  obj_err = sqrt(s.new_err / NP);
-  img_err = 0;
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    M31 Qproj = mmc(s.R, col(s.P, i), s.t);
-    double xx = (Qproj.a[0] / Qproj.a[2]) - s.qx0;
-    double yy = (Qproj.a[1] / Qproj.a[2]) - s.qy0;
-    img_err += (xx * xx + yy * yy);
-  }
-  img_err = sqrt(img_err / NP);
-  t = sub(s.t, mm(s.R, s.pbar));
-}
-
-// ObjPose (RPP.cpp:66-208); returns 1 when the (reference-unbounded) loop hit the cap
-MK_HD int obj_pose(const M34& P0, M34& Qp, const M33* initR, M33& R, M31& t, int& it, double& obj_err,
-                   double& img_err) {
-  OpState s;
-  op_setup(P0, Qp, initR, s);
-  int r;
-#pragma unroll 1
-  while ((r = op_step(s)) == 0) {
-  }
-  op_finish(s, R, t, obj_err, img_err);
-  it = s.it;
-  return r == 2 ? 1 : 0;
-}
-
-// Predicted AbsKernel count of an ObjPose from its state (longest-first
-// scheduling of the persistent job queues, kernels.hip k_objpose_probe):
-// kprobe more steps on a copy, then the stop test |de/e| <= kObjTol
-// (RPP.cpp:171) extrapolated with the observed linear convergence rate of
-// |de/e| over the last kPredSpan steps. Scheduling only: the results always
-// come from the unchanged iteration.
-constexpr int kPredSpan = 4;
-MK_HD float op_predict(OpState s, int kprobe) {
-  double e[2 + kPredSpan];  // the last errors (ring)
-  int n = 0;
-#pragma unroll 1
-  for (int i = 0; i < kprobe; i++) {
-    if (op_step(s)) return (float)s.it;  // converged (or capped) inside the probe
-#pragma unroll
-    for (int j = 0; j < 1 + kPredSpan; j++) e[j] = e[j + 1];
-    e[1 + kPredSpan] = s.new_err;
-    n++;
-  }
-  if (n < 2 + kPredSpan) return 1e6f;
-  const double r1 = fabs((e[kPredSpan] - e[1 + kPredSpan]) / e[kPredSpan]);
-  const double r0 = fabs((e[0] - e[1]) / e[0]);
-  if (!(r1 > kObjTol)) return (float)(s.it + 1);
-  const double rho = (r0 > 0 && r1 < r0) ? pow(r1 / r0, 1.0 / kPredSpan) : 1.0;
-  if (!(rho < 0.99999)) return 1e6f;
-  const double rem = log(kObjTol / r1) / log(rho);
-  return (float)(s.it + (rem > 0 ? rem : 0) + 1);
-}
 
 MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
   double d = v2[0] * v1[0] + v2[1] * v1[1] + v2[2] * v1[2];
@@ -1166,80 +934,6 @@ MK_HD bool decompose_r(const M33& R, M33& RzN) {
   return true;
 }
 
-// GetRotationY_wrtT (RPP.cpp:947-1222): the 5 root slots of the quartic in
-// order with a keep flag (the reference's translation candidates are
-// overwritten by the following ObjPose and are not formed here).
-MK_HD void rot_y_wrt_t(const M34& v, const M34& p, const M33& Rz, double* al, bool* keep) {
-  M33 V[NP];
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    M31 vv = col(v, i);
-    double a = mm(tr(vv), vv).a[0];
-    V[i] = mm(vv, tr(vv), 1.0 / a);
-  }
-  M33 G = zeros<3, 3>();
-#pragma unroll
-  for (int i = 0; i < NP; i++) G = add(G, V[i]);
-  M33 I = eye3();
-  G = scl(inv3(sub(I, scl(G, 1.0 / NP))), 1.0 / NP);
-  M33 opt = zeros<3, 3>();
-  const double r1 = Rz(0, 0), r2 = Rz(0, 1), r3 = Rz(0, 2), r4 = Rz(1, 0), r5 = Rz(1, 1), r6 = Rz(1, 2),
-               r7 = Rz(2, 0), r8 = Rz(2, 1), r9 = Rz(2, 2);
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      double w1 = V[i](k, 0), w2 = V[i](k, 1), w3 = V[i](k, 2);
-      if (k == 0) w1 = w1 - 1; else if (k == 1) w2 = w2 - 1; else w3 = w3 - 1;
-      double px = p(0, i), py = p(1, i), pz = p(2, i);
-      opt(k, 0) += ((w1 * r2 + w2 * r5 + w3 * r8) * py + (-w1 * r1 - w2 * r4 - w3 * r7) * px +
-                    (-w1 * r3 - w2 * r6 - w3 * r9) * pz);
-      opt(k, 1) += ((2 * w1 * r1 + 2 * w2 * r4 + 2 * w3 * r7) * pz + (-2 * w1 * r3 - 2 * w2 * r6 - 2 * w3 * r9) * px);
-      opt(k, 2) += (w1 * r1 + w2 * r4 + w3 * r7) * px + (w1 * r3 + w2 * r6 + w3 * r9) * pz +
-                   (w1 * r2 + w2 * r5 + w3 * r8) * py;
-    }
-  }
-  opt = mm(G, opt);
-  double E2[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < NP; i++) {
-    double px = p(0, i), py = p(1, i), pz = p(2, i);
-    M33 Rpi;
-    Rpi(0, 0) = -px; Rpi(0, 1) = 2 * pz; Rpi(0, 2) = px;
-    Rpi(1, 0) = py;  Rpi(1, 1) = 0;      Rpi(1, 2) = py;
-    Rpi(2, 0) = -pz; Rpi(2, 1) = -2 * px; Rpi(2, 2) = pz;
-    M33 E = mm(sub(I, V[i]), mmc(Rz, Rpi, opt));
-    double s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0;
-#pragma unroll
-    for (int r = 0; r < 3; r++) s1 += E(r, 0) * E(r, 0);
-#pragma unroll
-    for (int r = 0; r < 3; r++) s2 += 2 * (E(r, 1) * E(r, 0));
-#pragma unroll
-    for (int r = 0; r < 3; r++) s3 += (E(r, 2) * E(r, 0)) * 2 + E(r, 1) * E(r, 1) + 0.0;
-#pragma unroll
-    for (int r = 0; r < 3; r++) s4 += 2 * (E(r, 2) * E(r, 1));
-#pragma unroll
-    for (int r = 0; r < 3; r++) s5 += E(r, 2) * E(r, 2);
-    E2[0] += s1; E2[1] += s2; E2[2] += s3; E2[3] += s4; E2[4] += s5;
-  }
-  double e4 = E2[0], e3 = E2[1], e2 = E2[2], e1 = E2[3], e0 = E2[4];
-  double a4 = -e3, a3 = (4 * e4 - 2 * e2), a2 = (-3 * e1 + 3 * e3), a1 = (-4 * e0 + 2 * e2), a0 = e1;
-  double coeffs[5] = {a4, a3, a2, a1, a0};
-  double zr[5] = {0, 0, 0, 0, 0}, zi[5] = {0, 0, 0, 0, 0};
-  rpoly(coeffs, 4, zr, zi);
-#pragma unroll
-  for (int i = 0; i < 5; i++) {
-    double a = zr[i];
-    double p1 = pow(1.0 + a * a, 3.0);
-    bool k1 = fabs(p1) > 0.1 && zi[i] == 0;
-    double sa = (2.0 * a) / (1.0 + a * a);
-    double ca = (1.0 - a * a) / (1.0 + a * a);
-    al[i] = atan2(sa, ca) * 180 / M_PI;
-    double tMaxMin = (4 * a4 * a * a * a + 3 * a3 * a * a + 2 * a2 * a + a1);
-    keep[i] = k1 && tMaxMin > 0;
-  }
-}
-
 struct Result {
   double R[9], t[3];
   double obj_err, img_err;
@@ -1248,164 +942,44 @@ struct Result {
   int error;   // 0; 1 GetRotationbyVector failed (reference exit(1)); 2 iteration cap; 3 no best
 };
 
-// RPP::Rpp (RPP.cpp:13-64) split in three phases so the GPU runs each with a
-// small live state: stage1 = first ObjPose + Get2ndPose_Exact up to the
-// candidate rotations; refine = one ObjPose per candidate (independent work
-// items); merge = the reference's ordered lowest-obj_err selection.
-constexpr int kCand = 5;
-struct Stage1 {
-  double Q[3 * NP];         // iprts after the first ObjPose (AbsKernel rewrote it)
-  double R[9], t[3], obj_err, img_err;
-  double sR[kCand][9];      // initial rotations of the 2nd-pose candidates
-  int iterations, error;    // error: 0 / 1 (GetRotationbyVector) / 2 (cap)
-  int keep_mask;            // bit j: candidate j enters the search
-  int pad;
-};
-struct Refine {
-  double R[9], t[3], obj_err, img_err;
-  int iterations, capped;
-};
+constexpr int NP = 4;  // points per problem (a square's 4 corners)
+#include "mk_rpp_np.inc"
 
-// first ObjPose (no initial rotation)
-MK_HD void stage1a(const double* model, const double* iprts, Stage1& s) {
-  M34 P, Q;
-#pragma unroll
-  for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Q.a[i] = iprts[i]; }
-  M33 R;
-  M31 t;
-  int it = 0;
-  double oe = 0, ie = 0;
-  int capped = obj_pose(P, Q, nullptr, R, t, it, oe, ie);
-#pragma unroll
-  for (int k = 0; k < 3 * NP; k++) s.Q[k] = Q.a[k];
-#pragma unroll
-  for (int k = 0; k < 9; k++) s.R[k] = R.a[k];
-#pragma unroll
-  for (int k = 0; k < 3; k++) s.t[k] = t.a[k];
-  s.obj_err = oe;
-  s.img_err = ie;
-  s.iterations = it;
-  s.error = capped ? 2 : 0;
-  s.keep_mask = 0;
-}
-
-// Get2ndPose_Exact up to the candidate rotations (RPP.cpp:693-753)
-MK_HD void stage1b(const double* model, Stage1& s) {
-  M34 P, Q;
-  M33 R;
-#pragma unroll
-  for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Q.a[i] = s.Q[i]; }
-#pragma unroll
-  for (int k = 0; k < 9; k++) R.a[k] = s.R[k];
-  Mt<NP, 3> nv = tr(norm_rv(Q));
-  M31 mean;
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    double sm = 0;
-#pragma unroll
-    for (int i = 0; i < NP; i++) sm += nv(i, j);
-    mean.a[j] = sm / 3;
-  }
-  M31 cent = norm_rv(mean);
-  double c3[3] = {cent.a[0], cent.a[1], cent.a[2]}, z[3] = {0, 0, 1};
-  M33 Rim;
-  if (!rot_by_vector(z, c3, Rim)) { s.error = 1; return; }
-  M34 v_ = mm(Rim, Q);
-  M33 R_ = mm(Rim, R);
-  M33 RzN;
-  if (!decompose_r(R_, RzN)) return;
-  M33 R2 = mm(R_, RzN);
-  M34 P_ = mm(tr(RzN), P);
-  double ang[3];
-  if (!rpy_ang_x(R2, ang)) return;
-  M33 Rz = rpy_mat(0, 0, ang[2]);
-  double bl[kCand];
-  bool keep[kCand];
-  rot_y_wrt_t(v_, P_, Rz, bl, keep);
-  M33 RimT = tr(Rim);
-  M33 RzNt = tr(RzN);
-  int mask = 0;
-#pragma unroll 1
-  for (int j = 0; j < kCand; j++) {
-    if (!keep[j]) continue;
-    double b = bl[j] / 180 * M_PI;
-    M33 sR = mm(RimT, mm(mm(Rz, rpy_mat(0, b, 0)), RzNt));
-#pragma unroll
-    for (int k = 0; k < 9; k++) s.sR[j][k] = sR.a[k];
-    mask |= 1 << j;
-  }
-  s.keep_mask = mask;
-}
-
-MK_HD void stage1(const double* model, const double* iprts, Stage1& s) {
-  stage1a(model, iprts, s);
-  stage1b(model, s);
-}
-
-MK_HD void refine(const double* model, const double* Q, const double* sR, Refine& r) {
-  M34 P, Qp;
-#pragma unroll
-  for (int i = 0; i < 3 * NP; i++) { P.a[i] = model[i]; Qp.a[i] = Q[i]; }
-  M33 R0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) R0.a[k] = sR[k];
-  M33 Rl;
-  M31 tl;
-  int it = 0;
-  double oe = 0, ie = 0;
-  r.capped = obj_pose(P, Qp, &R0, Rl, tl, it, oe, ie);
-#pragma unroll
-  for (int k = 0; k < 9; k++) r.R[k] = Rl.a[k];
-#pragma unroll
-  for (int k = 0; k < 3; k++) r.t[k] = tl.a[k];
-  r.obj_err = oe;
-  r.img_err = ie;
-  r.iterations = it;
-}
-
-// ref: RPP.cpp:40-63 — candidates in order, strict "<" on obj_err from 1e6;
-// the reported iteration count is the last ObjPose's (the variable is shared)
-MK_HD Result merge(const Stage1& s, const Refine* rf) {
-  Result res;
-  for (int k = 0; k < 9; k++) res.R[k] = s.R[k];
-  for (int k = 0; k < 3; k++) res.t[k] = s.t[k];
-  res.obj_err = s.obj_err;
-  res.img_err = s.img_err;
-  res.iterations = s.iterations;
-  res.status = 0;
-  res.error = s.error;
-  if (s.error == 1 || s.keep_mask == 0) return res;
-  int best = -1;
-  double lowest = 1e6;
-  for (int j = 0; j < kCand; j++) {
-    if (!(s.keep_mask >> j & 1)) continue;
-    if (rf[j].capped) res.error = 2;
-    if (rf[j].obj_err < lowest) { lowest = rf[j].obj_err; best = j; }
-  }
-  if (best < 0) { res.error = 3; return res; }
-  const Refine& b = rf[best];
-  for (int k = 0; k < 9; k++) res.R[k] = b.R[k];
-  for (int k = 0; k < 3; k++) res.t[k] = b.t[k];
-  res.obj_err = b.obj_err;
-  res.img_err = b.img_err;
-  int last = 0;
-  for (int j = 0; j < kCand; j++)
-    if (s.keep_mask >> j & 1) last = j;
-  res.iterations = rf[last].iterations;
-  res.status = 1;
-  return res;
-}
-
-// RPP::Rpp (RPP.cpp:13-64) on model/iprts given as 3 x 4 row-major (host checks)
-MK_HD Result solve(const double* model, const double* iprts) {
-  Stage1 s;
-  stage1(model, iprts, s);
-  Refine rf[kCand];
-  if (s.error != 1)
-    for (int j = 0; j < kCand; j++)
-      if (s.keep_mask >> j & 1) refine(model, s.Q, s.sR[j], rf[j]);
-  return merge(s, rf);
-}
+// n-point instances (mantis_rpp_solve: RPP::Rpp on any point count the
+// reference accepts, e.g. demo.cpp:17-38's 10-point known answer)
+#define MK_RPP_INSTANCES(X) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+namespace n5 {
+constexpr int NP = 5;
+#include "mk_rpp_np.inc"
+}  // namespace n5
+namespace n6 {
+constexpr int NP = 6;
+#include "mk_rpp_np.inc"
+}  // namespace n6
+namespace n7 {
+constexpr int NP = 7;
+#include "mk_rpp_np.inc"
+}  // namespace n7
+namespace n8 {
+constexpr int NP = 8;
+#include "mk_rpp_np.inc"
+}  // namespace n8
+namespace n9 {
+constexpr int NP = 9;
+#include "mk_rpp_np.inc"
+}  // namespace n9
+namespace n10 {
+constexpr int NP = 10;
+#include "mk_rpp_np.inc"
+}  // namespace n10
+namespace n11 {
+constexpr int NP = 11;
+#include "mk_rpp_np.inc"
+}  // namespace n11
+namespace n12 {
+constexpr int NP = 12;
+#include "mk_rpp_np.inc"
+}  // namespace n12
 
 }  // namespace rpp
 }  // namespace mk

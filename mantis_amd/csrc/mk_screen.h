@@ -22,17 +22,19 @@
 //    FP32: |dp_i| <= ez = 6 u (|X|_1 + |t|_1) per coordinate (|R_ij| <= 1);
 //  * the pixel depends on p only through its direction: a direction error of
 //    |dp| / |p| rad moves it by at most S px, S = f_max * max over theta in
-//    [0, pi/2] of max(theta_d'(theta), theta_d(theta) / sin theta) (host-side,
-//    ScreenCam.sens carries 2.2 S: sqrt(3) for the three coordinates, the
-//    rest margin);
+//    [0, pi/2] of max(theta_d'(theta), theta_d(theta) / sin theta)
+//    (ScreenCam.sens carries 2.2 S: sqrt(3) for the three coordinates, the
+//    rest margin). S is an upper bound derived by interval subdivision
+//    (screen_cam_from), not a sample;
 //  * the FP32 evaluation itself: theta = atan2(rho, z) to <= 8 u rad (degree-6
 //    minimax polynomial, 4.9e-8 rad, plus the roundings of q = min / max and of
 //    pi/2 - atan), charged 16 u * S; the scale theta_d / rho and the products
-//    to <= 7 u relative of (u - cx), charged 24 u |u - cx|; the final add
-//    0.5 u |u|, charged 2 u |u|.
-// tools/check_screen.hip validates the bound on the GPU (hardware rcp / rsq,
-// ~2^32 projections from the scorers' pose distributions and from uniform
-// random poses): no decision taken by the screen differs from distort()'s.
+//    to <= (8 + 9 M) u relative of (u - cx), M = max over theta of
+//    (1 + sum |k_i| theta^(2i+2)) / F(theta), F = 1 + sum k_i theta^(2i+2)
+//    (Horner with FMAs over theta^2 with one rounding, coefficients rounded to
+//    FP32: the cancellation in F is what M measures), charged
+//    crel = max(24, 1.25 (8 + 9 M)) u |u - cx|; the final add 0.5 u |u|,
+//    charged 2 u |u|.
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -45,7 +47,7 @@ struct ScreenCam {
   float fx, fy, cx, cy;
   float k[4];
   float sens;   // 2.2 * S px per radian (see above); +inf disables the screen (every landmark unsure)
-  float cabs;   // unused padding to 16-byte multiple
+  float crel;   // relative error charge of the scale chain, max(24, 1.25 (8 + 9 M)) u (see above)
   float pad[2];
 };
 struct PoseF {   // c2w as FP32: rows of R, t, |t|_1
@@ -124,7 +126,7 @@ MK_HD ScrUV screen_uv(const PoseF& P, float X, float Y, float Z, float xn, const
   r.u = du + c.cx;
   r.v = dv + c.cy;
   r.eps = fmaf(c.sens, fmaf(ez, rinv, 16.0f * kScrU),
-               fmaf(24.0f * kScrU, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(r.u) + fabsf(r.v))));
+               fmaf(c.crel, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(r.u) + fabsf(r.v))));
   r.state = 1;
   return r;
 }
@@ -161,7 +163,7 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   const float du = c.fx * (x * sc), dv = c.fy * (y * sc);
   const float u = du + c.cx, v = dv + c.cy;
   const float eps = fmaf(c.sens, fmaf(ez, rinv, 16.0f * kScrU),
-                         fmaf(24.0f * kScrU, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(u) + fabsf(v))));
+                         fmaf(c.crel, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(u) + fabsf(v))));
   // z certainly > 0, off the optical axis, and a bound below 1/4 px: the FP32
   // values are meaningful (NaN / inf fail every comparison)
   const bool valid = (int)(z > ez) & (int)(rho2 > 1e-12f * z2) & (int)(eps < 0.25f);
@@ -185,33 +187,64 @@ MK_HD void screen_landmark(const double* X, float* o) {
   o[3] = (float)((fabs(X[0]) + fabs(X[1]) + fabs(X[2])) * 1.0000001);
 }
 
-// Host: the screen constants of a camera. S = f_max * max(theta_d', theta_d /
-// sin theta) over [0, pi/2], sampled densely with a 5 % margin; a distortion
-// whose theta_d is not increasing and positive there disables the screen.
+// Host: the screen constants of a camera, from bounds derived over [0, pi/2]
+// by interval subdivision. On a piece theta in [a, b], x = theta^2 in
+// [a^2, b^2]: every term c x^j of theta_d'(theta) = 1 + sum (2i+3) k_i x^(i+1),
+// of F(theta) = 1 + sum k_i x^(i+1) and of A(theta) = sum |k_i| x^(i+1) is
+// monotone in x >= 0, so the sum of the per-term maxima (minima) over the
+// piece's ends bounds the polynomial from above (below) on the whole piece;
+// theta / sin theta is increasing, so b / sin b bounds it. Then
+//   S >= max(theta_d', theta_d / sin theta)  (upper bounds of both per piece),
+//   M >= (1 + A) / F                           (upper bound of 1 + A over the
+//                                              lower bound of F per piece),
+// and the model needs theta_d increasing and positive: a piece whose lower
+// bound of theta_d' or of F is not > 0 disables the screen (sens = inf: every
+// landmark takes the exact path). The double arithmetic of the bounds is
+// covered by a 1e-9 relative margin.
+struct ScreenBounds {
+  double S, M;  // S per unit focal length; M as above
+  bool ok;
+};
+MK_HD ScreenBounds screen_bounds(const double* k, int pieces = 4096) {
+  ScreenBounds r{1.0, 1.0, true};
+  const double half_pi = 1.5707963267948966;
+  for (int i = 0; i < pieces; i++) {
+    const double a = half_pi * i / pieces, b = fmin(half_pi, half_pi * (i + 1) / pieces * (1 + 1e-15));
+    const double xa = a * a, xb = b * b;
+    double dhi = 1, dlo = 1, Fhi = 1, Flo = 1, Ahi = 0, pa = xa, pb = xb;
+    for (int j = 0; j < 4; j++) {
+      const double ta = k[j] * pa, tb = k[j] * pb;
+      const double mx = fmax(ta, tb), mn = fmin(ta, tb);
+      dhi += (2 * j + 3) * mx;
+      dlo += (2 * j + 3) * mn;
+      Fhi += mx;
+      Flo += mn;
+      Ahi += fmax(fabs(ta), fabs(tb));
+      pa *= xa;
+      pb *= xb;
+    }
+    if (!(dlo > 0) || !(Flo > 0)) r.ok = false;  // also false for NaN
+    const double ratio = b / sin(b);
+    r.S = fmax(r.S, fmax(dhi, ratio * Fhi));
+    r.M = fmax(r.M, (1 + Ahi) / Flo);
+  }
+  r.S *= 1 + 1e-9;
+  r.M *= 1 + 1e-9;
+  return r;
+}
 MK_HD ScreenCam screen_cam_from(const Cam& cm) {
   ScreenCam s;
   s.fx = (float)cm.fx; s.fy = (float)cm.fy; s.cx = (float)cm.cx; s.cy = (float)cm.cy;
   for (int k = 0; k < 4; k++) s.k[k] = (float)cm.k[k];
-  s.cabs = 0.f;
   s.pad[0] = s.pad[1] = 0.f;
-  const auto thd = [&](double t) {
-    const double t2 = t * t;
-    return t * (1.0 + t2 * (cm.k[0] + t2 * (cm.k[1] + t2 * (cm.k[2] + t2 * cm.k[3]))));
-  };
-  double S = 1.0, prev = 0.0;
   bool ok = cm.fx > 0 && cm.fy > 0 && cm.fx < 1e30 && cm.fy < 1e30;  // also false for NaN
-  const int N = 4096;
-  for (int i = 1; i <= N && ok; i++) {
-    const double t = 1.5707963267948966 * i / N, h = 1e-6;
-    const double d = thd(t), dd = (thd(t + h) - thd(t - h)) / (2 * h);
-    if (!(d > prev) || !(dd > 0)) ok = false;
-    prev = d;
-    S = fmax(S, fmax(dd, d / sin(t)));
-  }
   // the fp32 coefficients must reproduce theta_d closely: |k| bounded
   for (int k = 0; k < 4; k++) ok = ok && fabs(cm.k[k]) < 1.0;
+  const ScreenBounds b = ok ? screen_bounds(cm.k) : ScreenBounds{1.0, 1.0, false};
+  ok = ok && b.ok && b.M < 1e4;
   const double f = fmax(cm.fx, cm.fy);
-  s.sens = ok ? (float)(2.2 * 1.05 * S * f) : INFINITY;
+  s.sens = ok ? (float)(2.2 * b.S * f) : INFINITY;
+  s.crel = (float)(fmax(24.0, 1.25 * (8.0 + 9.0 * b.M)) * 5.9604644775390625e-8);
   return s;
 }
 

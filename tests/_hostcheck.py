@@ -20,6 +20,7 @@ def lib():
             raise RuntimeError("hostcheck not built: run `make tools`")
         L = C.CDLL(HC_SO)
         L.hc_rpp.restype = C.c_int
+        L.hc_rpp_n.restype = C.c_int
         L.hc_rpoly.restype = C.c_int
         L.hc_approx.restype = C.c_int
         L.hc_approx.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int]
@@ -43,6 +44,8 @@ def lib():
         L.hc_shard_offsets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p]
         L.hc_shard_merge.restype = C.c_int
         L.hc_screen_check.restype = C.c_int
+        L.hc_screen_consts.restype = C.c_int
+        L.hc_screen_consts.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.hc_screen_check.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                       C.c_void_p]
         _lib = L
@@ -62,6 +65,19 @@ def rpp(model, iprts):
     e = np.zeros(3)
     code = C.c_int(0)
     st = lib().hc_rpp(_d(model), _d(iprts), _d(R), _d(t), _d(e), C.byref(code))
+    return st, R.reshape(3, 3), t, e, code.value
+
+
+def rpp_n(model, iprts):
+    """RPP::Rpp on 3 x n problems, n in 4..12 (the device code's host build)."""
+    model = np.ascontiguousarray(model, np.float64)
+    iprts = np.ascontiguousarray(iprts, np.float64)
+    n = model.shape[1]
+    R = np.zeros(9)
+    t = np.zeros(3)
+    e = np.zeros(3)
+    code = C.c_int(0)
+    st = lib().hc_rpp_n(_d(model), _d(iprts), C.c_int(n), _d(R), _d(t), _d(e), C.byref(code))
     return st, R.reshape(3, 3), t, e, code.value
 
 
@@ -178,6 +194,15 @@ def screen_check(c2w, X, K, D, W, H):
     bad = lib().hc_screen_check(c2w.ctypes.data, X.ctypes.data, len(X), K.ctypes.data, D.ctypes.data, W, H,
                                 res.ctypes.data)
     return bad, res
+
+
+def screen_consts(K, D, pieces=4096):
+    """(admissible, sens, crel, S, M) of mk_screen.h screen_cam_from / screen_bounds."""
+    K = np.ascontiguousarray(K, np.float64).reshape(9)
+    D = np.ascontiguousarray(D, np.float64).reshape(4)
+    out = np.zeros(4)
+    ok = lib().hc_screen_consts(K.ctypes.data, D.ctypes.data, int(pieces), out.ctypes.data)
+    return bool(ok), out[0], out[1], out[2], out[3]
 
 
 # cross-rank bookkeeping of mantis_process_rig_sharded (mantis_amd/csrc/mk_shard.h)

@@ -195,5 +195,12 @@ def test_gauss_offsets_global_fabricated_gathers():
                 off, tot = m.shard_gauss_offsets(pairs, ng, locals_[r], per)
                 assert np.array_equal(off, seq[locals_[r]]), f"world {world} rank {r}"
                 assert tot == tot_host
+            # a malformed gather (a frame index >= n_global) is rejected by both
+            # halves: the host rule returns -1, the entry point an error
+            badp = pairs.copy()
+            badp[0] = ng
+            assert HC.shard_offsets(badp, ng, per)[2] == -1
+            with pytest.raises(M.MantisError, match="pair index"):
+                m.shard_gauss_offsets(badp, ng, locals_[0], per)
     finally:
         m.close()

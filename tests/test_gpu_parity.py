@@ -272,6 +272,67 @@ def test_rpp_batch_matches_oracle(mantis):
         np.testing.assert_allclose(e[k], re[:2], rtol=1e-9, atol=1e-15)
 
 
+def test_rpp_demo_known_answer_on_gpu(mantis):
+    """The reference's only known answer on the hot path, run by the device
+    RPP: demo.cpp:17-38's 10-point problem (mantis_rpp_solve, mk_rpp.h's
+    functions instantiated for 10 points) against demo.cpp's Matlab R, t
+    (printed to 5 decimals: 1e-4 + half a printed unit) and against the oracle."""
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rpp_demo.npz"),
+                allow_pickle=False)
+    R, t, e, st, it = mantis.rpp_solve(d["model"], d["iprts"])
+    assert st[0] == 1
+    np.testing.assert_allclose(R[0], d["matlab_R"], atol=1e-4 + 5e-6, rtol=0)
+    np.testing.assert_allclose(t[0], d["matlab_t"], atol=1e-4 + 5e-6, rtol=0)
+    ost, oR, ot, oe, code = O.rpp(d["model"], d["iprts"])
+    assert ost == 1 and code == 0
+    np.testing.assert_allclose(R[0], oR, atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(t[0], ot, atol=POSE_TOL, rtol=0)
+    np.testing.assert_allclose(e[0], oe[:2], rtol=1e-9, atol=1e-15)
+    assert it[0] == int(oe[2])
+    # the committed fixture is the oracle's output for this problem
+    np.testing.assert_allclose(R[0], d["R"], atol=POSE_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("npts", [4, 5, 7, 10, 12])
+def test_rpp_solve_n_points_matches_oracle(mantis, npts):
+    """mantis_rpp_solve on random planar n-point problems (noisy projections of
+    a random plane patch) against the oracle's RPP::Rpp restatement; n = 4 also
+    against mantis_rpp_batch (the queue path runs the same functions)."""
+    rng = np.random.default_rng(100 + npts)
+    models, iprts, refs = [], [], []
+    for k in range(48):
+        m = np.vstack([rng.uniform(-0.8, 0.8, size=(2, npts)), np.zeros((1, npts))])
+        R0 = synth.rot_z(rng.uniform(0, 6.28)) @ synth.NADIR @ synth.rot_x(rng.normal() * 0.4)
+        t0 = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(2, 12)])
+        Q = R0.T @ m + t0[:, None]
+        ip = np.vstack([Q[0] / Q[2], Q[1] / Q[2], np.ones(npts)])
+        ip[:2] += rng.normal(size=(2, npts)) * 0.002
+        models.append(m)
+        iprts.append(ip)
+        refs.append(O.rpp(m, ip))
+    R, t, e, st, it = mantis.rpp_solve(np.array(models), np.array(iprts))
+    for k, (rs, rR, rt, re, code) in enumerate(refs):
+        assert st[k] == (-1 if code == 1 else rs), k
+        np.testing.assert_allclose(R[k], rR, atol=POSE_TOL, rtol=0)
+        np.testing.assert_allclose(t[k], rt, atol=POSE_TOL * max(1.0, np.abs(rt).max()), rtol=0)
+        np.testing.assert_allclose(e[k], re[:2], rtol=1e-9, atol=1e-15)
+        assert it[k] == int(re[2]), k
+    if npts == 4:
+        img = np.array([ip[:2].T for ip in iprts])
+        obj = np.array([m.T for m in models])
+        Rb, tb, eb, sb = mantis.rpp(img, obj)
+        assert np.array_equal(Rb, R) and np.array_equal(tb, t) and np.array_equal(eb, e) and np.array_equal(sb, st)
+
+
+def test_rpp_solve_rejects_bad_point_counts(mantis):
+    import mantis_amd as M
+
+    m = np.zeros((3, 13))
+    q = np.ones((3, 13))
+    with pytest.raises(M.MantisError):
+        mantis.rpp_solve(m, q)
+
+
 def test_scoring_matches_oracle(mantis, frames, landmark_map):
     orc = O.Oracle(*landmark_map)
     K, D = synth.intrinsics()

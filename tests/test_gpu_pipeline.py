@@ -638,6 +638,22 @@ def test_dense_batch_matches_per_frame(m720, landmark_map):
                 mc.h2d(dm2[f], np.ascontiguousarray(masks[f], np.uint8))
             got2 = mc.score_argmin_batch(imgs, dh2, [len(h) for h in hyps], bases, True, [dm2[0], dm2[1], dm2[2], 0])
             assert got2 == got
+            # rank-local failures go through the agreement all-reduce before the
+            # all-gather (with more ranks the others return MANTIS_ERR_COMM
+            # instead of blocking in it); the communicator stays usable
+            bad = list(imgs)
+            bad[1] = M.make_image(np.zeros((720, 1280, 3), np.uint8), K, D)
+            bad[1].step_bytes = 3 * 1280 - 3
+            with pytest.raises(M.MantisError, match="step"):
+                mc.score_argmin_batch(bad, dh2, [len(h) for h in hyps], bases, True, [dm2[0], dm2[1], dm2[2], 0])
+            with pytest.raises(M.MantisError, match="hypothesis block"):
+                mc.score_argmin_batch(imgs, dh2, [len(h) for h in hyps[:3]] + [-1], bases, True,
+                                      [dm2[0], dm2[1], dm2[2], 0])
+            with pytest.raises(M.MantisError, match="step"):
+                mc.score_argmin(bad[1], hyps[0], 0, True, masks[0])
+            assert mc.score_argmin_batch(imgs, dh2, [len(h) for h in hyps], bases, True,
+                                         [dm2[0], dm2[1], dm2[2], 0]) == got
+            assert mc.score_argmin(imgs[0], hyps[0], bases[0], True, masks[0]) == want[0]
         finally:
             mc.close()
     finally:

@@ -45,6 +45,32 @@ def test_rpp_phases_vs_oracle_hard_cases():
             assert np.array_equal(u, v, equal_nan=True)
 
 
+def test_rpp_n_points_host_build_vs_oracle():
+    """mantis_rpp_solve's per-point-count instances (mk_rpp_np.inc), host
+    build, bit-exact against the oracle's RPP on demo.cpp's 10-point problem
+    and on random planar problems of 4..12 points."""
+    d = np.load(os.path.join(GOLD, "rpp_demo.npz"), allow_pickle=False)
+    a, b = H.rpp_n(d["model"], d["iprts"]), O.rpp(d["model"], d["iprts"])
+    assert a[0] == b[0] == 1 and a[4] == b[4] == 0
+    for u, v in zip(a[1:4], b[1:4]):
+        assert np.array_equal(u, v)
+    np.testing.assert_allclose(a[1], d["matlab_R"], atol=1e-4 + 5e-6, rtol=0)
+    np.testing.assert_allclose(a[2], d["matlab_t"], atol=1e-4 + 5e-6, rtol=0)
+    rng = np.random.default_rng(5)
+    for n in range(4, 13):
+        for k in range(40):
+            m = np.vstack([rng.uniform(-0.8, 0.8, size=(2, n)), np.zeros((1, n))])
+            R = synth.rot_z(rng.uniform(0, 6.3)) @ synth.NADIR @ synth.rot_x(rng.normal() * 0.6)
+            t = np.array([rng.normal() * 0.3, rng.normal() * 0.3, rng.uniform(1, 12)])
+            Q = R.T @ m + t[:, None]
+            ip = np.vstack([Q[0] / Q[2], Q[1] / Q[2], np.ones(n)])
+            ip[:2] += rng.normal(size=(2, n)) * 0.01
+            a, b = H.rpp_n(m, ip), O.rpp(m, ip)
+            assert a[0] == b[0] and a[4] == b[4], (n, k)
+            for u, v in zip(a[1:4], b[1:4]):
+                assert np.array_equal(u, v, equal_nan=True), (n, k)
+
+
 def test_jacobi_noise_fast_forward_is_bit_exact():
     """mk_rpp.h jacobi_noise_ff skips the Jacobi sweeps that only shrink the
     rank-deficient row of a planar problem; every output byte (signs of zero
@@ -287,3 +313,82 @@ def test_fp32_screen_decisions_match_exact_projection():
     assert inside.sum() > 0.5 * n_scene
     assert (unsure & inside).sum() < 0.03 * inside.sum(), f"unsure {unsure.sum()} of {inside.sum()} in-frame"
     assert (res[:, 0] == 1).sum() > 0 and (res[:, 0] == 0).sum() > 0
+
+
+def _sampled_screen_consts(D, n=200001):
+    """Dense samples of max(theta_d', theta_d / sin theta) and of
+    (1 + sum |k| theta^(2i+2)) / F over (0, pi/2] (what round 3 sampled)."""
+    th = np.linspace(1.5707963267948966 / n, 1.5707963267948966, n)
+    x = th * th
+    k = np.asarray(D, np.float64)
+    terms = np.stack([k[j] * x ** (j + 1) for j in range(4)])
+    F = 1 + terms.sum(0)
+    dd = 1 + sum((2 * j + 3) * terms[j] for j in range(4))
+    S = max(1.0, float(np.max(np.maximum(dd, th * F / np.sin(th)))))
+    M = float(np.max((1 + np.abs(terms).sum(0)) / F))
+    ok = bool(np.all(dd > 0) and np.all(F > 0))
+    return ok, S, M
+
+
+def test_screen_bounds_derived_dominate_samples():
+    """The FP32 screen's constants (mk_screen.h screen_bounds) are derived upper
+    bounds: on the bench (720p), 1080p and grid1 (D = 0) intrinsics and on 10^4
+    random admissible distortions, the derived S and M are >= their densely
+    sampled maxima, tight (within 1 %), and the screen is disabled wherever
+    the sampled curve is not increasing and positive."""
+    K, D = synth.intrinsics()
+    K1080 = np.array(K, np.float64).reshape(3, 3).copy()
+    K1080[:2] *= 1.5
+    Kg = np.array([[450, 0, 453], [0, 450, 252], [0, 0, 1]], np.float64)
+    cases = [(K, D), (K1080, D), (Kg, np.zeros(4))]
+    rng = np.random.default_rng(2024)
+    for _ in range(10000):
+        d = rng.normal(size=4) * np.array([0.05, 0.02, 0.01, 0.005]) * 10 ** rng.uniform(-2, 0.7)
+        cases.append((K, d))
+    n_ok = 0
+    for Kc, Dc in cases:
+        ok, sens, crel, S, M = H.screen_consts(Kc, Dc, 4096)
+        sok, sS, sM = _sampled_screen_consts(Dc, 4097)
+        if not sok:
+            assert not ok  # a bound never admits a curve the samples reject
+            assert np.isinf(sens)
+            continue
+        if not ok:
+            continue  # admissible samples, but a piece's bound could not prove monotonicity: screen off (safe)
+        n_ok += 1
+        assert S >= sS and M >= sM, (Dc, S, sS, M, sM)
+        assert S <= sS * 1.01 and M <= sM * 1.01, (Dc, S, sS, M, sM)
+        f = max(float(np.asarray(Kc).reshape(9)[0]), float(np.asarray(Kc).reshape(9)[4]))
+        assert abs(sens - 2.2 * S * f) <= 1e-6 * sens
+        assert crel >= 24 * 2.0 ** -24 and crel >= 1.25 * (8 + 9 * M) * 2.0 ** -24 * (1 - 1e-6)
+    assert n_ok > 8000, n_ok
+    # the bench camera: mild distortion, M ~ 1.29, so the charge is ~24.5 u (round 3 charged 24 u)
+    ok, sens, crel, S, M = H.screen_consts(K, D)
+    assert ok and M < 1.5 and crel < 26 * 2.0 ** -24
+
+
+def test_fp32_screen_strong_distortion_decisions():
+    """The screen on strongly distorted Kannala-Brandt coefficients (theta_d
+    far from theta, cancellation in 1 + k theta^2 + ...: M well above 1):
+    every decision still equals the exact projection's."""
+    K, _ = synth.intrinsics()
+    rng = np.random.default_rng(77)
+    for D in ([0.30, -0.20, 0.08, -0.012], [-0.25, 0.06, -0.004, 0.0002], [0.6, -0.5, 0.2, -0.03]):
+        ok, sens, crel, S, M = H.screen_consts(K, D)
+        sok, _, _ = _sampled_screen_consts(D)
+        assert ok == sok
+        n = 200000
+        Q = rng.normal(size=(n, 4))
+        Q /= np.linalg.norm(Q, axis=1)[:, None]
+        a, b, c, d = Q.T
+        Rr = np.stack([a * a + b * b - c * c - d * d, 2 * (b * c - a * d), 2 * (b * d + a * c),
+                       2 * (b * c + a * d), a * a - b * b + c * c - d * d, 2 * (c * d - a * b),
+                       2 * (b * d - a * c), 2 * (c * d + a * b), a * a - b * b - c * c + d * d], 1).reshape(-1, 3, 3)
+        Cc = rng.uniform(-3, 3, (n, 3))
+        t = -np.einsum("nij,nj->ni", Rr, Cc)
+        c2w = np.concatenate([Rr.reshape(-1, 9), t], 1)
+        X = rng.uniform(-3, 3, (n, 3))
+        bad, res = H.screen_check(c2w, X, K, D, 1280, 720)
+        assert bad == 0, (D, bad)
+        if ok:
+            assert (res[:, 0] == 1).sum() > 0  # the screen still certifies landmarks

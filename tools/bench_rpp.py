@@ -61,7 +61,7 @@ def main():
         best = None
         for _ in range(3):
             R, t, e, st = m.rpp(I, O)
-            kt = dict(m.kernel_times())
+            kt = dict(m.stage_times())
             tot = sum(kt.values())
             if best is None or tot < best[0]:
                 best = (tot, kt)

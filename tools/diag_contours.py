@@ -32,7 +32,7 @@ imgs = [M.make_image(None, K, D, T_base_cam=Tbc[i], device_ptr=dev + i * fb, wid
 m.process(imgs, rigs=rigs)
 m.set_profiling(True)
 m.process(imgs, rigs=rigs)
-print("stages", [(k, round(v, 3)) for k, v in m.kernel_times()], flush=True)
+print("stages", [(k, round(v, 3)) for k, v in m.stage_times()], flush=True)
 C = np.array([m.frame_counters(i) for i in range(n)])
 names = ["borders", "points", "raw_q", "quads", "gen", "hyps", "pf", "goff", "ovf", "cand"]
 print("longest walk steps mean", C[:, 18].mean(), "max", C[:, 18].max())

@@ -47,7 +47,7 @@ def main(calls):
         t0 = time.perf_counter()
         m.process(one, rigs=1)
         lat.append((time.perf_counter() - t0) * 1e3)
-        for name, ms in m.kernel_times():
+        for name, ms in m.stage_times():
             st.setdefault(name, []).append(ms)
         m.set_profiling(False)
     med = {k: round(float(np.median(v)), 3) for k, v in st.items()}

@@ -56,7 +56,7 @@ def main(settings):
         t0 = time.perf_counter()
         for _ in range(reps):
             b.run()
-            for k, v in m.kernel_times():
+            for k, v in m.stage_times():
                 acc[k] = acc.get(k, 0.0) + v / reps
         el = (time.perf_counter() - t0) / reps
         m.set_profiling(False)
