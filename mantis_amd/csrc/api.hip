@@ -138,6 +138,7 @@ struct Ctx {
   uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
   int morph_bh = 48;       // k_morph output rows per band (MB_BH, or MB_BH_NARROW at wide max_width)
+  int morph_walk = 180;    // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
@@ -409,12 +410,20 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
   mark(c, "hysteresis/k_hyst_fix");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
-  dim3 gm((H + c->morph_bh - 1) / c->morph_bh, n);
-  k_morph<<<gm, MB_THREADS, morph_lds(W, c->morph_bh), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
-                                                              c->morph_bh);
+  if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 64) {
+    // register walker: one wave per (frame, row segment)
+    const int seg = c->morph_walk, nseg = (H + seg - 1) / seg, nwv = nseg * n;
+    k_morph_walk<<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
+                                                               seg, nseg, nwv);
+    mark(c, "morph/k_morph_walk");
+  } else {
+    dim3 gm((H + c->morph_bh - 1) / c->morph_bh, n);
+    k_morph<<<gm, MB_THREADS, morph_lds(W, c->morph_bh), c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
+                                                                c->morph_bh);
+    mark(c, "morph/k_morph");
+  }
   if (det_bytes) k_bits_to_bytes<<<blocks_for((size_t)(W + 2) * (H + 2)), 256, 0, c->s>>>(c->d_dbits, c->d_det, W + 2, H + 2,
                                                                                           dbits_wpw(W + 2));
-  mark(c, "morph/k_morph");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -896,6 +905,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     return MANTIS_ERR_ARG;
   }
   c->morph_bh = morph_lds(c->Wmax, MB_BH) <= 160 * 1024 ? MB_BH : MB_BH_NARROW;
+  if (const char* e = getenv("MANTIS_MORPH_WALK")) c->morph_walk = std::max(0, atoi(e));
   if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)morph_lds(c->Wmax, c->morph_bh)) !=

@@ -1424,6 +1424,144 @@ __global__ __launch_bounds__(MB_THREADS) void k_morph(const uint32_t* __restrict
   }
 }
 
+// The same two chains as k_morph, walked down the frame by one wave per
+// (frame, row segment) with every stage's window in registers (no LDS, no
+// barriers): lane w owns word column w (W <= 2016: the row fits one wave),
+// the horizontal part of each stage takes the neighbour words from lanes
+// w - 1 / w + 1 by DPP (lanes past the row hold the stage's identity, so the
+// clipped-window rule at the left / right edge falls out), and the vertical
+// part keeps the stage's last 2R + 1 horizontally processed input rows in a
+// register ring. Stage outputs lag the input row i: NG(i - 1), M0 and the
+// detector dilation (i - 2), detector erosion (i - 3), then the mask chain's
+// seven passes (i - 5 ... i - 29). A row outside [0, H) enters a ring as the
+// stage's identity (the clipped window of mk_bits.h). A segment starts its
+// walk MB_HALO rows above its first output row, so every stored row is exact.
+// Bit-identical to k_morph (tests/test_gpu_parity.py: masks and detector).
+template <int R, bool DIL>
+struct MwStage {
+  uint32_t ring[2 * R + 1];  // rows y - R .. y + R of the horizontally processed input
+  __device__ void init() {
+#pragma unroll
+    for (int k = 0; k <= 2 * R; k++) ring[k] = DIL ? 0u : ~0u;
+  }
+  // horizontal OP over x - R .. x + R of word `cur` (prev / next: the lanes
+  // beside; every word already carries the identity outside the image)
+  __device__ static uint32_t hop(uint32_t cur) {
+    const uint32_t prev = dpp_from_left(cur), next = dpp_from_right(cur);
+    uint32_t acc = cur;
+#pragma unroll
+    for (int k = 1; k <= R; k++) {
+      const uint32_t rt = __builtin_amdgcn_alignbit(next, cur, k);       // in(x + k)
+      const uint32_t lf = __builtin_amdgcn_alignbit(cur, prev, 32 - k);  // in(x - k)
+      acc = DIL ? (acc | rt | lf) : (acc & rt & lf);
+    }
+    return acc;
+  }
+  // push input row y + R (present: inside the image; `in` already masked to
+  // the image with this stage's identity outside), return output row y
+  __device__ uint32_t push(uint32_t in, bool present) {
+#pragma unroll
+    for (int k = 0; k < 2 * R; k++) ring[k] = ring[k + 1];
+    ring[2 * R] = present ? hop(in) : (DIL ? 0u : ~0u);
+    uint32_t acc = ring[0];
+#pragma unroll
+    for (int k = 1; k <= 2 * R; k++) acc = DIL ? (acc | ring[k]) : (acc & ring[k]);
+    return acc;
+  }
+};
+__global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
+                                                    uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
+                                                    size_t dstride, int seg_rows, int nseg, int nwaves) {
+  const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  if (gw >= nwaves) return;
+  const int lane = threadIdx.x & 63;
+  const int f = gw / nseg, sg = gw - f * nseg;
+  const int ys = sg * seg_rows, ye = min(H, ys + seg_rows);
+  const int WW = bits::words(W), wpw = dbits_wpw(W + 2);
+  const uint32_t vm = lane < WW ? bits::valid(lane, W) : 0u;  // valid pixels of this lane's word
+  const uint32_t* E = eb + (size_t)f * bstride;
+  uint32_t* D = dbits + (size_t)f * dstride;
+  uint32_t* M = mbits + (size_t)f * bstride;
+  // padded detector ring rows (zero) by the first / last segment
+  if (sg == 0 && lane < wpw) D[lane] = 0u;
+  if (ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
+  MwStage<2, true> d1;   // detector dilate 5x5 of E
+  MwStage<1, false> d2;  // detector erode 3x3
+  MwStage<3, true> s1;
+  MwStage<3, false> s2;
+  MwStage<4, true> s3;
+  MwStage<4, false> s4;
+  MwStage<5, true> s5;
+  MwStage<5, false> s6;
+  MwStage<3, false> s7;
+  d1.init(); d2.init(); s1.init(); s2.init(); s3.init(); s4.init(); s5.init(); s6.init(); s7.init();
+  uint32_t e0 = 0, e1 = 0, e2 = 0;  // E rows i - 2, i - 1, i (masked to the image)
+  uint32_t n0 = 0, n1 = 0, n2 = 0;  // NG rows i - 3, i - 2, i - 1
+  const int i0 = max(0, ys - MB_HALO), i1 = min(H, ye) + MB_HALO;
+  // E rows prefetched two steps ahead
+  uint32_t q0 = (i0 < H && lane < WW) ? E[(size_t)i0 * WW + lane] : 0u;
+  uint32_t q1 = (i0 + 1 < H && lane < WW) ? E[(size_t)(i0 + 1) * WW + lane] : 0u;
+  for (int i = i0; i < i1; i++) {
+    const uint32_t q2 = (i + 2 < H && lane < WW) ? E[(size_t)(i + 2) * WW + lane] : 0u;
+    const bool pin = i < H;  // input row i inside the image
+    e0 = e1;
+    e1 = e2;
+    e2 = pin ? (q0 & vm) : 0u;
+    q0 = q1;
+    q1 = q2;
+    // NOT(gradient) of row y = i - 1: cross max / min, rows outside excluded
+    const int yn = i - 1;
+    uint32_t ng = 0u;
+    if (yn >= 0 && yn < H) {
+      const uint32_t c0 = e1, c1 = e1 | ~vm;  // horizontal identities 0 / 1 outside the image
+      uint32_t mx = c0 | __builtin_amdgcn_alignbit(dpp_from_right(c0), c0, 1) |
+                    __builtin_amdgcn_alignbit(c0, dpp_from_left(c0), 31);
+      uint32_t mn = c1 & __builtin_amdgcn_alignbit(dpp_from_right(c1), c1, 1) &
+                    __builtin_amdgcn_alignbit(c1, dpp_from_left(c1), 31);
+      if (yn > 0) { mx |= e0; mn &= e0; }
+      if (yn + 1 < H) { mx |= e2; mn &= e2; }
+      ng = ~(mx ^ mn) & vm;
+    }
+    n0 = n1;
+    n1 = n2;
+    n2 = ng;
+    // M0 of row y = i - 2 = edge | border(NG)
+    const int y2 = i - 2;
+    uint32_t m0 = 0u;
+    const bool p2 = y2 >= 0 && y2 < H;
+    if (p2) {
+      const uint32_t left = __builtin_amdgcn_alignbit(n1, dpp_from_left(n1), 31);  // ng(x - 1)
+      const uint32_t right = __builtin_amdgcn_alignbit(dpp_from_right(n1), n1, 1);  // ng(x + 1)
+      const uint32_t up = y2 > 0 ? n0 : 0u, down = y2 + 1 < H ? n2 : 0u;
+      m0 = (e0 | (n1 & (~left | ~right | ~up | ~down))) & vm;
+    }
+    // detector: dilate r2 of E (row i in, row i - 2 out), erode r1 (row i - 3 out)
+    const uint32_t dd = d1.push(e2, pin) & vm;
+    const uint32_t de = d2.push(dd | ~vm, p2) & vm;
+    const int yd = i - 3;
+    {
+      const uint32_t prv = dpp_from_left(de);
+      if (yd >= ys && yd < ye && lane < wpw) D[(size_t)(yd + 1) * wpw + lane] = (de << 1) | (prv >> 31);
+    }
+    // mask: {dilate, erode}(3), (4), (5), erode(3): M0 row i - 2 in, row i - 29 out
+    const uint32_t a1 = s1.push(m0, p2) & vm;
+    const bool p5 = (unsigned)(i - 5) < (unsigned)H;
+    const uint32_t a2 = s2.push(a1 | ~vm, p5) & vm;
+    const bool p8 = (unsigned)(i - 8) < (unsigned)H;
+    const uint32_t a3 = s3.push(a2, p8) & vm;
+    const bool p12 = (unsigned)(i - 12) < (unsigned)H;
+    const uint32_t a4 = s4.push(a3 | ~vm, p12) & vm;
+    const bool p16 = (unsigned)(i - 16) < (unsigned)H;
+    const uint32_t a5 = s5.push(a4, p16) & vm;
+    const bool p21 = (unsigned)(i - 21) < (unsigned)H;
+    const uint32_t a6 = s6.push(a5 | ~vm, p21) & vm;
+    const bool p26 = (unsigned)(i - 26) < (unsigned)H;
+    const uint32_t a7 = s7.push(a6 | ~vm, p26) & vm;
+    const int ym = i - MB_HALO;
+    if (ym >= ys && ym < ye && lane < WW) M[bits::tiled_word(ym, lane, WW)] = a7;
+  }
+}
+
 // debug bytes (frame 0): a W x H bit plane (wpw = 0: ceil(W/32) words per
 // row; wpw = -1: the tiled mask plane) or the padded detector plane (wpw = its
 // words per row) -> one byte per pixel
@@ -3603,6 +3741,133 @@ __device__ inline void wave_score_color(const Xf& c2w, const double* green, int 
   }
 }
 
+// The same COLOR errors for a block's whole hypothesis set at once
+// (k_score_final's 80 yaw-set hypotheses): phase 1 projects every
+// (hypothesis, green landmark) pair (exact FP64, one per thread), phase 2 takes
+// the window rows -- (pair, row) items spread over every thread of the block,
+// several row loads in flight per thread, integer row sums added into the
+// pair's LDS slot (exact, order-free) -- and phase 3 sums each hypothesis's
+// window means in landmark order. Same pixels, same sums and the same ordered
+// double sum as wave_score_color, without its per-hypothesis chain of
+// dependent row trips.
+constexpr int kColorPairs = 3072;  // (hypothesis, green landmark) pairs the block path holds (80 x 37 = 2960)
+struct ColorPairs {
+  int32_t x0[kColorPairs];  // cvRound(u - 5)
+  int32_t yf[kColorPairs];  // cvRound(v - 5) << 3 | yrun << 2 | xrun << 1 | ok
+  int32_t acc[kColorPairs]; // window sum
+};
+// window row r of pair (T, X) when a column or row of the window does not
+// follow from x0 / y0 (a rounding of u - 5 + k or v - 5 + r that moves the
+// pixel by other than k / r: only within an ulp of a half-integer)
+__device__ __attribute__((noinline)) int color_row_exact(const Xf& T, const double* X, const Cam& cm,
+                                                         const uint8_t* bgr, int W, int H, int r) {
+  double rp[3], u, v;
+  xf_apply(T, X, rp);
+  distort(cm, rp[0], rp[1], rp[2], &u, &v);
+  const long npx = (long)W * H;
+  const int y = cv_round(v + (-5.0 + (double)r));
+  int rs = 0;
+  for (int ox = 0; ox < 10; ox++) {
+    const int x = cv_round(u + (-5.0 + (double)ox));
+    const long lin = (long)y * W + x;
+    int b = 0, g = 0, rr = 0;
+    if (lin >= 0 && lin < npx) {
+      const uint32_t pv = load_bgr(bgr, lin, npx);
+      b = (int)(pv & 0xffu);
+      g = (int)((pv >> 8) & 0xffu);
+      rr = (int)((pv >> 16) & 0xffu);
+    }
+    const int e0 = b - 50, e1 = g - 255, e2 = rr - 85;
+    rs += e0 * e0 + e1 * e1 + e2 * e2;
+  }
+  return rs;
+}
+// COLOR errors of nh hypotheses (pose_of(h) = FP64 c2w) into err[h]; the whole
+// block calls it (nh * ngr <= kColorPairs)
+template <int NT, class PoseOf>
+__device__ inline void block_score_color(const PoseOf& pose_of, int nh, const double* green, int ngr, const Cam& cm,
+                                         const uint8_t* bgr, int W, int H, ColorPairs* cp, double* err) {
+  const int tid = threadIdx.x;
+  const int np = nh * ngr;
+  const long npx = (long)W * H;
+  for (int i = tid; i < np; i += NT) {
+    const int h = i / ngr, l = i - h * ngr;
+    double rp[3], u, v;
+    xf_apply(pose_of(h), green + 3 * l, rp);
+    distort(cm, rp[0], rp[1], rp[2], &u, &v);
+    const int ok = rp[2] > 0 && in_frame(u, v, H, W);
+    const int x0 = cv_round(u + (-5.0 + 0.0)), y0 = cv_round(v + (-5.0 + 0.0));
+    int xrun = 1, yrun = 1;
+#pragma unroll
+    for (int k = 1; k < 10; k++) {
+      xrun &= cv_round(u + (-5.0 + (double)k)) == x0 + k;
+      yrun &= cv_round(v + (-5.0 + (double)k)) == y0 + k;
+    }
+    cp->x0[i] = x0;
+    cp->yf[i] = (int32_t)((uint32_t)y0 << 3) | (yrun << 2) | (xrun << 1) | ok;
+    cp->acc[i] = 0;
+  }
+  __syncthreads();
+  // (pair, row) items, row-major over the pairs so a wave's lanes add into
+  // different pairs; 4 items per thread per trip (their row loads in flight together)
+  const int ni = 10 * np;
+  constexpr int kU = 4;
+  for (int q0 = tid; q0 < ni; q0 += kU * NT) {
+    int rsum[kU], slot[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const int q = q0 + k * NT;
+      slot[k] = -1;
+      rsum[k] = 0;
+      if (q >= ni) continue;
+      const int r = q / np, i = q - r * np;
+      const int yf = cp->yf[i];
+      if (!(yf & 1)) continue;
+      slot[k] = i;
+      const int x0 = cp->x0[i], y = (yf >> 3) + r;
+      const long lin0 = (long)y * W + x0;
+      if ((yf & 6) == 6 && lin0 >= 0 && lin0 + 12 <= npx) {
+        rsum[k] = color_row_run(bgr, lin0);
+      } else if ((yf & 6) == 6) {  // rows reaching past the buffer: pixel by pixel, out-of-buffer reads 0 (Q10)
+        int rs = 0;
+        for (int ox = 0; ox < 10; ox++) {
+          const long lin = lin0 + ox;
+          int b = 0, g = 0, rr = 0;
+          if (lin >= 0 && lin < npx) {
+            const uint32_t pv = load_bgr(bgr, lin, npx);
+            b = (int)(pv & 0xffu);
+            g = (int)((pv >> 8) & 0xffu);
+            rr = (int)((pv >> 16) & 0xffu);
+          }
+          const int e0 = b - 50, e1 = g - 255, e2 = rr - 85;
+          rs += e0 * e0 + e1 * e1 + e2 * e2;
+        }
+        rsum[k] = rs;
+      } else {
+        const int h = i / ngr;
+        rsum[k] = color_row_exact(pose_of(h), green + 3 * (i - h * ngr), cm, bgr, W, H, r);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++)
+      if (slot[k] >= 0) atomicAdd(&cp->acc[slot[k]], rsum[k]);
+  }
+  __syncthreads();
+  for (int h = tid; h < nh; h += NT) {
+    double total = 0;
+    int n = 0;
+    for (int l = 0; l < ngr; l++) {
+      const int i = h * ngr + l;
+      if (cp->yf[i] & 1) {
+        total += (double)cp->acc[i] / (double)(10 * 10);
+        n++;
+      }
+    }
+    err[h] = n <= 0 ? DBL_MAX : total / ((double)n * 1.1);
+  }
+  __syncthreads();
+}
+
 // ------------------------------------------------------ screened fast scoring
 // Every landmark is first projected with the FP32 screen (mk_screen.h), whose
 // decision (z > 0, inFrame, cvRound pixel) is taken where it is certain; the
@@ -4092,7 +4357,10 @@ __global__ __launch_bounds__(NT) void k_score_final(
   __shared__ float4 lmf[768];
   __shared__ PoseLds P[96];
   __shared__ ErrIdx ei[96];
-  __shared__ ColorLds cls[(NT / 64)];
+  // COLOR phase: the block path's pair table, or (maps with more than
+  // kColorPairs / 80 green landmarks) the per-wave path's scratch in the same bytes
+  static_assert(sizeof(ColorPairs) >= sizeof(ColorLds) * (NT / 64), "color scratch");
+  __shared__ ColorPairs cpairs;
   __shared__ PoseLds cur;
   __shared__ double shv[9];
   __shared__ double yerr[4];
@@ -4125,14 +4393,23 @@ __global__ __launch_bounds__(NT) void k_score_final(
   }
   __syncthreads();
   const UQueue q{uqe, &uqn, kTailQueue};
-  for (int j = __builtin_amdgcn_readfirstlane(wave); j < NS; j += (NT / 64)) {
+  if (tid < NS) {
+    hs[tid] = 0;
+    hn[tid] = 0;
+  }
+  __syncthreads();
+  // tasks = (shift, half of the landmarks): 162 one-trip tasks over the waves
+  // instead of 81 two-trip ones (the last round of whole hypotheses kept one
+  // wave busy); the halves' integer sums combine exactly
+  for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * NS; t += (NT / 64)) {
+    const int j = t >> 1, h = t & 1;
     long long sum;
     int n;
-    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, 0, nl, fd.scam, W, H, fd.bgr, mask, q, j, &P[j].c2w,
-                                 lmk.xyz, &frames[f].cam, sum, n);
+    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, nl * h / 2, nl * (h + 1) / 2, fd.scam, W, H, fd.bgr, mask,
+                                 q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
     if (lane == 0) {
-      hs[j] = (unsigned long long)sum;
-      hn[j] = n;
+      atomicAdd(&hs[j], (unsigned long long)sum);
+      atomicAdd(&hn[j], n);
     }
   }
   __syncthreads();
@@ -4206,18 +4483,27 @@ __global__ __launch_bounds__(NT) void k_score_final(
   __syncthreads();
   const double* green = lmk.xyz + 3 * (lmk.nw + lmk.nr);
   __shared__ double yset_err[80];
-  for (int j = wave; j < 80; j += (NT / 64)) {
-    double e;
-    int n;
 #ifdef MK_DIAG_NO_COLOR  // timing diagnostic only: wrong results
-    e = 1.0 + j;
-    n = 1;
-#else
-    wave_score_color(P[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
-#endif
-    if (lane == 0) yset_err[j] = e;
-  }
+  if (tid < 80) yset_err[tid] = 1.0 + tid;
   __syncthreads();
+#else
+#ifndef MK_COLOR_WAVE
+#define MK_COLOR_WAVE 0
+#endif
+  if (!MK_COLOR_WAVE && 80 * lmk.ng <= kColorPairs) {
+    block_score_color<NT>([&](int h) -> const Xf& { return P[h].c2w; }, 80, green, lmk.ng, fd.cam, fd.bgr, W, H,
+                          &cpairs, yset_err);
+  } else {
+    ColorLds* cls = (ColorLds*)&cpairs;
+    for (int j = wave; j < 80; j += (NT / 64)) {
+      double e;
+      int n;
+      wave_score_color(P[j].c2w, green, lmk.ng, fd.cam, fd.bgr, W, H, &cls[wave], &e, &n);
+      if (lane == 0) yset_err[j] = e;
+    }
+    __syncthreads();
+  }
+#endif
   if (tid == 0) {
     double best_error = DBL_MAX;
     int best_k = -1;

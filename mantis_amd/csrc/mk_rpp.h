@@ -880,7 +880,7 @@ MK_HD Mt<3, C> norm_rv(const Mt<3, C>& R) {
 typedef Mt<3, 3> M33;
 typedef Mt<3, 1> M31;
 
-MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
+__attribute__((always_inline)) MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
   double d = v2[0] * v1[0] + v2[1] * v1[1] + v2[2] * v1[2];
   double winkel = acos(d);
   M31 axm;
@@ -918,7 +918,7 @@ MK_HD bool rot_by_vector(const double* v1, const double* v2, M33& R) {
   return !(s * s > 1e-3);
 }
 
-MK_HD bool decompose_r(const M33& R, M33& RzN) {
+__attribute__((always_inline)) MK_HD bool decompose_r(const M33& R, M33& RzN) {
   double cl = atan2(R(2, 1), R(2, 0));
   M33 Rz = rpy_mat(0, 0, cl);
   M33 R_ = mm(R, Rz);

@@ -116,6 +116,45 @@ def test_detector_binary_and_mask_bit_exact(mantis, frames):
         assert np.array_equal(mask, ref_mask), f"clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
 
 
+@pytest.mark.parametrize("walk", ["180", "64", "7", "0"])
+def test_morphology_kernels_bit_exact(walk):
+    """Both morphology kernels (k_morph_walk: one wave per frame row segment,
+    stage windows in registers, MANTIS_MORPH_WALK = segment rows; k_morph: LDS
+    bands, MANTIS_MORPH_WALK=0) against the oracle's detector binary and
+    cleanImageByEdge mask: widths ending mid-word, segments shorter than the
+    29-row reach, frames shorter than it, blob noise and i.i.d. noise."""
+    import mantis_amd as M
+
+    saved = os.environ.get("MANTIS_MORPH_WALK")
+    os.environ["MANTIS_MORPH_WALK"] = walk
+    try:
+        mt = M.Mantis(max_cams=1, max_width=1920, max_height=1080)
+    finally:
+        if saved is None:
+            os.environ.pop("MANTIS_MORPH_WALK")
+        else:
+            os.environ["MANTIS_MORPH_WALK"] = saved
+    rng = np.random.default_rng(17)
+    K, D = synth.intrinsics()
+    try:
+        sizes = [(1280, 720), (1920, 1080), (1000, 611), (232, 40), (33, 7), (64, 30), (95, 61)]
+        for k, (w, h) in enumerate(sizes):
+            if k % 2 == 0:
+                base = rng.integers(0, 256, (h // 5 + 2, w // 5 + 2, 3)).astype(np.float64)
+                img = np.repeat(np.repeat(base, 5, 0), 5, 1)[:h, :w]
+                img = np.clip(img + rng.normal(0, 30, img.shape), 0, 255).astype(np.uint8)
+            else:
+                img = rng.integers(0, 256, (h, w, 3)).astype(np.uint8)
+            det, mask = mt.masks(M.make_image(img, K, D))
+            cn = O.canny(img)
+            ref_det = O.detector_binary(cn)
+            ref_mask = O.clean_mask(cn)
+            assert np.array_equal(det, ref_det), f"{w}x{h}: detector binary differs: {np.count_nonzero(det != ref_det)} px"
+            assert np.array_equal(mask, ref_mask), f"{w}x{h}: clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
+    finally:
+        mt.close()
+
+
 def test_quads_bit_exact(mantis, frames, landmark_map):
     orc = O.Oracle(*landmark_map)
     K, D = synth.intrinsics()
