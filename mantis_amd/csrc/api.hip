@@ -113,6 +113,12 @@ struct Ctx {
   hipStream_t s = nullptr;
   hipStream_t s_copy = nullptr;     // side stream: the gaussian stream's H2D, overlapped with RPP
   hipEvent_t ev_gauss = nullptr;    // ... which s waits on before scoring
+  // batch calls wait for the stream on a blocking-sync event (the host thread
+  // sleeps instead of spinning in hipStreamSynchronize: one spinning thread per
+  // context was most of a step's host CPU time); calls of at most
+  // spin_frames frames spin (latency). MANTIS_SPIN_FRAMES overrides.
+  hipEvent_t ev_wait = nullptr;
+  int spin_frames = 16;
   std::string err;
   uint64_t rng_state = 1;
   // map
@@ -125,6 +131,7 @@ struct Ctx {
   bool trace_lds_ok = false;
   size_t trace_lds_max = 0;
   int trace_lds_frames = 0;
+  int fc_small_frames = 0;  // k_frame_contours at 1024 threads for batches of at most this many frames
   size_t plane = 0;
   int pool_cap = 0;
   // device workspace
@@ -286,6 +293,11 @@ void mark(Ctx* c, const char* name) {
   (void)hipEventRecord(c->ev[c->ev_names.size()], c->s);
   c->ev_names.push_back(name);
 }
+
+// Wait for everything queued on the ctx's stream: a blocking-sync event for
+// batches of more than spin_frames frames (the thread sleeps), else a spin.
+struct Ctx;
+hipError_t wait_stream(Ctx* c, int frames);
 
 // Entry points may be called from any host thread (one ctx per thread at a
 // time): make the ctx's GPU current on the calling thread.
@@ -461,7 +473,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   mark(c, "border_trace");
   // small batches (latency): 1024 threads per frame; large ones: 256, so the
   // per-frame blocks fit beside other contexts' kernels on a CU
-  k_frame_contours<<<n, n <= c->trace_lds_frames ? 1024 : MK_FC_THREADS, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
+  k_frame_contours<<<n, n <= c->fc_small_frames ? 1024 : MK_FC_THREADS, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
                                          c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
                                          Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon,
                                          c->cfg.search_radius_multiplier);
@@ -644,6 +656,13 @@ void finish_profile(Ctx* c, bool append = false) {
   c->ev_names.clear();
 }
 
+hipError_t wait_stream(Ctx* c, int frames) {
+  if (frames <= c->spin_frames || !c->ev_wait) return hipStreamSynchronize(c->s);
+  hipError_t e = hipEventRecord(c->ev_wait, c->s);
+  if (e != hipSuccess) return e;
+  return hipEventSynchronize(c->ev_wait);
+}
+
 // rig fusion and 4x4 helpers: mk_shard.h (shared with the CPU test build)
 using mk::shard::fuse_rig;
 using mk::shard::mat4_inv_rigid;
@@ -706,7 +725,7 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shar
   HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipMemcpyAsync(c->h_gtotal, c->d_gtotal, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
   if (sh) HIP_OK(hipMemcpyAsync(c->h_sh_flags, c->d_sh_flags, sizeof(int32_t) * ng, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipStreamSynchronize(c->s));
+  HIP_OK(wait_stream(c, n));
   finish_profile(c);
   const int per = c->cfg.particles * c->cfg.iterations * 6;
   int used = 0;
@@ -852,7 +871,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   c->rng_state = cfg.rng_seed ? cfg.rng_seed : 0xffffffffULL;
   if (hipSetDevice(cfg.device) != hipSuccess || hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gauss, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_gauss, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_wait, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
     g_create_err = "hipSetDevice/hipStreamCreate failed";
     if (c->s) (void)hipStreamDestroy(c->s);
     if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
@@ -882,6 +902,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     c->screen_off = so && so[0] == '0';
     const char* e = getenv("MANTIS_TRACE_LDS_FRAMES");
     c->trace_lds_frames = e ? atoi(e) : c->n_cu / 4;
+    const char* e2 = getenv("MANTIS_FC_SMALL_FRAMES");
+    c->fc_small_frames = e2 ? atoi(e2) : c->n_cu / 4;
   }
   {
     // LDS-staged mask for the particle filter: the tiled plane of a max-size
@@ -906,6 +928,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   }
   c->morph_bh = morph_lds(c->Wmax, MB_BH) <= 160 * 1024 ? MB_BH : MB_BH_NARROW;
   if (const char* e = getenv("MANTIS_MORPH_WALK")) c->morph_walk = std::max(0, atoi(e));
+  if (const char* e = getenv("MANTIS_SPIN_FRAMES")) c->spin_frames = atoi(e);
   if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)morph_lds(c->Wmax, c->morph_bh)) !=
@@ -1013,6 +1036,7 @@ mantis_status mantis_destroy(void* ctx) {
     if (p) (void)hipHostFree(p);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->ev_gauss) (void)hipEventDestroy(c->ev_gauss);
+  if (c->ev_wait) (void)hipEventDestroy(c->ev_wait);
   if (c->s_copy) (void)hipStreamDestroy(c->s_copy);
   if (c->s) (void)hipStreamDestroy(c->s);
   delete c;

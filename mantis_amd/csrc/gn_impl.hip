@@ -275,7 +275,7 @@ mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, 
   mark(c, "rig_gn");
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(io.data(), c->d_rigio, sizeof(RigGnIO) * n_rigs, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipStreamSynchronize(c->s));
+  HIP_OK(wait_stream(c, n));
   finish_profile(c, true);
   c->gn_last_rigs = n_rigs;
   c->gn_last_local = cams_local;

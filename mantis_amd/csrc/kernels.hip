@@ -1439,10 +1439,14 @@ __global__ __launch_bounds__(MB_THREADS) void k_morph(const uint32_t* __restrict
 // Bit-identical to k_morph (tests/test_gpu_parity.py: masks and detector).
 template <int R, bool DIL>
 struct MwStage {
-  uint32_t ring[2 * R + 1];  // rows y - R .. y + R of the horizontally processed input
+  // rows y - R .. y + 1 + R of the horizontally processed input: a step pushes
+  // two rows and yields two output rows, so the ring shifts and the window's
+  // OP over its middle 2R rows are shared by the pair (half the register moves
+  // and vertical OPs of a one-row step)
+  uint32_t ring[2 * R + 2];
   __device__ void init() {
 #pragma unroll
-    for (int k = 0; k <= 2 * R; k++) ring[k] = DIL ? 0u : ~0u;
+    for (int k = 0; k < 2 * R + 2; k++) ring[k] = DIL ? 0u : ~0u;
   }
   // horizontal OP over x - R .. x + R of word `cur` (prev / next: the lanes
   // beside; every word already carries the identity outside the image)
@@ -1457,18 +1461,37 @@ struct MwStage {
     }
     return acc;
   }
-  // push input row y + R (present: inside the image; `in` already masked to
-  // the image with this stage's identity outside), return output row y
-  __device__ uint32_t push(uint32_t in, bool present) {
+  // push input rows y + R, y + R + 1 (present: inside the image; the words
+  // already carry this stage's identity outside it); yields rows y, y + 1
+  __device__ void push2(uint32_t in0, bool p0, uint32_t in1, bool p1, uint32_t& o0, uint32_t& o1) {
 #pragma unroll
-    for (int k = 0; k < 2 * R; k++) ring[k] = ring[k + 1];
-    ring[2 * R] = present ? hop(in) : (DIL ? 0u : ~0u);
-    uint32_t acc = ring[0];
+    for (int k = 0; k < 2 * R; k++) ring[k] = ring[k + 2];
+    ring[2 * R] = p0 ? hop(in0) : (DIL ? 0u : ~0u);
+    ring[2 * R + 1] = p1 ? hop(in1) : (DIL ? 0u : ~0u);
+    uint32_t mid = ring[1];
 #pragma unroll
-    for (int k = 1; k <= 2 * R; k++) acc = DIL ? (acc | ring[k]) : (acc & ring[k]);
-    return acc;
+    for (int k = 2; k <= 2 * R; k++) mid = DIL ? (mid | ring[k]) : (mid & ring[k]);
+    o0 = DIL ? (mid | ring[0]) : (mid & ring[0]);
+    o1 = DIL ? (mid | ring[2 * R + 1]) : (mid & ring[2 * R + 1]);
   }
 };
+// NOT(gradient) word of the row with rows up / down (their presence: inside the image)
+__device__ inline uint32_t mw_ng(uint32_t up, bool hu, uint32_t c0, uint32_t dn, bool hd, uint32_t vm) {
+  const uint32_t c1 = c0 | ~vm;  // horizontal identities 0 / 1 outside the image
+  uint32_t mx = c0 | __builtin_amdgcn_alignbit(dpp_from_right(c0), c0, 1) |
+                __builtin_amdgcn_alignbit(c0, dpp_from_left(c0), 31);
+  uint32_t mn = c1 & __builtin_amdgcn_alignbit(dpp_from_right(c1), c1, 1) &
+                __builtin_amdgcn_alignbit(c1, dpp_from_left(c1), 31);
+  if (hu) { mx |= up; mn &= up; }
+  if (hd) { mx |= dn; mn &= dn; }
+  return ~(mx ^ mn) & vm;
+}
+// M0 = edge | border(NG) word of the row (NG rows up / down: 0 outside the image)
+__device__ inline uint32_t mw_m0(uint32_t e, uint32_t nu, uint32_t n, uint32_t nd, uint32_t vm) {
+  const uint32_t left = __builtin_amdgcn_alignbit(n, dpp_from_left(n), 31);   // ng(x - 1)
+  const uint32_t right = __builtin_amdgcn_alignbit(dpp_from_right(n), n, 1);  // ng(x + 1)
+  return (e | (n & (~left | ~right | ~nu | ~nd))) & vm;
+}
 __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                     uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
                                                     size_t dstride, int seg_rows, int nseg, int nwaves) {
@@ -1495,70 +1518,48 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   MwStage<5, false> s6;
   MwStage<3, false> s7;
   d1.init(); d2.init(); s1.init(); s2.init(); s3.init(); s4.init(); s5.init(); s6.init(); s7.init();
-  uint32_t e0 = 0, e1 = 0, e2 = 0;  // E rows i - 2, i - 1, i (masked to the image)
-  uint32_t n0 = 0, n1 = 0, n2 = 0;  // NG rows i - 3, i - 2, i - 1
+  const auto in = [H](int y) { return (unsigned)y < (unsigned)H; };
+  uint32_t eA = 0, eB = 0;  // E rows i - 2, i - 1 (masked to the image, 0 outside it)
+  uint32_t nA = 0, nB = 0;  // NG rows i - 3, i - 2
   const int i0 = max(0, ys - MB_HALO), i1 = min(H, ye) + MB_HALO;
-  // E rows prefetched two steps ahead
-  uint32_t q0 = (i0 < H && lane < WW) ? E[(size_t)i0 * WW + lane] : 0u;
-  uint32_t q1 = (i0 + 1 < H && lane < WW) ? E[(size_t)(i0 + 1) * WW + lane] : 0u;
-  for (int i = i0; i < i1; i++) {
-    const uint32_t q2 = (i + 2 < H && lane < WW) ? E[(size_t)(i + 2) * WW + lane] : 0u;
-    const bool pin = i < H;  // input row i inside the image
-    e0 = e1;
-    e1 = e2;
-    e2 = pin ? (q0 & vm) : 0u;
-    q0 = q1;
-    q1 = q2;
-    // NOT(gradient) of row y = i - 1: cross max / min, rows outside excluded
-    const int yn = i - 1;
-    uint32_t ng = 0u;
-    if (yn >= 0 && yn < H) {
-      const uint32_t c0 = e1, c1 = e1 | ~vm;  // horizontal identities 0 / 1 outside the image
-      uint32_t mx = c0 | __builtin_amdgcn_alignbit(dpp_from_right(c0), c0, 1) |
-                    __builtin_amdgcn_alignbit(c0, dpp_from_left(c0), 31);
-      uint32_t mn = c1 & __builtin_amdgcn_alignbit(dpp_from_right(c1), c1, 1) &
-                    __builtin_amdgcn_alignbit(c1, dpp_from_left(c1), 31);
-      if (yn > 0) { mx |= e0; mn &= e0; }
-      if (yn + 1 < H) { mx |= e2; mn &= e2; }
-      ng = ~(mx ^ mn) & vm;
-    }
-    n0 = n1;
-    n1 = n2;
-    n2 = ng;
-    // M0 of row y = i - 2 = edge | border(NG)
-    const int y2 = i - 2;
-    uint32_t m0 = 0u;
-    const bool p2 = y2 >= 0 && y2 < H;
-    if (p2) {
-      const uint32_t left = __builtin_amdgcn_alignbit(n1, dpp_from_left(n1), 31);  // ng(x - 1)
-      const uint32_t right = __builtin_amdgcn_alignbit(dpp_from_right(n1), n1, 1);  // ng(x + 1)
-      const uint32_t up = y2 > 0 ? n0 : 0u, down = y2 + 1 < H ? n2 : 0u;
-      m0 = (e0 | (n1 & (~left | ~right | ~up | ~down))) & vm;
-    }
-    // detector: dilate r2 of E (row i in, row i - 2 out), erode r1 (row i - 3 out)
-    const uint32_t dd = d1.push(e2, pin) & vm;
-    const uint32_t de = d2.push(dd | ~vm, p2) & vm;
-    const int yd = i - 3;
+  const auto ld = [&](int y) { return (in(y) && lane < WW) ? E[(size_t)y * WW + lane] & vm : 0u; };
+  uint32_t q0 = ld(i0), q1 = ld(i0 + 1);  // E rows prefetched a step ahead
+  for (int i = i0; i < i1; i += 2) {
+    const uint32_t e0 = q0, e1 = q1;  // E rows i, i + 1
+    q0 = ld(i + 2);
+    q1 = ld(i + 3);
+    // NOT(gradient) rows i - 1, i; M0 rows i - 2, i - 1
+    const uint32_t g0 = in(i - 1) ? mw_ng(eA, in(i - 2), eB, e0, in(i), vm) : 0u;
+    const uint32_t g1 = in(i) ? mw_ng(eB, in(i - 1), e0, e1, in(i + 1), vm) : 0u;
+    const uint32_t m0 = in(i - 2) ? mw_m0(eA, nA, nB, g0, vm) : 0u;
+    const uint32_t m1 = in(i - 1) ? mw_m0(eB, nB, g0, g1, vm) : 0u;
+    eA = e0;
+    eB = e1;
+    nA = g0;
+    nB = g1;
+    // detector: dilate r2 of E (rows i, i + 1 in; i - 2, i - 1 out), erode r1 (i - 3, i - 2 out)
+    uint32_t a0, a1, b0, b1;
+    d1.push2(e0, in(i), e1, in(i + 1), a0, a1);
+    d2.push2((a0 & vm) | ~vm, in(i - 2), (a1 & vm) | ~vm, in(i - 1), b0, b1);
+    b0 &= vm;
+    b1 &= vm;
     {
-      const uint32_t prv = dpp_from_left(de);
-      if (yd >= ys && yd < ye && lane < wpw) D[(size_t)(yd + 1) * wpw + lane] = (de << 1) | (prv >> 31);
+      const uint32_t p0 = dpp_from_left(b0), p1 = dpp_from_left(b1);
+      const int y = i - 3;
+      if (y >= ys && y < ye && lane < wpw) D[(size_t)(y + 1) * wpw + lane] = (b0 << 1) | (p0 >> 31);
+      if (y + 1 >= ys && y + 1 < ye && lane < wpw) D[(size_t)(y + 2) * wpw + lane] = (b1 << 1) | (p1 >> 31);
     }
-    // mask: {dilate, erode}(3), (4), (5), erode(3): M0 row i - 2 in, row i - 29 out
-    const uint32_t a1 = s1.push(m0, p2) & vm;
-    const bool p5 = (unsigned)(i - 5) < (unsigned)H;
-    const uint32_t a2 = s2.push(a1 | ~vm, p5) & vm;
-    const bool p8 = (unsigned)(i - 8) < (unsigned)H;
-    const uint32_t a3 = s3.push(a2, p8) & vm;
-    const bool p12 = (unsigned)(i - 12) < (unsigned)H;
-    const uint32_t a4 = s4.push(a3 | ~vm, p12) & vm;
-    const bool p16 = (unsigned)(i - 16) < (unsigned)H;
-    const uint32_t a5 = s5.push(a4, p16) & vm;
-    const bool p21 = (unsigned)(i - 21) < (unsigned)H;
-    const uint32_t a6 = s6.push(a5 | ~vm, p21) & vm;
-    const bool p26 = (unsigned)(i - 26) < (unsigned)H;
-    const uint32_t a7 = s7.push(a6 | ~vm, p26) & vm;
-    const int ym = i - MB_HALO;
-    if (ym >= ys && ym < ye && lane < WW) M[bits::tiled_word(ym, lane, WW)] = a7;
+    // mask: {dilate, erode}(3), (4), (5), erode(3): M0 rows i - 2, i - 1 in; i - 29, i - 28 out
+    s1.push2(m0, in(i - 2), m1, in(i - 1), a0, a1);
+    s2.push2((a0 & vm) | ~vm, in(i - 5), (a1 & vm) | ~vm, in(i - 4), b0, b1);
+    s3.push2(b0 & vm, in(i - 8), b1 & vm, in(i - 7), a0, a1);
+    s4.push2((a0 & vm) | ~vm, in(i - 12), (a1 & vm) | ~vm, in(i - 11), b0, b1);
+    s5.push2(b0 & vm, in(i - 16), b1 & vm, in(i - 15), a0, a1);
+    s6.push2((a0 & vm) | ~vm, in(i - 21), (a1 & vm) | ~vm, in(i - 20), b0, b1);
+    s7.push2((b0 & vm) | ~vm, in(i - 26), (b1 & vm) | ~vm, in(i - 25), a0, a1);
+    const int y = i - MB_HALO;
+    if (y >= ys && y < ye && lane < WW) M[bits::tiled_word(y, lane, WW)] = a0 & vm;
+    if (y + 1 >= ys && y + 1 < ye && lane < WW) M[bits::tiled_word(y + 1, lane, WW)] = a1 & vm;
   }
 }
 
@@ -3883,6 +3884,11 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
 #define MK_SCR_UNROLL 6
 #endif
 constexpr int kScrUnroll = MK_SCR_UNROLL;  // landmarks per lane in flight (their pixel loads overlap)
+#ifndef MK_SCORE_PIPE2
+// scorers' tasks software-pipelined (screen_issue / screen_finish): measured
+// slower (score stage 11.0 / 11.2 -> 11.8 / 11.8 ms per 4096 frames, A/B/A/B)
+#define MK_SCORE_PIPE2 0
+#endif
 struct UQueue {
   uint32_t* e;  // entries: tag << 16 | landmark
   int32_t* n;   // entries pushed (past cap: those were recomputed in place)
@@ -4012,6 +4018,133 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
   s_out = s64;
   n_out = n;
 }
+// The same trip split in two halves so a wave can keep one trip's pixel
+// loads in flight while it projects the next (software pipelining over a
+// wave's tasks): screen_issue projects the trip's landmarks, queues the unsure
+// ones and issues the mask / pixel loads; screen_finish turns the loaded
+// pixels into the integer sum and count. A task is one trip (le - lb <=
+// 64 U landmarks). Same terms and sums as wave_sums_screen.
+template <int U>
+struct ScrPend {
+  uint32_t pv[U];        // loaded pixel dword per slot
+  uint32_t hit, in, lst; // bit k: mask hit / SCR_IN / last pixel of the frame (read one byte early)
+  int s, n;              // terms added in place (the queue was full)
+};
+template <int U, class MK>
+__device__ inline void screen_issue(const PoseF& P, const float4* lmf, int lb, int le, const ScreenCam& sc, int W,
+                                    int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
+                                    const double* lmd, const Cam* cmp, ScrPend<U>& pd) {
+  const int lane = threadIdx.x & 63;
+  const int last = W * H - 1;
+  int st[U], lin[U], px[U], py[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    const int l = lb + lane + 64 * k;
+    const float4 L = lmf[l < le ? l : le - 1];
+    int x, y;
+    const int t = screen_project(P, L.x, L.y, L.z, L.w, sc, W, H, &x, &y);
+    st[k] = l < le ? t : SCR_OUT;
+    const bool in = st[k] == SCR_IN;
+    px[k] = in ? x : 0;
+    py[k] = in ? y : 0;
+    lin[k] = in ? y * W + x : 0;
+  }
+  uint32_t mw[U];
+#pragma unroll
+  for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+  pd.hit = pd.in = pd.lst = 0u;
+  pd.s = pd.n = 0;
+  int cu = 0;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    const bool hit = st[k] == SCR_IN && mask.test(mw[k], px[k]);
+    const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
+    typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
+    pd.pv[k] = *(gu32u*)(bgr + off);
+    pd.hit |= (hit ? 1u : 0u) << k;
+    pd.in |= (st[k] == SCR_IN ? 1u : 0u) << k;
+    pd.lst |= (lin[k] == last ? 1u : 0u) << k;
+    cu += st[k] == SCR_UNSURE;
+  }
+  if (__ballot(cu > 0)) {  // wave-aggregated queue append: one LDS atomic
+    const int incl = wave_incl_scan(cu, lane);
+    int base = 0;
+    if (lane == 63) base = atomicAdd(q.n, incl);
+    base = __shfl(base, 63);
+    int idx = base + incl - cu;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      if (st[k] != SCR_UNSURE) continue;
+      const int l = lb + lane + 64 * k;
+      if (idx < q.cap) {
+        q.e[idx] = ((uint32_t)tag << 16) | (uint32_t)l;
+      } else {
+        int e;
+        if (exact_term(*Tx, lmd + 3 * l, *cmp, W, H, bgr, mask, e)) { pd.n++; pd.s += e; }
+      }
+      idx++;
+    }
+  }
+}
+template <int U>
+__device__ inline void screen_finish(const ScrPend<U>& pd, long long& s_out, int& n_out) {
+  int s = pd.s, n = pd.n;
+#pragma unroll
+  for (int k = 0; k < U; k++) {
+    const uint32_t v = (pd.lst >> k) & 1u ? pd.pv[k] >> 8 : pd.pv[k];
+    const uint32_t d = ~v & 0xffffffu;
+    const int term = (int)__builtin_amdgcn_udot4(d, d, 0u, false);
+    constexpr int kBlack = 3 * 255 * 255;
+    const int hm = -(int)((pd.hit >> k) & 1u), im = -(int)((pd.in >> k) & 1u);
+    const int e = kBlack ^ ((term ^ kBlack) & hm);
+    n -= im;
+    s += e & im;
+  }
+  long long s64 = s;
+  for (int o = 32; o > 0; o >>= 1) {
+    s64 += __shfl_xor(s64, o);
+    n += __shfl_xor(n, o);
+  }
+  s_out = s64;
+  n_out = n;
+}
+// A wave's tasks t = first, first + stride, ... < ntasks, each one trip,
+// pipelined: task t's pixel loads are in flight while task t + stride is
+// projected. task(t, P, lb, le, tag, Tx) describes task t (pose, landmark
+// range, queue tag, exact pose); done(t, sum, count) takes its result (all lanes).
+template <int U, class MK, class Task, class Done>
+__device__ inline void wave_tasks_screen(int first, int stride, int ntasks, const float4* lmf, const ScreenCam& sc,
+                                         int W, int H, const uint8_t* bgr, const MK& mask, UQueue q,
+                                         const double* lmd, const Cam* cmp, const Task& task, const Done& done) {
+  int t = first;
+  if (t >= ntasks) return;
+  ScrPend<U> cur;
+  {
+    PoseF P;
+    int lb, le, tag;
+    const Xf* Tx;
+    task(t, P, lb, le, tag, Tx);
+    screen_issue<U>(P, lmf, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp, cur);
+  }
+  while (true) {
+    const int tn = t + stride;
+    ScrPend<U> nxt;
+    if (tn < ntasks) {
+      PoseF P;
+      int lb, le, tag;
+      const Xf* Tx;
+      task(tn, P, lb, le, tag, Tx);
+      screen_issue<U>(P, lmf, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp, nxt);
+    }
+    long long sum;
+    int cnt;
+    screen_finish<U>(cur, sum, cnt);
+    done(t, sum, cnt);
+    if (tn >= ntasks) break;
+    cur = nxt;
+    t = tn;
+  }
+}
 // the block recomputes the queued landmarks exactly: add(tag, term) for those
 // in frame (pose_of(tag) = the tag's FP64 c2w)
 template <class MK, class PoseOf, class Add>
@@ -4131,6 +4264,31 @@ __global__ __launch_bounds__(NT) void k_score_init(
   const int C = st[f].n_hyps;
   // evaluateHypotheses(hyps, cleaned): screened pass, then the unsure landmarks exactly
   const UQueue q{uqe, &uqn, kInitQueue};
+#if MK_SCORE_PIPE2
+  // tasks = (hypothesis, half of the landmarks), one trip each, pipelined
+  for (int h = tid; h < C; h += NT) {
+    hs[h] = 0;
+    hn[h] = 0;
+  }
+  __syncthreads();
+  wave_tasks_screen<kScrUnroll>(
+      __builtin_amdgcn_readfirstlane(wave), NT / 64, 2 * C, lmf, fd.scam, W, H, fd.bgr, mask, q, lmk.xyz,
+      &frames[f].cam,
+      [&](int t, PoseF& P, int& lb, int& le, int& tag, const Xf*& Tx) {
+        const int h = t >> 1, k = t & 1;
+        P = posef_from(Hh[h].c2w);
+        lb = nl * k / 2;
+        le = nl * (k + 1) / 2;
+        tag = h;
+        Tx = &Hh[h].c2w;
+      },
+      [&](int t, long long sum, int cnt) {
+        if (lane == 0) {
+          atomicAdd(&hs[t >> 1], (unsigned long long)sum);
+          atomicAdd(&hn[t >> 1], cnt);
+        }
+      });
+#else
   for (int h = __builtin_amdgcn_readfirstlane(wave); h < C; h += (NT / 64)) {
     long long s;
     int n;
@@ -4141,6 +4299,7 @@ __global__ __launch_bounds__(NT) void k_score_init(
       hn[h] = n;
     }
   }
+#endif
   __syncthreads();
   block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return Hh[t].c2w; },
               [&](int t, int e) {
@@ -4270,7 +4429,29 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     if (tid == 0) uqn = 0;
     __syncthreads();
     // SPLIT waves per particle (landmark slices; integer sums, so the
-    // partials combine exactly in any order)
+    // partials combine exactly in any order); a wave's tasks pipelined
+#if MK_SCORE_PIPE2
+    const auto task = [&](int t, PoseF& P, int& lb, int& le, int& tag, const Xf*& Tx) {
+      const int j = t / SPLIT, h = t - j * SPLIT;
+      P = Pf[j];
+      lb = nl * h / SPLIT;
+      le = nl * (h + 1) / SPLIT;
+      tag = j;
+      Tx = &Pc[j];
+    };
+    const auto done = [&](int t, long long sum, int cnt) {
+      if (lane == 0) {
+        Ps[t] = (unsigned long long)sum;
+        Pn[t] = cnt;
+      }
+    };
+    if (LM)
+      wave_tasks_screen<kScrUnroll>(__builtin_amdgcn_readfirstlane(wave), kW, particles * SPLIT, lmf, fd.scam, W, H,
+                                    fd.bgr, mlds, q, lmk.xyz, &frames[f].cam, task, done);
+    else
+      wave_tasks_screen<kScrUnroll>(__builtin_amdgcn_readfirstlane(wave), kW, particles * SPLIT, lmf, fd.scam, W, H,
+                                    fd.bgr, mglb, q, lmk.xyz, &frames[f].cam, task, done);
+#else
     for (int task = __builtin_amdgcn_readfirstlane(wave); task < particles * SPLIT; task += kW) {
       const int j = task / SPLIT, h = task - j * SPLIT;
       long long sum;
@@ -4286,6 +4467,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
         Pn[task] = cnt;
       }
     }
+#endif
     __syncthreads();
     const auto pose_of = [&](int t) -> const Xf& { return Pc[t]; };
     const auto add = [&](int t, int e) {
@@ -4401,6 +4583,25 @@ __global__ __launch_bounds__(NT) void k_score_final(
   // tasks = (shift, half of the landmarks): 162 one-trip tasks over the waves
   // instead of 81 two-trip ones (the last round of whole hypotheses kept one
   // wave busy); the halves' integer sums combine exactly
+#if MK_SCORE_PIPE2
+  wave_tasks_screen<kScrUnroll>(
+      __builtin_amdgcn_readfirstlane(wave), NT / 64, 2 * NS, lmf, fd.scam, W, H, fd.bgr, mask, q, lmk.xyz,
+      &frames[f].cam,
+      [&](int t, PoseF& Pp, int& lb, int& le, int& tag, const Xf*& Tx) {
+        const int j = t >> 1, h = t & 1;
+        Pp = posef_from(P[j].c2w);
+        lb = nl * h / 2;
+        le = nl * (h + 1) / 2;
+        tag = j;
+        Tx = &P[j].c2w;
+      },
+      [&](int t, long long sum, int cnt) {
+        if (lane == 0) {
+          atomicAdd(&hs[t >> 1], (unsigned long long)sum);
+          atomicAdd(&hn[t >> 1], cnt);
+        }
+      });
+#else
   for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * NS; t += (NT / 64)) {
     const int j = t >> 1, h = t & 1;
     long long sum;
@@ -4412,6 +4613,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
       atomicAdd(&hn[j], n);
     }
   }
+#endif
   __syncthreads();
   block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return P[t].c2w; },
               [&](int t, int e) {

@@ -14,7 +14,13 @@ st = {k: round(v, 2) for k, v in r["stages_ms"].items() if v > 0.5}
 print(sys.argv[2], "p50", d["p50_latency_ms"], "kern", r.get("kernels_ms"), st, flush=True)
 P
 }
+# an argument VAR=value runs the in-tree library with that environment variable
 for rep in 1 2; do
   run "$R/mantis_amd/libmantis_amd.so" base || exit 1
-  for l in "$@"; do run "$R/$l" "$(basename $l .so)" || exit 1; done
+  for l in "$@"; do
+    case "$l" in
+      *=*) env "$l" bash -c "true" && export "$l" && run "$R/mantis_amd/libmantis_amd.so" "${l//[^A-Za-z0-9_]/_}"; rc=$?; unset "${l%%=*}"; [ $rc = 0 ] || exit 1 ;;
+      *) run "$R/$l" "$(basename $l .so)" || exit 1 ;;
+    esac
+  done
 done
