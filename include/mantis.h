@@ -379,6 +379,11 @@ mantis_status mantis_get_contours(void* ctx, int32_t frame, int32_t* counts, int
  * offset, overflow flags, then 7 contour-kernel phase ends (10 ns ticks).
  * Returns the number of int32 written (<= max), -1 on a bad argument. */
 int32_t mantis_frame_counters(void* ctx, int32_t frame, int32_t* out, int32_t max);
+/* Batches of at most this many frames take the latency kernels (tile Canny, segmented
+ * morphology walker, LDS border walks, 1024-thread contour blocks), larger ones the
+ * throughput kernels; both give identical results (CUs / 4 by default,
+ * MANTIS_FC_SMALL_FRAMES). No reference counterpart: a tuning query. */
+int32_t mantis_small_batch_frames(void* ctx);
 
 #ifdef __cplusplus
 }

@@ -106,6 +106,7 @@ _SIGS = {
                                           C.c_int32, C.c_void_p, C.c_void_p]),
     "mantis_rpp_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    "mantis_small_batch_frames": (C.c_int32, [C.c_void_p]),
     "mantis_rpp_solve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mantis_quad_gn": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32,

@@ -145,7 +145,9 @@ struct Ctx {
   uint32_t* d_mbits = nullptr;  // cleanImageByEdge mask bits (k_morph -> k_frame_score)
   size_t bstride = 0;                                           // words per frame
   int morph_bh = 48;       // k_morph output rows per band (MB_BH, or MB_BH_NARROW at wide max_width)
-  int morph_walk = 180;    // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
+  int morph_walk = 1 << 20;  // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
+  bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
+  int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
@@ -172,6 +174,10 @@ struct Ctx {
   int op_rounds = 6, op_spill = 32;
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
   int canny_strip = 2;  // k_canny_strip: 2 = 8 columns per lane where W % 8 == 0, 1 = 4 columns; 0 = tiles (MANTIS_CANNY_STRIP)
+  // the same for batches of at most fc_small_frames frames (the rig-latency
+  // path): tiles, whose ~230 blocks per frame run at once, where the strip
+  // walk of a frame is 720 dependent row steps (MANTIS_CANNY_STRIP sets both)
+  int canny_small = 0;
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -387,13 +393,14 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   mark(c, "start");
   const size_t B = c->bstride;
   const int tgx = (W + FTW - 1) / FTW, tgy = (H + FTH - 1) / FTH;
-  if (c->canny_strip >= 2 && c->vec_ok && W % 8 == 0 && W >= 16 && H >= 3) {
+  const int cstrip = n <= c->fc_small_frames ? c->canny_small : c->canny_strip;
+  if (cstrip >= 2 && c->vec_ok && W % 8 == 0 && W >= 16 && H >= 3) {
     // column strips walked by one wave each, 8 columns per lane (W % 8 == 0)
     const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols, nw = ns * n;
     k_canny_strip<2><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
                                                                  c->d_b1, c->d_b2, B, ns, nw);
     mark(c, "canny_nms/k_canny_strip<2>");
-  } else if (c->canny_strip && c->vec_ok && W >= 8 && H >= 3) {
+  } else if (cstrip && c->vec_ok && W >= 8 && H >= 3) {
     // 4 columns per lane (W % 4 == 0, dword-aligned rows)
     const int ns = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols, nw = ns * n;
     k_canny_strip<1><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
@@ -422,11 +429,26 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
   mark(c, "hysteresis/k_hyst_fix");
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
-  if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 64) {
-    // register walker: one wave per (frame, row segment)
-    const int seg = c->morph_walk, nseg = (H + seg - 1) / seg, nwv = nseg * n;
-    k_morph_walk<<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B, c->dstride,
-                                                               seg, nseg, nwv);
+  // the contour stage's frame states are zeroed here: the walker's run
+  // numbering writes n_runs
+  HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
+  c->runs_done = false;
+  if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 63) {
+    // register walker: one wave per (frame, row segment); with one segment per
+    // frame it also numbers the detector runs (k_run_count / scan / emit)
+    // small batches (latency): short segments, many waves per frame (the
+    // walk down a whole frame is ~1 ms of dependent steps)
+    const int seg = n <= c->fc_small_frames ? c->morph_walk_small : c->morph_walk;
+    const int nseg = (H + seg - 1) / seg, nwv = nseg * n;
+    const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st};
+    if (nseg == 1) {
+      k_morph_walk<true><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
+                                                                      c->dstride, seg, nseg, nwv, wr);
+      c->runs_done = true;
+    } else {
+      k_morph_walk<false><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
+                                                                       c->dstride, seg, nseg, nwv, wr);
+    }
     mark(c, "morph/k_morph_walk");
   } else {
     dim3 gm((H + c->morph_bh - 1) / c->morph_bh, n);
@@ -443,12 +465,13 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
 mantis_status run_contours(Ctx* c, int n, int W, int H) {
   const size_t P = c->plane;
   const int Wp = W + 2, Hp = H + 2;
-  HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
   dim3 grow((Hp + 4 * RUN_RPW - 1) / (4 * RUN_RPW), n);  // k_run_count / emit / border: RUN_RPW rows per wave
   uint16_t* rx = c->d_lroot;  // free after hysteresis: run starts (u16, one run per pixel at most)
-  k_run_count<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, Wp, Hp);
-  k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
-  k_run_emit<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
+  if (!c->runs_done) {  // the morphology walker numbered the runs already
+    k_run_count<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, Wp, Hp);
+    k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
+    k_run_emit<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
+  }
   k_run_band<<<dim3((Hp + RB_ROWS - 1) / RB_ROWS, n), 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
   const int seams = (Hp - 1) / RB_ROWS;
   if (seams > 0)
@@ -885,7 +908,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
-  if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = std::atoi(e);
+  if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
@@ -927,8 +950,12 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     return MANTIS_ERR_ARG;
   }
   c->morph_bh = morph_lds(c->Wmax, MB_BH) <= 160 * 1024 ? MB_BH : MB_BH_NARROW;
-  if (const char* e = getenv("MANTIS_MORPH_WALK")) c->morph_walk = std::max(0, atoi(e));
+  if (const char* e = getenv("MANTIS_MORPH_WALK")) {  // an explicit choice applies to every batch size
+    c->morph_walk = std::max(0, atoi(e));
+    c->morph_walk_small = std::max(1, c->morph_walk);
+  }
   if (const char* e = getenv("MANTIS_SPIN_FRAMES")) c->spin_frames = atoi(e);
+  if (const char* e = getenv("MANTIS_MORPH_WALK_SMALL")) c->morph_walk_small = std::max(1, atoi(e));
   if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)morph_lds(c->Wmax, c->morph_bh)) !=
@@ -1821,6 +1848,10 @@ mantis_status mantis_synchronize(void* ctx) {
   if (!c) return MANTIS_ERR_ARG;
   HIP_OK(hipStreamSynchronize(c->s));
   return MANTIS_OK;
+}
+int32_t mantis_small_batch_frames(void* ctx) {
+  const Ctx* c = (const Ctx*)ctx;
+  return c ? c->fc_small_frames : -1;
 }
 int32_t mantis_kernel_times(void* ctx, const char** names, float* ms, int32_t max) {
   Ctx* c = (Ctx*)ctx;

@@ -639,16 +639,34 @@ struct StripWave {
   uint32_t* cb;
   uint32_t* sbp;
   uint32_t nx[K][3];  // input row i (prefetched)
+#if MK_CANNY_PF > 1
+  uint32_t nx2[K][3];  // input row i + 1 (prefetch depth 2)
+#endif
 };
+#ifndef MK_CANNY_PF
+#define MK_CANNY_PF 1  // BGR rows in flight per wave (1: the next row; 2: the next two)
+#endif
 template <int K>
-__device__ __forceinline__ void strip_load(StripWave<K>& w, int row) {
+__device__ __forceinline__ void strip_load_to(const StripWave<K>& w, int row, uint32_t (&d)[K][3]) {
 #pragma unroll
   for (int k = 0; k < K; k++) {
     gu32* q = gwords(w.bgr + (w.loff + 12u * k + (uint32_t)row * w.rstep));
-    w.nx[k][0] = q[0];
-    w.nx[k][1] = q[1];
-    w.nx[k][2] = q[2];
+    d[k][0] = q[0];
+    d[k][1] = q[1];
+    d[k][2] = q[2];
   }
+}
+template <int K>
+__device__ __forceinline__ void strip_load(StripWave<K>& w, int row) {
+#if MK_CANNY_PF > 1
+#pragma unroll
+  for (int k = 0; k < K; k++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) w.nx[k][j] = w.nx2[k][j];
+  strip_load_to(w, row + 1 < w.H ? row + 1 : w.H - 1, w.nx2);
+#else
+  strip_load_to(w, row, w.nx);
+#endif
 }
 // Iteration i of the walk (S = i % 3): hblur(i), blur(i-1), Sobel(i-2), NMS(i-3).
 // ROWS: the frame's first / last rows may be among them (else all four rows
@@ -899,7 +917,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 
   w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes &&
                  base + G * (w.lane & ~(LPW - 1)) < W;
   StripRegs<K> R = {};
+#if MK_CANNY_PF > 1
+  strip_load_to(w, 0, w.nx);
+  strip_load_to(w, 1 < w.H ? 1 : 0, w.nx2);
+#else
   strip_load(w, 0);
+#endif
   if (sidx == 0 || sidx == nstrip - 1) strip_walk<K, true>(w, R);
   else strip_walk<K, false>(w, R);
 }
@@ -1492,9 +1515,22 @@ __device__ inline uint32_t mw_m0(uint32_t e, uint32_t nu, uint32_t n, uint32_t n
   const uint32_t right = __builtin_amdgcn_alignbit(dpp_from_right(n), n, 1);  // ng(x + 1)
   return (e | (n & (~left | ~right | ~nu | ~nd))) & vm;
 }
+// RUNS (one segment per frame): the walker also numbers the runs of each
+// padded detector row as it produces it -- the outputs of k_run_count /
+// k_run_scan / k_run_emit (row bases, run starts, labels = own ids, n_runs),
+// with a running id in an SGPR instead of a frame-wide scan.
+struct WalkRuns {
+  int32_t* rowb;
+  size_t rstride;
+  uint16_t* rx;
+  int32_t* lab;
+  size_t plane;
+  FrameState* st;
+};
+template <bool RUNS>
 __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                     uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
-                                                    size_t dstride, int seg_rows, int nseg, int nwaves) {
+                                                    size_t dstride, int seg_rows, int nseg, int nwaves, WalkRuns wr) {
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   if (gw >= nwaves) return;
   const int lane = threadIdx.x & 63;
@@ -1508,6 +1544,30 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   // padded detector ring rows (zero) by the first / last segment
   if (sg == 0 && lane < wpw) D[lane] = 0u;
   if (ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
+  int32_t* RB = RUNS ? wr.rowb + (size_t)f * wr.rstride : nullptr;
+  uint16_t* RX = RUNS ? wr.rx + (size_t)f * wr.plane : nullptr;
+  int32_t* RL = RUNS ? wr.lab + (size_t)f * wr.plane : nullptr;
+  int run_id = 0;  // next run id (wave-uniform)
+  // runs of padded row py (words v, lanes < wpw): the ring run at x = 0, then
+  // one run per transition, in lane (word) order
+  const auto emit_runs = [&](uint32_t v, int py) {
+    const uint32_t prv = dpp_from_left(v);
+    const uint32_t T = v ^ ((v << 1) | (prv >> 31));
+    const int c = __popc(T);
+    const int inc = wave_incl_scan(c, lane);
+    if (lane == 0) {
+      RB[py] = run_id;
+      RX[run_id] = 0;
+      RL[run_id] = run_id;
+    }
+    int o = run_id + 1 + inc - c;
+    for (uint32_t t = T; t; t &= t - 1, o++) {
+      RX[o] = (uint16_t)(32 * lane + __ffs(t) - 1);
+      RL[o] = o;
+    }
+    run_id += 1 + __builtin_amdgcn_readlane(inc, 63);
+  };
+  if (RUNS) emit_runs(0u, 0);
   MwStage<2, true> d1;   // detector dilate 5x5 of E
   MwStage<1, false> d2;  // detector erode 3x3
   MwStage<3, true> s1;
@@ -1546,8 +1606,15 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     {
       const uint32_t p0 = dpp_from_left(b0), p1 = dpp_from_left(b1);
       const int y = i - 3;
-      if (y >= ys && y < ye && lane < wpw) D[(size_t)(y + 1) * wpw + lane] = (b0 << 1) | (p0 >> 31);
-      if (y + 1 >= ys && y + 1 < ye && lane < wpw) D[(size_t)(y + 2) * wpw + lane] = (b1 << 1) | (p1 >> 31);
+      const uint32_t v0 = lane < wpw ? (b0 << 1) | (p0 >> 31) : 0u, v1 = lane < wpw ? (b1 << 1) | (p1 >> 31) : 0u;
+      if (y >= ys && y < ye) {
+        if (lane < wpw) D[(size_t)(y + 1) * wpw + lane] = v0;
+        if (RUNS) emit_runs(v0, y + 1);
+      }
+      if (y + 1 >= ys && y + 1 < ye) {
+        if (lane < wpw) D[(size_t)(y + 2) * wpw + lane] = v1;
+        if (RUNS) emit_runs(v1, y + 2);
+      }
     }
     // mask: {dilate, erode}(3), (4), (5), erode(3): M0 rows i - 2, i - 1 in; i - 29, i - 28 out
     s1.push2(m0, in(i - 2), m1, in(i - 1), a0, a1);
@@ -1560,6 +1627,13 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     const int y = i - MB_HALO;
     if (y >= ys && y < ye && lane < WW) M[bits::tiled_word(y, lane, WW)] = a0 & vm;
     if (y + 1 >= ys && y + 1 < ye && lane < WW) M[bits::tiled_word(y + 1, lane, WW)] = a1 & vm;
+  }
+  if (RUNS) {
+    emit_runs(0u, H + 1);
+    if (lane == 0) {
+      RB[H + 2] = run_id;
+      wr.st[f].n_runs = run_id;
+    }
   }
 }
 
@@ -4551,6 +4625,14 @@ __global__ __launch_bounds__(NT) void k_score_final(
   __shared__ int32_t hn[96];
   __shared__ uint32_t uqe[kTailQueue];
   __shared__ int32_t uqn;
+#ifdef MK_SCORE_TICKS  // diagnostics: phase ends of this kernel into st[f].ticks (10 ns), tools/score_ticks.py
+  const uint64_t tk0 = wall_clock64();
+  int32_t* tk = const_cast<FrameState*>(st)[f].ticks;
+#define MK_STICK(k) \
+  if (tid == 0) tk[k] = (int32_t)(wall_clock64() - tk0);
+#else
+#define MK_STICK(k)
+#endif
   for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
   if (tid == 0) {
     uqn = 0;
@@ -4615,6 +4697,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   }
 #endif
   __syncthreads();
+  MK_STICK(0);
   block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return P[t].c2w; },
               [&](int t, int e) {
                 atomicAdd(&hs[t], (unsigned long long)e);
@@ -4630,6 +4713,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
     D.shift_err[tid] = e;
   }
   __syncthreads();
+  MK_STICK(1);
   // getBestNHypotheses(20) (HypothesisEvaluation.h:484-518): std::sort by
   // descending error, keep the last 20. When the 20 smallest errors are all
   // distinct from every other error, their sorted positions follow from
@@ -4662,6 +4746,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
     nsc += NS;
   }
   __syncthreads();
+  MK_STICK(2);
   // determineBestYaw: 4 yaw sets (rotZ^k * w2c, left-multiplied), COLOR errors
   // on the original image. Set k derives from set k-1; all four are built
   // first (P[20k + i], the shifts are no longer needed) so their 80 scorings
@@ -4683,6 +4768,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
     }
   }
   __syncthreads();
+  MK_STICK(3);
   const double* green = lmk.xyz + 3 * (lmk.nw + lmk.nr);
   __shared__ double yset_err[80];
 #ifdef MK_DIAG_NO_COLOR  // timing diagnostic only: wrong results
@@ -4706,6 +4792,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
     __syncthreads();
   }
 #endif
+  MK_STICK(4);
   if (tid == 0) {
     double best_error = DBL_MAX;
     int best_k = -1;
@@ -4769,6 +4856,8 @@ __global__ __launch_bounds__(NT) void k_score_final(
       D.publish = R.publish;
     }
   }
+  MK_STICK(5);
+#undef MK_STICK
 }
 
 // ============================================ legacy rig weighting (f-4)

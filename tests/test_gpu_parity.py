@@ -69,7 +69,7 @@ def test_canny_bit_exact_odd_sizes_and_noise(mantis):
         assert np.array_equal(got, ref), f"{w}x{h}: canny differs at {np.argwhere(got != ref)[:10]}"
 
 
-@pytest.mark.parametrize("strip", ["1", "0"])
+@pytest.mark.parametrize("strip", ["2", "1", "0"])
 def test_canny_strip_and_tile_kernels_bit_exact(strip):
     """Both Canny kernels (k_canny_strip: column strips walked by one wave,
     DPP neighbour taps; k_canny: 128x32 LDS tiles; MANTIS_CANNY_STRIP picks)
@@ -116,19 +116,21 @@ def test_detector_binary_and_mask_bit_exact(mantis, frames):
         assert np.array_equal(mask, ref_mask), f"clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
 
 
-@pytest.mark.parametrize("walk", ["180", "64", "7", "0"])
+@pytest.mark.parametrize("walk", ["1048576", "180", "64", "7", "0"])
 def test_morphology_kernels_bit_exact(walk):
     """Both morphology kernels (k_morph_walk: one wave per frame row segment,
-    stage windows in registers, MANTIS_MORPH_WALK = segment rows; k_morph: LDS
-    bands, MANTIS_MORPH_WALK=0) against the oracle's detector binary and
-    cleanImageByEdge mask: widths ending mid-word, segments shorter than the
-    29-row reach, frames shorter than it, blob noise and i.i.d. noise."""
+    stage windows in registers, MANTIS_MORPH_WALK = segment rows; with one
+    segment per frame it also numbers the detector runs for the contour CCL;
+    k_morph: LDS bands, MANTIS_MORPH_WALK=0) against the oracle's detector
+    binary and cleanImageByEdge mask, and the contours that follow against
+    findContours: widths ending mid-word, segments shorter than the 29-row
+    reach, frames shorter than it, blob noise and i.i.d. noise."""
     import mantis_amd as M
 
     saved = os.environ.get("MANTIS_MORPH_WALK")
     os.environ["MANTIS_MORPH_WALK"] = walk
     try:
-        mt = M.Mantis(max_cams=1, max_width=1920, max_height=1080)
+        mt = M.Mantis(max_cams=1, max_width=1920, max_height=1080, max_contour_points=1 << 21)
     finally:
         if saved is None:
             os.environ.pop("MANTIS_MORPH_WALK")
@@ -151,6 +153,14 @@ def test_morphology_kernels_bit_exact(walk):
             ref_mask = O.clean_mask(cn)
             assert np.array_equal(det, ref_det), f"{w}x{h}: detector binary differs: {np.count_nonzero(det != ref_det)} px"
             assert np.array_equal(mask, ref_mask), f"{w}x{h}: clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
+            if k % 2 == 1 and w * h > 100000:
+                continue  # i.i.d. noise at full size: masks only (its contours are millions of points)
+            mt.detect_quads(M.make_image(img, K, D))
+            cnt = mt.frame_counters(0)
+            cs, _ = O.find_contours(ref_det, 2)
+            assert cnt[8] == 0, f"{w}x{h}: overflow flags {cnt[8]}"
+            assert cnt[0] == len(cs), f"{w}x{h}: borders {cnt[0]} vs findContours {len(cs)}"
+            _contours_equal(mt, img)
     finally:
         mt.close()
 

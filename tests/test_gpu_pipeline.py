@@ -807,3 +807,53 @@ def test_reason4_no_green_landmarks_match_oracle(landmark_map):
         assert m.rng_state == orc.rng_state
     finally:
         m.close()
+
+
+def test_throughput_and_latency_kernel_paths_agree(landmark_map):
+    """Batches above CUs / 4 frames take the throughput kernels (strip Canny,
+    the morphology walker that numbers the runs, the L2 border walks, 256-thread
+    contour blocks); one rig at a time takes the latency ones (tile Canny,
+    segmented walker + run kernels, LDS border walks, 1024-thread contour
+    blocks), which the oracle tests cover. The same 72 rendered frames through
+    both: every camera result, frame record and the cv::RNG state bit-identical."""
+    import mantis_amd as M
+
+    W, H, CAMS, RIGS = 1280, 720, 4, 18
+    K, D = synth.intrinsics(W, H)
+    ext = synth.rig_extrinsics(CAMS)
+    rng = np.random.default_rng(404)
+    cams = []
+    for r in range(RIGS):
+        Twb = synth.random_base_pose(rng)
+        for c in range(CAMS):
+            Twc = Twb @ ext[c]
+            cams.append(synth.make_cam(Twc[:3, :3], Twc[:3, 3], W, H))
+    mb = M.Mantis(max_cams=RIGS * CAMS, max_width=W, max_height=H)
+    ms = M.Mantis(max_cams=CAMS, max_width=W, max_height=H)
+    try:
+        assert RIGS * CAMS > M.lib().mantis_small_batch_frames(mb.h)
+        for m in (mb, ms):
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+        fb = W * H * 3
+        dev = mb.device_alloc(len(cams) * fb)
+        mb.synth_render(cams, [synth.frame_seed(6, i) for i in range(len(cams))], dev)
+        mb.synchronize()
+        imgs = [M.make_image(None, K, D, T_base_cam=ext[i % CAMS], device_ptr=dev + i * fb, width=W, height=H)
+                for i in range(len(cams))]
+        rb, cb = mb.process(imgs, rigs=RIGS)
+        dbg_b = [bytes(mb.frame_debug(i)) for i in range(len(cams))]
+        cnt_b = [mb.frame_counters(i)[:10].copy() for i in range(len(cams))]
+        for r in range(RIGS):
+            rs, cs = ms.process(imgs[r * CAMS:(r + 1) * CAMS], rigs=1)
+            assert bytes(rs[0]) == bytes(rb[r]), f"rig {r}"
+            for c in range(CAMS):
+                assert bytes(cs[c]) == bytes(cb[r * CAMS + c]), f"rig {r} cam {c}"
+                assert bytes(ms.frame_debug(c)) == dbg_b[r * CAMS + c], f"rig {r} cam {c} debug record"
+                a, b = ms.frame_counters(c)[:10], cnt_b[r * CAMS + c]
+                assert np.array_equal(a[[0, 1, 2, 3, 4, 5, 6, 8, 9]], b[[0, 1, 2, 3, 4, 5, 6, 8, 9]]), (r, c)
+        assert ms.rng_state == mb.rng_state
+        mb.device_free(dev)
+    finally:
+        mb.close()
+        ms.close()
