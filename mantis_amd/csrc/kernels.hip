@@ -618,6 +618,14 @@ struct StripGeom {
   static constexpr int cols = out_lanes * 4 * K;            // columns per strip
   static constexpr int lanes_per_word = 8 / K;
 };
+// BGR rows a wave keeps in flight: K = 2 has the registers for MK_CANNY_PF
+// (126 VGPRs at depth 2, under the 128 of 4 waves per SIMD; depth 3 spills),
+// K = 1 (64 VGPRs for 8 waves) only for one
+#ifndef MK_CANNY_PF
+#define MK_CANNY_PF 1
+#endif
+template <int K>
+constexpr int strip_pf() { return K == 2 ? MK_CANNY_PF : 1; }
 // Per-wave state of a strip: three row slots per stage (row r in slot r % 3),
 // so the walk unrolled by three indexes registers with constants and moves
 // nothing between rows.
@@ -638,14 +646,10 @@ struct StripWave {
   s16x2 LOW, HIGH;
   uint32_t* cb;
   uint32_t* sbp;
-  uint32_t nx[K][3];  // input row i (prefetched)
-#if MK_CANNY_PF > 1
-  uint32_t nx2[K][3];  // input row i + 1 (prefetch depth 2)
-#endif
+  // BGR rows in flight (strip_pf): 1 = row i, 2 = rows i, i+1 (shifted down a
+  // slot per row), 3 = rows i .. i+2 in slots i % 3 (the walk's unroll)
+  uint32_t rows[strip_pf<K>()][K][3];
 };
-#ifndef MK_CANNY_PF
-#define MK_CANNY_PF 1  // BGR rows in flight per wave (1: the next row; 2: the next two)
-#endif
 template <int K>
 __device__ __forceinline__ void strip_load_to(const StripWave<K>& w, int row, uint32_t (&d)[K][3]) {
 #pragma unroll
@@ -656,17 +660,27 @@ __device__ __forceinline__ void strip_load_to(const StripWave<K>& w, int row, ui
     d[k][2] = q[2];
   }
 }
-template <int K>
-__device__ __forceinline__ void strip_load(StripWave<K>& w, int row) {
-#if MK_CANNY_PF > 1
+// the input row of iteration i (S = i % 3) and the load that replaces it:
+// row i + strip_pf (the last row again past the end)
+template <int K, int S>
+__device__ __forceinline__ const uint32_t (&strip_row(const StripWave<K>& w))[K][3] {
+  return w.rows[strip_pf<K>() == 3 ? S : 0];
+}
+template <int K, int S>
+__device__ __forceinline__ void strip_advance(StripWave<K>& w, int i) {
+  constexpr int PF = strip_pf<K>();
+  const int r = i + PF < w.H ? i + PF : w.H - 1;
+  if constexpr (PF == 3) {
+    strip_load_to(w, r, w.rows[S]);
+  } else {
 #pragma unroll
-  for (int k = 0; k < K; k++)
+    for (int p = 0; p + 1 < PF; p++)
 #pragma unroll
-    for (int j = 0; j < 3; j++) w.nx[k][j] = w.nx2[k][j];
-  strip_load_to(w, row + 1 < w.H ? row + 1 : w.H - 1, w.nx2);
-#else
-  strip_load_to(w, row, w.nx);
-#endif
+      for (int k = 0; k < K; k++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) w.rows[p][k][j] = w.rows[p + 1][k][j];
+    strip_load_to(w, r, w.rows[PF - 1]);
+  }
 }
 // Iteration i of the walk (S = i % 3): hblur(i), blur(i-1), Sobel(i-2), NMS(i-3).
 // ROWS: the frame's first / last rows may be among them (else all four rows
@@ -684,9 +698,12 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
   // ---- gray and horizontal blur of input row i
   if (!ROWS || i < H) {
     uint32_t g[K];
+    {
+      const uint32_t(&nx)[K][3] = strip_row<K, S>(w);
 #pragma unroll
-    for (int k = 0; k < K; k++) g[k] = gray4(w.nx[k][0], w.nx[k][1], w.nx[k][2]);
-    strip_load(w, i + 1 < H ? i + 1 : i);  // next row (the last row again at the end)
+      for (int k = 0; k < K; k++) g[k] = gray4(nx[k][0], nx[k][1], nx[k][2]);
+    }
+    strip_advance<K, S>(w, i);
     uint32_t gl = dpp_from_left(g[K - 1]), gr = dpp_from_right(g[0]);
     if (EDGE && w.left_edge) gl = g[0] << 16;       // gray(-1) = gray(1)
     if (EDGE && w.right_edge) gr = g[K - 1] >> 16;  // gray(W) = gray(W-2)
@@ -917,12 +934,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 
   w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes &&
                  base + G * (w.lane & ~(LPW - 1)) < W;
   StripRegs<K> R = {};
-#if MK_CANNY_PF > 1
-  strip_load_to(w, 0, w.nx);
-  strip_load_to(w, 1 < w.H ? 1 : 0, w.nx2);
-#else
-  strip_load(w, 0);
-#endif
+#pragma unroll
+  for (int p = 0; p < strip_pf<K>(); p++) strip_load_to(w, p < w.H ? p : w.H - 1, w.rows[p]);
   if (sidx == 0 || sidx == nstrip - 1) strip_walk<K, true>(w, R);
   else strip_walk<K, false>(w, R);
 }
