@@ -413,7 +413,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   }
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
   HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
-              HB_ROWS * ((W + 1) / 2)};
+              HB_ROWS * ((W + 1) / 2), c->d_st};
   // list counters |A|, |B| of every frame (rowb[H + 1], rowb[H + 2])
   HIP_OK(hipMemset2DAsync(c->d_rowb + H + 1, c->rstride * sizeof(int32_t), 0, 2 * sizeof(int32_t), n, c->s));
   const int WWb = bits::words(W);

@@ -997,6 +997,7 @@ struct HystRuns {  // per-frame planes (frame f at + f * stride)
                    // [H + 3 + b] = runs of band b
   size_t x_stride, lab_stride, flag_stride, rstride, half;
   int bs;          // run ids per band: run i of band b is b * bs + i (bs = band rows x ceil(W / 2))
+  FrameState* st;  // diagnostics only (MK_HYST_TICKS: phase ends of one band per frame into st[f].ticks)
 };
 
 // Per band of HB_ROWS rows: unions in LDS (labels = band roots, written to
@@ -1109,12 +1110,20 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   uint32_t* Cw = Sw + nr * WW;
   const uint32_t* sb = sbits + (size_t)f * bstride + (size_t)y0 * WW;
   const uint32_t* cb = cbits + (size_t)f * bstride + (size_t)y0 * WW;
+#ifdef MK_HYST_TICKS  // diagnostics: phase ends of the middle band's block (10 ns), tools/hyst_ticks.py
+  const uint64_t tk0 = wall_clock64();
+#define MK_HTICK(k) \
+  if (t == 0 && band == (H / HB_ROWS) / 2) hr.st[f].ticks[k] = (int32_t)(wall_clock64() - tk0);
+#else
+#define MK_HTICK(k)
+#endif
   for (int i = t; i < nr * WW; i += HB_THREADS) {
     Ew[i] = 0u;
     Sw[i] = sb[i];
     Cw[i] = cb[i];
   }
   __syncthreads();
+  MK_HTICK(0);
   // runs per row (wave per row), then the band's row bases
   for (int q = wave; q < nr; q += HB_WAVES) {
     int c = 0;
@@ -1134,6 +1143,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
     if (t == nr - 1) rb[H + 3 + band] = s;
   }
   __syncthreads();
+  MK_HTICK(1);
   const int n = rbl[nr];
   // a row whose components may continue past the band: its first / last row inside the frame
   const auto edge_row = [&](int q) { return (q == 0 && y0 > 0) || (q == nr - 1 && y1 < H); };
@@ -1176,11 +1186,13 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   for (int i = t; i < (n + 3) / 4; i += HB_THREADS) Sl[i] = 0u;
 #endif
   __syncthreads();
+  MK_HTICK(2);
   uint16_t* Li = Ll;
   const auto uni = [Li](int a, int b) { hb_union(Li, a, b); };
   for (int q = 1 + wave; q < nr; q += HB_WAVES)
     hyst_row_union(Xl, rbl[q - 1], rbl[q] - rbl[q - 1], rbl[q], rbl[q + 1] - rbl[q], lane, uni);
   __syncthreads();
+  MK_HTICK(3);
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = hb_find(Ll, j);
@@ -1198,6 +1210,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
     }
   }
   __syncthreads();
+  MK_HTICK(4);
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
 #if MK_HB_LFLAGS
@@ -1224,6 +1237,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
     }
   }
   __syncthreads();
+  MK_HTICK(5);
   for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = Ew[i];
 }
 
@@ -2717,8 +2731,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     }
   };
   const uint64_t t0 = wall_clock64();
+#ifdef MK_HYST_TICKS  // the ticks are k_hyst_band's
+#define MK_TICK(k)
+#else
 #define MK_TICK(k) \
   if (tid == 0) st[f].ticks[k] = (int32_t)(wall_clock64() - t0);
+#endif
   if (tid == 0) { nraw = 0; total = 0; nlong = 0; nchunk = st[f].n_chunks; }
   __syncthreads();
 
@@ -4495,6 +4513,20 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     cur_err = sst[f].cur.err;
   }
   __syncthreads();
+#if defined(MK_SCORE_TICKS) && MK_SCORE_TICKS == 2  // diagnostics: this kernel's phases summed over the iterations
+  // into st[f].ticks (10 ns): staging, particles, screened tasks, drain, sums, argmin (tools/score_ticks.py pf)
+  uint64_t tkp = wall_clock64();
+  int32_t tka[6] = {0, 0, 0, 0, 0, 0};
+#define MK_PTICK(k)                                \
+  if (tid == 0) {                                  \
+    const uint64_t nw = wall_clock64();            \
+    tka[k] += (int32_t)(nw - tkp);                 \
+    tkp = nw;                                      \
+  }
+#else
+#define MK_PTICK(k)
+#endif
+  MK_PTICK(0);
   const float* gs = gauss + st[f].gauss_offset;
   const UQueue q{uqe, &uqn, kPfQueue};
   const MaskLds mlds{(lds_cu32*)pf_mask, bits::words(W)};
@@ -4515,6 +4547,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     }
     if (tid == 0) uqn = 0;
     __syncthreads();
+    MK_PTICK(1);
     // SPLIT waves per particle (landmark slices; integer sums, so the
     // partials combine exactly in any order); a wave's tasks pipelined
 #if MK_SCORE_PIPE2
@@ -4556,6 +4589,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     }
 #endif
     __syncthreads();
+    MK_PTICK(2);
     const auto pose_of = [&](int t) -> const Xf& { return Pc[t]; };
     const auto add = [&](int t, int e) {
       atomicAdd(&Ps[t * SPLIT], (unsigned long long)e);
@@ -4564,6 +4598,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     if (LM) block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mlds, pose_of, add);
     else block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mglb, pose_of, add);
     __syncthreads();
+    MK_PTICK(3);
     if (tid < particles) {
       long long sum = 0;
       int cnt = 0;
@@ -4574,6 +4609,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
       Pe[tid] = cnt <= 0 ? DBL_MAX : (double)sum / ((double)cnt * 1.1);
     }
     __syncthreads();
+    MK_PTICK(4);
     if (wave == 0) {
       double be = DBL_MAX;
       int bj = 0x7fffffff;
@@ -4594,7 +4630,13 @@ __global__ __launch_bounds__(NT) void k_score_pf(
       }
     }
     __syncthreads();
+    MK_PTICK(5);
   }
+#if defined(MK_SCORE_TICKS) && MK_SCORE_TICKS == 2
+  if (tid == 0)
+    for (int k = 0; k < 6; k++) const_cast<FrameState*>(st)[f].ticks[k] = tka[k];
+#endif
+#undef MK_PTICK
   if (tid == 0) {
     ScoreState& S = sst[f];
     S.cur.c2w = cur_c2w;
@@ -4638,7 +4680,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   __shared__ int32_t hn[96];
   __shared__ uint32_t uqe[kTailQueue];
   __shared__ int32_t uqn;
-#ifdef MK_SCORE_TICKS  // diagnostics: phase ends of this kernel into st[f].ticks (10 ns), tools/score_ticks.py
+#if defined(MK_SCORE_TICKS) && MK_SCORE_TICKS != 2  // diagnostics: phase ends of this kernel into st[f].ticks (10 ns), tools/score_ticks.py
   const uint64_t tk0 = wall_clock64();
   int32_t* tk = const_cast<FrameState*>(st)[f].ticks;
 #define MK_STICK(k) \

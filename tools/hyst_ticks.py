@@ -1,11 +1,9 @@
-"""Phase times of k_score_final per frame (a library built with
--DMK_SCORE_TICKS, MANTIS_AMD_LIB): one context, one batch of bench rigs;
-median / p90 of each phase over the frames that reach the particle filter.
-Phases: shift tasks, unsure drain, top-20, yaw-set build, COLOR windows, publish.
-With "pf" (a library built with -DMK_SCORE_TICKS=2): k_score_pf (the particle filter)'s
-phases summed over its iterations: mask staging, particle poses, screened
-tasks, unsure drain, per-particle sums, argmin.
-usage: MANTIS_AMD_LIB=abvar/ticks.so python tools/score_ticks.py [pf] [rigs]"""
+"""Phase times of k_hyst_band (middle band of each frame; a library built with
+-DMK_HYST_TICKS, MANTIS_AMD_LIB): one context, one batch of bench rigs;
+median / p90 of each phase over the frames (wall clock: the block shares its
+CU with others, so the phases' shares matter more than their sums).
+Phases: planes to LDS, run counts + row bases, run extents + label init, row unions, finds + band flags, global writes + lists (the edge-word store after them is not timed).
+usage: MANTIS_AMD_LIB=abvar/hticks.so python tools/hyst_ticks.py [rigs]"""
 import os
 import sys
 
@@ -15,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(rigs, pf=False):
+def main(rigs):
     import mantis_amd as M
     from mantis_amd import synth
 
@@ -44,16 +42,10 @@ def main(rigs, pf=False):
     tk = []
     for i in range(n):
         fc = m.frame_counters(i)
-        if m.frame_debug(i).n_hyps > 0:
-            tk.append(fc[10:16].astype(np.float64) * 0.01)  # 10 ns ticks -> us
+        tk.append(fc[10:16].astype(np.float64) * 0.01)  # 10 ns ticks -> us
     tk = np.array(tk)
-    if pf:  # per-phase sums already
-        d = tk
-        tk = np.cumsum(tk, axis=1)
-        names = ["staging", "particles", "tasks", "drain", "sums", "argmin"]
-    else:
-        d = np.diff(np.concatenate([np.zeros((len(tk), 1)), tk], 1), axis=1)
-        names = ["shift tasks", "drain", "top-20", "yaw build", "COLOR", "publish"]
+    d = np.diff(np.concatenate([np.zeros((len(tk), 1)), tk], 1), axis=1)
+    names = ["load", "counts+scan", "runs+init", "unions", "finds+flags", "writes+lists"]
     for j, nm in enumerate(names):
         print(f"{nm:12s} median {np.median(d[:, j]):8.1f} us  p90 {np.percentile(d[:, j], 90):8.1f} us")
     print(f"total        median {np.median(tk[:, 5]):8.1f} us over {len(tk)} frames")
@@ -61,7 +53,4 @@ def main(rigs, pf=False):
 
 
 if __name__ == "__main__":
-    a = sys.argv[1:]
-    pf = bool(a) and a[0] == "pf"
-    a = a[1:] if pf else a
-    main(int(a[0]) if a else 256, pf)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 256)
