@@ -431,7 +431,15 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   // the contour stage's frame states are zeroed here: the walker's run
   // numbering writes n_runs
+#ifdef MK_HYST_TICKS  // diagnostics: keep k_hyst_band's ticks
+  {
+    const size_t a = offsetof(FrameState, ticks), b = a + sizeof(FrameState::ticks);
+    HIP_OK(hipMemset2DAsync(c->d_st, sizeof(FrameState), 0, a, n, c->s));
+    HIP_OK(hipMemset2DAsync((char*)c->d_st + b, sizeof(FrameState), 0, sizeof(FrameState) - b, n, c->s));
+  }
+#else
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
+#endif
   c->runs_done = false;
   if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 63) {
     // register walker: one wave per (frame, row segment); with one segment per

@@ -1015,6 +1015,9 @@ struct HystRuns {  // per-frame planes (frame f at + f * stride)
 #ifndef MK_HB_THREADS
 #define MK_HB_THREADS 512
 #endif
+#ifndef MK_HB_LISTAGG
+#define MK_HB_LISTAGG 0  // dense bands' list entries placed per block (one global atomic per list) instead of per wave
+#endif
 constexpr int HB_ROWS = MK_HB_ROWS, HB_CAP = 4096, HB_THREADS = MK_HB_THREADS, HB_WAVES = HB_THREADS / 64;
 // global id of row y's first run and the row's run count
 __device__ inline void hr_row(const int32_t* rb, int H, int bs, int y, int& g, int& cnt) {
@@ -1211,6 +1214,10 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   }
   __syncthreads();
   MK_HTICK(4);
+#if MK_HB_LISTAGG
+  __shared__ int32_t lcnt[HB_WAVES][2], lbase[2], ltot[2];
+  int nA = 0, nB = 0;  // this wave's list entries (wave-uniform)
+#endif
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
 #if MK_HB_LFLAGS
@@ -1232,11 +1239,57 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
         const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
         for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
       }
+#if MK_HB_LISTAGG
+      nB += __popcll(__ballot(fb == 2));
+      nA += __popcll(__ballot(root == j && fb == 3));
+#else
       hyst_push(lists, cnt + 1, g0 + j, fb == 2, true, top);
       hyst_push(lists, cnt, g0 + j, root == j && fb == 3, false, top);
+#endif
     }
   }
+#if MK_HB_LISTAGG
+  // list entries: the waves' counts, one global atomic per list and block,
+  // then each wave writes its entries from its own base (no atomic per wave)
+  if (lane == 0) {
+    lcnt[wave][0] = nA;
+    lcnt[wave][1] = nB;
+  }
   __syncthreads();
+  if (t < 2) {
+    int tot = 0;
+    for (int v = 0; v < HB_WAVES; v++) {
+      const int c = lcnt[v][t];
+      lcnt[v][t] = tot;
+      tot += c;
+    }
+    lbase[t] = tot ? atomicAdd(cnt + t, tot) : 0;
+    ltot[t] = tot;
+  }
+  __syncthreads();
+  if (ltot[0] | ltot[1]) {
+    int oA = lbase[0] + lcnt[wave][0], oB = lbase[1] + lcnt[wave][1];
+    const uint64_t below = (1ull << lane) - 1;
+    for (int q = wave; q < nr; q += HB_WAVES)
+      for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
+#if MK_HB_LFLAGS
+        const int root = Ll[j] & 0xfff;
+        const int fb = (Ll[root] >> 12) & 3;
+#else
+        const int root = Ll[j];
+        const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
+#endif
+        const bool pa = root == j && fb == 3, pb = fb == 2;
+        const uint64_t ma = __ballot(pa), mb = __ballot(pb);
+        if (pa) lists[oA + __popcll(ma & below)] = g0 + j;
+        if (pb) lists[top - 1 - (oB + __popcll(mb & below))] = g0 + j;
+        oA += __popcll(ma);
+        oB += __popcll(mb);
+      }
+  }
+#else
+  __syncthreads();
+#endif
   MK_HTICK(5);
   for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = Ew[i];
 }
@@ -4068,7 +4121,11 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
     // needed), so the U loads of a lane are in flight together
     uint32_t mw[U];
 #pragma unroll
+#ifdef MK_PF_EXP_NOMASK  // cost experiment (wrong results): no mask lookups, every pixel a hit
+    for (int k = 0; k < U; k++) mw[k] = 0xffffffffu;
+#else
     for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+#endif
     uint32_t pv[U];
     int hm[U];
 #pragma unroll
@@ -4077,7 +4134,11 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
       hm[k] = hit ? -1 : 0;
       const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
       typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
+#ifdef MK_PF_EXP_NOPIX  // cost experiment (wrong results): no pixel gathers
+      pv[k] = (uint32_t)off;
+#else
       pv[k] = *(gu32u*)(bgr + off);
+#endif
     }
     // the terms as masks, not selects: every loaded value is consumed, so the
     // compiler keeps the U loads unconditional (in flight together) instead
