@@ -149,6 +149,8 @@ struct Ctx {
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
+  bool pf_split = true;    // small batches: each particle-filter iteration over several blocks per frame
+                           // (k_score_pf_part); MANTIS_PF_SPLIT=0 keeps one block per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
   uint32_t* d_tbits = nullptr;                                  // the same in 32x32 tiles (k_trace_borders)
   size_t tstride = 0;
@@ -655,7 +657,14 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // exactly); the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0:
   // 720p yes, 1080p no)
   const size_t ml = c->pf_mask_lds;
-  if (ml)
+  constexpr int ppb = std::max(1, kPfThreads / 64 / kPfSplit);  // particles per block (one task per wave)
+  if (c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles) {
+    const int nblk = (c->cfg.particles + ppb - 1) / ppb;
+    for (int it = 0; it < c->cfg.iterations; it++)
+      k_score_pf_part<kPfThreads, kPfSplit><<<dim3(nblk, n), kPfThreads, 0, c->s>>>(
+          c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
+          c->cfg.iterations, it, ppb, nblk);
+  } else if (ml)
     k_score_pf<kPfThreads, kPfSplit, true><<<n, kPfThreads, ml, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
         c->cfg.iterations);
@@ -935,6 +944,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     c->trace_lds_frames = e ? atoi(e) : c->n_cu / 4;
     const char* e2 = getenv("MANTIS_FC_SMALL_FRAMES");
     c->fc_small_frames = e2 ? atoi(e2) : c->n_cu / 4;
+    const char* e3 = getenv("MANTIS_PF_SPLIT");
+    c->pf_split = !(e3 && e3[0] == '0');
   }
   {
     // LDS-staged mask for the particle filter: the tiled plane of a max-size

@@ -35,16 +35,38 @@
 
 namespace mk {
 
-__device__ inline int wave_sum(int v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+// Wave scans on DPP (no LDS crossbar trips): Hillis-Steele inside each
+// 16-lane row (row_shr 1, 2, 4, 8; lanes past the row's start read 0), then
+// the rows' totals carried by row_bcast:15 (row r-1's last lane into rows 1
+// and 3) and row_bcast:31 (lane 31 into rows 2 and 3). Every active lane must
+// call them (inactive lanes read as 0 only inside the row steps).
+#ifndef MK_DPP_SCAN
+#define MK_DPP_SCAN 1
+#endif
 __device__ inline int wave_incl_scan(int v, int lane) {
+#if MK_DPP_SCAN
+  (void)lane;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+#else
   for (int o = 1; o < 64; o <<= 1) {
     const int u = __shfl_up(v, o);
     if (lane >= o) v += u;
   }
+#endif
   return v;
+}
+__device__ inline int wave_sum(int v) {
+#if MK_DPP_SCAN
+  return __builtin_amdgcn_readlane(wave_incl_scan(v, 0), 63);
+#else
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+#endif
 }
 
 // Frame pointers come out of FrameDesc records in memory, so the compiler
@@ -87,10 +109,30 @@ __device__ inline int lds_find(const int* L, int x) {
   while ((p = L[x]) != x) x = p;
   return x;
 }
+#ifndef MK_HB_HALVE  // LDS union-finds (band CCLs) with path halving in their unions' finds
+#define MK_HB_HALVE 1
+#endif
+// the unions' finds halve the path as uf_find_c does (a non-root slot takes
+// its grandparent; roots change only through the CAS)
+__device__ inline int lds_find_halve(int* L, int x) {
+  while (true) {
+    const int p = L[x];
+    if (p == x) return x;
+    const int g = L[p];
+    if (g == p) return p;
+    L[x] = g;
+    x = g;
+  }
+}
 __device__ inline void lds_union(int* L, int a, int b) {
   while (true) {
+#if MK_HB_HALVE
+    a = lds_find_halve(L, a);
+    b = lds_find_halve(L, b);
+#else
     a = lds_find(L, a);
     b = lds_find(L, b);
+#endif
     if (a == b) return;
     if (a < b) { int t = a; a = b; b = t; }
     int old = atomicCAS(&L[a], a, b);
@@ -1015,9 +1057,6 @@ struct HystRuns {  // per-frame planes (frame f at + f * stride)
 #ifndef MK_HB_THREADS
 #define MK_HB_THREADS 512
 #endif
-#ifndef MK_HB_LISTAGG
-#define MK_HB_LISTAGG 0  // dense bands' list entries placed per block (one global atomic per list) instead of per wave
-#endif
 constexpr int HB_ROWS = MK_HB_ROWS, HB_CAP = 4096, HB_THREADS = MK_HB_THREADS, HB_WAVES = HB_THREADS / 64;
 // global id of row y's first run and the row's run count
 __device__ inline void hr_row(const int32_t* rb, int H, int bs, int y, int& g, int& cnt) {
@@ -1035,10 +1074,30 @@ __device__ inline int hb_find(const uint16_t* L, int x) {
   while ((p = L[x] & 0xfff) != x) x = p;
   return x;
 }
+// find with path halving (the unions' finds): a non-root slot takes its
+// grandparent, which is still an ancestor, so every find and link stays
+// valid; the 16-bit store leaves the other half of the dword alone, and a
+// concurrent link's CAS on that half sees the change and retries. Roots are
+// the same smallest ids, so the labels do not depend on the halving.
+__device__ inline int hb_find_halve(uint16_t* L, int x) {
+  while (true) {
+    const int p = L[x] & 0xfff;
+    if (p == x) return x;
+    const int g = L[p] & 0xfff;
+    if (g == p) return p;
+    L[x] = (uint16_t)g;
+    x = g;
+  }
+}
 __device__ inline void hb_union(uint16_t* L, int a, int b) {
   while (true) {
+#if MK_HB_HALVE
+    a = hb_find_halve(L, a);
+    b = hb_find_halve(L, b);
+#else
     a = hb_find(L, a);
     b = hb_find(L, b);
+#endif
     if (a == b) return;
     if (a < b) { const int tt = a; a = b; b = tt; }
     uint32_t* wp = (uint32_t*)(L + (a & ~1));
@@ -1075,8 +1134,8 @@ __device__ inline void hb_emit_runs(const uint32_t* cw, int WW, P* X16, int o, i
     const int is = wave_incl_scan(cs, lane), ie = wave_incl_scan(ce, lane);
     for (int os = bs + is - cs; S; S &= S - 1, os++) X16[2 * os] = (uint16_t)(32 * w + __ffs(S) - 1);
     for (int oe = be + ie - ce; E; E &= E - 1, oe++) X16[2 * oe + 1] = (uint16_t)(32 * w + __ffs(E) - 1);
-    bs += __shfl(is, 63);
-    be += __shfl(ie, 63);
+    bs += __builtin_amdgcn_readlane(is, 63);
+    be += __builtin_amdgcn_readlane(ie, 63);
   }
 }
 // One block per band: the band's candidate and strong words into LDS, its
@@ -1214,10 +1273,6 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   }
   __syncthreads();
   MK_HTICK(4);
-#if MK_HB_LISTAGG
-  __shared__ int32_t lcnt[HB_WAVES][2], lbase[2], ltot[2];
-  int nA = 0, nB = 0;  // this wave's list entries (wave-uniform)
-#endif
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
 #if MK_HB_LFLAGS
@@ -1239,57 +1294,11 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
         const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
         for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
       }
-#if MK_HB_LISTAGG
-      nB += __popcll(__ballot(fb == 2));
-      nA += __popcll(__ballot(root == j && fb == 3));
-#else
       hyst_push(lists, cnt + 1, g0 + j, fb == 2, true, top);
       hyst_push(lists, cnt, g0 + j, root == j && fb == 3, false, top);
-#endif
     }
   }
-#if MK_HB_LISTAGG
-  // list entries: the waves' counts, one global atomic per list and block,
-  // then each wave writes its entries from its own base (no atomic per wave)
-  if (lane == 0) {
-    lcnt[wave][0] = nA;
-    lcnt[wave][1] = nB;
-  }
   __syncthreads();
-  if (t < 2) {
-    int tot = 0;
-    for (int v = 0; v < HB_WAVES; v++) {
-      const int c = lcnt[v][t];
-      lcnt[v][t] = tot;
-      tot += c;
-    }
-    lbase[t] = tot ? atomicAdd(cnt + t, tot) : 0;
-    ltot[t] = tot;
-  }
-  __syncthreads();
-  if (ltot[0] | ltot[1]) {
-    int oA = lbase[0] + lcnt[wave][0], oB = lbase[1] + lcnt[wave][1];
-    const uint64_t below = (1ull << lane) - 1;
-    for (int q = wave; q < nr; q += HB_WAVES)
-      for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
-#if MK_HB_LFLAGS
-        const int root = Ll[j] & 0xfff;
-        const int fb = (Ll[root] >> 12) & 3;
-#else
-        const int root = Ll[j];
-        const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
-#endif
-        const bool pa = root == j && fb == 3, pb = fb == 2;
-        const uint64_t ma = __ballot(pa), mb = __ballot(pb);
-        if (pa) lists[oA + __popcll(ma & below)] = g0 + j;
-        if (pb) lists[top - 1 - (oB + __popcll(mb & below))] = g0 + j;
-        oA += __popcll(ma);
-        oB += __popcll(mb);
-      }
-  }
-#else
-  __syncthreads();
-#endif
   MK_HTICK(5);
   for (int i = t; i < nr * WW; i += HB_THREADS) eb[i] = Ew[i];
 }
@@ -1829,7 +1838,7 @@ __global__ __launch_bounds__(256) void k_run_emit(const uint32_t* __restrict__ d
         L[o] = o;
         o++;
       }
-      base += __shfl(inc, 63);
+      base += __builtin_amdgcn_readlane(inc, 63);
     }
   }
 }
@@ -3809,19 +3818,21 @@ __device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
   uint32_t w[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], m);
-  int rs = 0;
+  w[7] &= 0xffffu;  // bytes 28, 29: the stream's 30 bytes end there
+  // sum over the 30 bytes c of (c - t)^2, t = GREEN's channel of the byte
+  // (50, 255, 85 repeating): sum c^2 - 2 sum c t + 10 |GREEN|^2, both sums as
+  // v_dot4_u32_u8 chains over the realigned dwords (dword j starts at byte 4j,
+  // channel 4j mod 3 = j mod 3)
+  constexpr uint32_t T0 = 50u | 255u << 8 | 85u << 16 | 50u << 24;   // channels 0 1 2 0
+  constexpr uint32_t T1 = 255u | 85u << 8 | 50u << 16 | 255u << 24;  // 1 2 0 1
+  constexpr uint32_t T2 = 85u | 50u << 8 | 255u << 16 | 85u << 24;   // 2 0 1 2
+  uint32_t sq = 0, ct = 0;
 #pragma unroll
-  for (int k = 0; k < 10; k++) {
-    int c[3];
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-      const int o = 3 * k + ch;  // byte of the realigned stream
-      c[ch] = (int)((w[o >> 2] >> (8 * (o & 3))) & 0xffu);
-    }
-    const int e0 = c[0] - 50, e1 = c[1] - 255, e2 = c[2] - 85;
-    rs += e0 * e0 + e1 * e1 + e2 * e2;
+  for (int j = 0; j < 8; j++) {
+    sq = __builtin_amdgcn_udot4(w[j], w[j], sq, false);
+    ct = __builtin_amdgcn_udot4(w[j], j % 3 == 0 ? T0 : (j % 3 == 1 ? T1 : T2), ct, false);
   }
-  return rs;
+  return (int)sq - 2 * (int)ct + 10 * (50 * 50 + 255 * 255 + 85 * 85);
 }
 __device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
                                         const uint8_t* bgr, int W, int H, ColorLds* cl, double* err_out,
@@ -4160,7 +4171,7 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
       const int incl = wave_incl_scan(cu, lane);
       int base = 0;
       if (lane == 63) base = atomicAdd(q.n, incl);
-      base = __shfl(base, 63);
+      base = __builtin_amdgcn_readlane(base, 63);
       int idx = base + incl - cu;
 #pragma unroll
       for (int k = 0; k < U; k++) {
@@ -4176,13 +4187,9 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
       }
     }
   }
-  long long s64 = s;
-  for (int o = 32; o > 0; o >>= 1) {
-    s64 += __shfl_xor(s64, o);
-    n += __shfl_xor(n, o);
-  }
-  s_out = s64;
-  n_out = n;
+  // wave totals in int32 (<= 64 lanes x 12 landmarks x 3 * 255^2 < 2^31)
+  s_out = wave_sum(s);
+  n_out = wave_sum(n);
 }
 // The same trip split in two halves so a wave can keep one trip's pixel
 // loads in flight while it projects the next (software pipelining over a
@@ -4236,7 +4243,7 @@ __device__ inline void screen_issue(const PoseF& P, const float4* lmf, int lb, i
     const int incl = wave_incl_scan(cu, lane);
     int base = 0;
     if (lane == 63) base = atomicAdd(q.n, incl);
-    base = __shfl(base, 63);
+    base = __builtin_amdgcn_readlane(base, 63);
     int idx = base + incl - cu;
 #pragma unroll
     for (int k = 0; k < U; k++) {
@@ -4266,13 +4273,9 @@ __device__ inline void screen_finish(const ScrPend<U>& pd, long long& s_out, int
     n -= im;
     s += e & im;
   }
-  long long s64 = s;
-  for (int o = 32; o > 0; o >>= 1) {
-    s64 += __shfl_xor(s64, o);
-    n += __shfl_xor(n, o);
-  }
-  s_out = s64;
-  n_out = n;
+  // wave totals in int32 (<= 64 lanes x 12 landmarks x 3 * 255^2 < 2^31)
+  s_out = wave_sum(s);
+  n_out = wave_sum(n);
 }
 // A wave's tasks t = first, first + stride, ... < ntasks, each one trip,
 // pipelined: task t's pixel loads are in flight while task t + stride is
@@ -4360,10 +4363,15 @@ struct PoseLds {
   Quat q;
   double err;
 };
-// per-frame state handed from one scoring kernel to the next
+// per-frame state handed from one scoring kernel to the next; psum / pcnt /
+// ctr: the split particle filter's per-particle partial results and its
+// last-block counter (small batches, k_score_pf_part)
+constexpr int kPfMaxParticles = 96;
 struct ScoreState {
   PoseLds cur;
-  int32_t nsc, pad;
+  int32_t nsc, ctr;
+  long long psum[kPfMaxParticles];
+  int32_t pcnt[kPfMaxParticles];
 };
 
 // wave-uniform double into SGPRs (pose operands of the projection loop)
@@ -4528,7 +4536,19 @@ __global__ __launch_bounds__(NT) void k_score_init(
   if (tid == 0) {
     sst[f].cur = cur;
     sst[f].nsc = nsc;
+    sst[f].ctr = 0;
   }
+}
+
+// particle pose of the six gaussians g6 around the current pose
+__device__ inline void pf_particle(const Xf& cur_w2c, const float* g6, Xf& w2c, Xf& c2w) {
+  double yaw = (double)g6[0] * 0.03, pitch = (double)g6[1] * 0.03, roll = (double)g6[2] * 0.03;
+  double tz = (double)g6[3] * 0.01, ty = (double)g6[4] * 0.01, tx = (double)g6[5] * 0.01;
+  Xf rnd;
+  basis_from_rpy_small(roll, pitch, yaw, rnd.R);  // |angle| < 2 rad: float gaussian x 0.03
+  rnd.t[0] = tx; rnd.t[1] = ty; rnd.t[2] = tz;
+  w2c = xf_mul(cur_w2c, rnd);
+  c2w = xf_inverse(w2c);
 }
 
 // optimizeHypothesisWithParticleFilter (PoseAdjustment.h:13-60): particles are
@@ -4594,14 +4614,8 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   const MaskBits mglb{fm, bits::words(W), W};
   for (int it = 0; it < iterations; it++) {
     if (tid < particles) {
-      const float* g6 = gs + (size_t)(it * particles + tid) * 6;
-      double yaw = (double)g6[0] * 0.03, pitch = (double)g6[1] * 0.03, roll = (double)g6[2] * 0.03;
-      double tz = (double)g6[3] * 0.01, ty = (double)g6[4] * 0.01, tx = (double)g6[5] * 0.01;
-      Xf rnd;
-      basis_from_rpy_small(roll, pitch, yaw, rnd.R);  // |angle| < 2 rad: float gaussian x 0.03
-      rnd.t[0] = tx; rnd.t[1] = ty; rnd.t[2] = tz;
-      const Xf w2c = xf_mul(cur_w2c, rnd);
-      const Xf c2w = xf_inverse(w2c);
+      Xf w2c, c2w;
+      pf_particle(cur_w2c, gs + (size_t)(it * particles + tid) * 6, w2c, c2w);
       Pw[tid] = w2c;
       Pc[tid] = c2w;
       Pf[tid] = posef_from(c2w);
@@ -4687,7 +4701,7 @@ __global__ __launch_bounds__(NT) void k_score_pf(
           cur_c2w = Pc[bj];
           cur_w2c = Pw[bj];
         }
-        D.pf_iter_err[it + 1] = cur_err;
+        if (it + 1 < (int)(sizeof(D.pf_iter_err) / sizeof(double))) D.pf_iter_err[it + 1] = cur_err;  // the record holds 10 iterations
       }
     }
     __syncthreads();
@@ -4709,6 +4723,116 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     for (int k = 0; k < 3; k++) D.pf_c2w[9 + k] = cur_c2w.t[k];
     D.pf_err = cur_err;
     res[f].pf_error = cur_err;
+  }
+}
+
+// One iteration of the particle filter spread over `nblk` blocks per frame
+// (small batches, where one block per frame leaves the chip idle and the
+// iterations' chain is the latency): block b takes particles [b * ppb, (b+1)
+// * ppb), each a task per landmark slice (one per wave), over the global
+// mask plane; it writes its particles' integer sums and counts, and the
+// frame's last block to finish (counter in ScoreState) takes the argmin and
+// moves the current pose, as k_score_pf does at the end of an iteration.
+// Same sums, same first strict minimum, same poses (pf_particle recomputes
+// the winner's), so the results are identical to k_score_pf's.
+template <int NT, int SPLIT>
+__global__ __launch_bounds__(NT) void k_score_pf_part(
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
+    const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
+    FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations, int it, int ppb, int nblk) {
+  const int f = blockIdx.y, b = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (!st[f].reaches_pf) return;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  constexpr int kW = NT / 64, kPP = kW / SPLIT > 0 ? kW / SPLIT : 1;  // particles per block (one task per wave)
+  __shared__ float4 lmf[768];
+  __shared__ Xf Pc[kPP];
+  __shared__ PoseF Pf[kPP];
+  __shared__ unsigned long long Ps[kPP];
+  __shared__ int32_t Pn[kPP];
+  __shared__ uint32_t uqe[kPfQueue];
+  __shared__ int32_t uqn, last;
+  ScoreState& S = sst[f];
+  const int p0 = b * ppb, np = max(0, min(ppb, particles - p0));
+  const float* gs = gauss + st[f].gauss_offset + (size_t)it * particles * 6;
+  for (int i = tid; i < nl; i += NT) lmf[i] = lmk.xyzf[i];
+  if (tid < np) {
+    Xf w2c, c2w;
+    pf_particle(S.cur.w2c, gs + (size_t)(p0 + tid) * 6, w2c, c2w);
+    Pc[tid] = c2w;
+    Pf[tid] = posef_from(c2w);
+    Ps[tid] = 0;
+    Pn[tid] = 0;
+  }
+  if (tid == 0) uqn = 0;
+  __syncthreads();
+  const UQueue q{uqe, &uqn, kPfQueue};
+  const MaskBits mglb{mbits + (size_t)f * bstride, bits::words(W), W};
+  for (int task = __builtin_amdgcn_readfirstlane(wave); task < np * SPLIT; task += kW) {
+    const int j = task / SPLIT, h = task - j * SPLIT;
+    long long sum;
+    int cnt;
+    wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr, mglb, q, j,
+                                 &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+    if (lane == 0) {
+      atomicAdd(&Ps[j], (unsigned long long)sum);
+      atomicAdd(&Pn[j], cnt);
+    }
+  }
+  __syncthreads();
+  block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mglb, [&](int t) -> const Xf& { return Pc[t]; },
+              [&](int t, int e) {
+                atomicAdd(&Ps[t], (unsigned long long)e);
+                atomicAdd(&Pn[t], 1);
+              });
+  __syncthreads();
+  if (tid < np) {
+    S.psum[p0 + tid] = (long long)Ps[tid];
+    S.pcnt[p0 + tid] = Pn[tid];
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&S.ctr, 1) == nblk - 1;
+  __syncthreads();
+  if (!last || wave != 0) return;
+  // the frame's last block: argmin by (error, index), taken only when strictly
+  // below the current error
+  __threadfence();
+  const volatile long long* vs = S.psum;
+  const volatile int32_t* vc = S.pcnt;
+  double be = DBL_MAX;
+  int bj = 0x7fffffff;
+  for (int j = lane; j < particles; j += 64) {
+    const int cnt = vc[j];
+    const double e = cnt <= 0 ? DBL_MAX : (double)vs[j] / ((double)cnt * 1.1);
+    if (e < be || bj == 0x7fffffff) { be = e; bj = j; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double oe = __shfl_xor(be, o);
+    const int oj = __shfl_xor(bj, o);
+    if (oe < be || (oe == be && oj < bj)) { be = oe; bj = oj; }
+  }
+  if (lane == 0) {
+    FrameDebug& D = dbg[f];
+    if (bj < particles && be < S.cur.err) {
+      Xf w2c, c2w;
+      pf_particle(S.cur.w2c, gs + (size_t)bj * 6, w2c, c2w);
+      S.cur.c2w = c2w;
+      S.cur.w2c = w2c;
+      S.cur.err = be;
+    }
+    if (it + 1 < (int)(sizeof(D.pf_iter_err) / sizeof(double))) D.pf_iter_err[it + 1] = S.cur.err;
+    S.ctr = 0;
+    if (it == iterations - 1) {
+      S.cur.q = basis_to_quat(S.cur.w2c.R);
+      S.nsc += iterations * particles;
+      for (int k = 0; k < 9; k++) D.pf_c2w[k] = S.cur.c2w.R[k];
+      for (int k = 0; k < 3; k++) D.pf_c2w[9 + k] = S.cur.c2w.t[k];
+      D.pf_err = S.cur.err;
+      res[f].pf_error = S.cur.err;
+    }
   }
 }
 

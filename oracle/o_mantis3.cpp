@@ -453,7 +453,7 @@ int32_t orc_process_frame(orc_ctx* c, const uint8_t* bgr_in, int32_t w, int32_t 
       t.error = eval_hyp_fast(t, vc, cm, c->map);
       if (t.error < cur.error) cur = t;
     }
-    dbg->pf_iter_err[it + 1] = cur.error;
+    if (it + 1 < (int)(sizeof(dbg->pf_iter_err) / sizeof(double))) dbg->pf_iter_err[it + 1] = cur.error;  // the record holds 10 iterations
   }
   n_scored += 500;
   to12(cur.c2w, dbg->pf_c2w);
