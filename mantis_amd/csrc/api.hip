@@ -658,7 +658,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // 720p yes, 1080p no)
   const size_t ml = c->pf_mask_lds;
   constexpr int ppb = std::max(1, kPfThreads / 64 / kPfSplit);  // particles per block (one task per wave)
-  if (c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles) {
+  if (c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles) {  // MANTIS_PF_SPLIT
     const int nblk = (c->cfg.particles + ppb - 1) / ppb;
     for (int it = 0; it < c->cfg.iterations; it++)
       k_score_pf_part<kPfThreads, kPfSplit><<<dim3(nblk, n), kPfThreads, 0, c->s>>>(
@@ -673,8 +673,14 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
         c->cfg.iterations);
   mark(c, "score_pf_yaw/k_score_pf");
+  const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles;
+  if (split) {  // small batches: the 81 shifts over several blocks per frame first
+    constexpr int spb = kScoreTail / 128;
+    k_score_shift_part<kScoreTail><<<dim3((81 + spb - 1) / spb, n), kScoreTail, 0, c->s>>>(
+        c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_sst, c->cfg.grid_spacing, 9, spb);
+  }
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
-                                               c->d_sst, c->cfg.grid_spacing, 9);
+                                               c->d_sst, c->cfg.grid_spacing, 9, split);
   mark(c, "score_pf_yaw/k_score_final");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;

@@ -4836,11 +4836,90 @@ __global__ __launch_bounds__(NT) void k_score_pf_part(
   }
 }
 
+// computeAllShiftedHypothesesFAST's shift values (accumulated in double as the
+// reference loop does) and shifted pose j = (j / 9, j % 9) of the optimum
+__device__ inline void shift_values(int grid_size, double grid_spacing, double* shv) {
+  double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
+  int k = 0;
+  for (; x < ((double)grid_size / 2.0) * grid_spacing && k < 9; x += grid_spacing) shv[k++] = x;
+}
+__device__ inline void shift_pose(const Xf& w2c, const double* shv, int j, PoseLds& o) {
+  Xf nw = w2c;
+  nw.t[0] += shv[j / 9];
+  nw.t[1] += shv[j % 9];
+  nw.t[2] += 0.0;
+  Hyp h;
+  hyp_set_w2c(h, nw);
+  o.c2w = h.c2w; o.w2c = h.w2c; o.q = h.q;
+}
+
+// The 81 shifted hypotheses' screened sums spread over `nblk` blocks per frame
+// (small batches): block b takes shifts [b * spb, (b+1) * spb), one task per
+// (shift, landmark half), drains its own unsure landmarks, and writes each
+// shift's integer sum and count to ScoreState; k_score_final (pre = true)
+// takes them from there instead of scoring the shifts itself. Same sums.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_score_shift_part(
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
+    const FrameState* __restrict__ st, ScoreState* __restrict__ sst, double grid_spacing, int grid_size, int spb) {
+  const int f = blockIdx.y, b = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (!st[f].reaches_pf) return;
+  const FrameDesc fd = frames[f];
+  const int W = fd.w, H = fd.h;
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  constexpr int NS = 81, kMaxSpb = NT / 128 > 0 ? NT / 128 : 1;  // shifts per block: two tasks each, one per wave
+  __shared__ float4 lmf[768];
+  __shared__ PoseLds P[kMaxSpb];
+  __shared__ double shv[9];
+  __shared__ unsigned long long hs[kMaxSpb];
+  __shared__ int32_t hn[kMaxSpb];
+  __shared__ uint32_t uqe[kTailQueue];
+  __shared__ int32_t uqn;
+  const int j0 = b * spb, ns = max(0, min(min(spb, kMaxSpb), NS - j0));
+  for (int i = tid; i < nl; i += NT) lmf[i] = lmk.xyzf[i];
+  if (tid == 0) {
+    uqn = 0;
+    shift_values(grid_size, grid_spacing, shv);
+  }
+  __syncthreads();
+  if (tid < ns) {
+    shift_pose(sst[f].cur.w2c, shv, j0 + tid, P[tid]);
+    hs[tid] = 0;
+    hn[tid] = 0;
+  }
+  __syncthreads();
+  const UQueue q{uqe, &uqn, kTailQueue};
+  for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * ns; t += NT / 64) {
+    const int j = t >> 1, h = t & 1;
+    long long sum;
+    int n;
+    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, nl * h / 2, nl * (h + 1) / 2, fd.scam, W, H, fd.bgr, mask,
+                                 q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
+    if (lane == 0) {
+      atomicAdd(&hs[j], (unsigned long long)sum);
+      atomicAdd(&hn[j], n);
+    }
+  }
+  __syncthreads();
+  block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return P[t].c2w; },
+              [&](int t, int e) {
+                atomicAdd(&hs[t], (unsigned long long)e);
+                atomicAdd(&hn[t], 1);
+              });
+  __syncthreads();
+  if (tid < ns) {
+    sst[f].psum[j0 + tid] = (long long)hs[tid];
+    sst[f].pcnt[j0 + tid] = hn[tid];
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_score_final(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
-    const ScoreState* __restrict__ sst, double grid_spacing, int grid_size) {
+    const ScoreState* __restrict__ sst, double grid_spacing, int grid_size, bool pre) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (!st[f].reaches_pf) return;
@@ -4878,30 +4957,20 @@ __global__ __launch_bounds__(NT) void k_score_final(
     uqn = 0;
     cur = sst[f].cur;
     nsc = sst[f].nsc;
-    // shift values accumulate in double exactly as the reference loop does
-    double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
-    int k = 0;
-    for (; x < ((double)grid_size / 2.0) * grid_spacing && k < 9; x += grid_spacing) shv[k++] = x;
+    shift_values(grid_size, grid_spacing, shv);
   }
   __syncthreads();
   // computeAllShiftedHypothesesFAST: 81 shifted copies of the optimum
   const int NS = 81;
-  if (tid < NS) {
-    Xf nw = cur.w2c;
-    nw.t[0] += shv[tid / 9];
-    nw.t[1] += shv[tid % 9];
-    nw.t[2] += 0.0;
-    Hyp h;
-    hyp_set_w2c(h, nw);
-    P[tid].c2w = h.c2w; P[tid].w2c = h.w2c; P[tid].q = h.q;
-  }
+  if (tid < NS) shift_pose(cur.w2c, shv, tid, P[tid]);
   __syncthreads();
   const UQueue q{uqe, &uqn, kTailQueue};
   if (tid < NS) {
-    hs[tid] = 0;
-    hn[tid] = 0;
+    hs[tid] = pre ? (unsigned long long)sst[f].psum[tid] : 0ull;  // pre: k_score_shift_part's sums
+    hn[tid] = pre ? sst[f].pcnt[tid] : 0;
   }
   __syncthreads();
+  if (!pre) {
   // tasks = (shift, half of the landmarks): 162 one-trip tasks over the waves
   // instead of 81 two-trip ones (the last round of whole hypotheses kept one
   // wave busy); the halves' integer sums combine exactly
@@ -4944,6 +5013,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
                 atomicAdd(&hn[t], 1);
               });
   __syncthreads();
+  }
   if (tid < NS) {
     const int n = hn[tid];
     const double e = n <= 0 ? DBL_MAX : (double)(long long)hs[tid] / ((double)n * 1.1);
