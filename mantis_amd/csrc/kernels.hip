@@ -110,7 +110,7 @@ __device__ inline int lds_find(const int* L, int x) {
   return x;
 }
 #ifndef MK_HB_HALVE  // LDS union-finds (band CCLs) with path halving in their unions' finds
-#define MK_HB_HALVE 1
+#define MK_HB_HALVE 0  // measured slower: hysteresis 5.27 -> 5.65, components 3.59 -> 3.82 ms per 4096 frames
 #endif
 // the unions' finds halve the path as uf_find_c does (a non-root slot takes
 // its grandparent; roots change only through the CAS)
@@ -3806,14 +3806,10 @@ struct ColorLds {
 // inside the buffer with 36 bytes to spare): two 16-byte loads and one dword
 // of the 30 bytes from the dword-aligned start, realigned with v_alignbyte,
 // instead of ten unaligned pixel loads. Same pixels, same integer sum.
-__device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
-  const long b = 3 * lin0;
-  const uint32_t m = (uint32_t)(b & 3);
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(1), aligned(4))) const u32x4 gu4a;
-  const uint8_t* a = bgr + (b - m);
-  const u32x4 q0 = *(gu4a*)a, q1 = *(gu4a*)(a + 16);
-  const uint32_t d8 = *(gu32*)(a + 32);
+typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+// the row sum from its 36 loaded bytes (dword-aligned start, m = the row's
+// byte offset in the first dword)
+__device__ inline int color_row_words(cu32x4 q0, cu32x4 q1, uint32_t d8, uint32_t m) {
   const uint32_t d[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, d8};
   uint32_t w[8];
 #pragma unroll
@@ -3833,6 +3829,13 @@ __device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
     ct = __builtin_amdgcn_udot4(w[j], j % 3 == 0 ? T0 : (j % 3 == 1 ? T1 : T2), ct, false);
   }
   return (int)sq - 2 * (int)ct + 10 * (50 * 50 + 255 * 255 + 85 * 85);
+}
+__device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
+  const long b = 3 * lin0;
+  const uint32_t m = (uint32_t)(b & 3);
+  typedef __attribute__((address_space(1), aligned(4))) const cu32x4 gu4a;
+  const uint8_t* a = bgr + (b - m);
+  return color_row_words(*(gu4a*)a, *(gu4a*)(a + 16), *(gu32*)(a + 32), m);
 }
 __device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
                                         const uint8_t* bgr, int W, int H, ColorLds* cl, double* err_out,
@@ -3983,28 +3986,55 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
   const int ni = 10 * np;
   constexpr int kU = 4;
   for (int q0 = tid; q0 < ni; q0 += kU * NT) {
-    int rsum[kU], slot[kU];
+    int rsum[kU], slot[kU], row[kU];
+    long lin[kU];
+    uint32_t run = 0;  // bit k: item k takes the realigned-row path
 #pragma unroll
     for (int k = 0; k < kU; k++) {
       const int q = q0 + k * NT;
       slot[k] = -1;
       rsum[k] = 0;
+      row[k] = 0;
+      lin[k] = 0;
       if (q >= ni) continue;
       const int r = q / np, i = q - r * np;
       const int yf = cp->yf[i];
       if (!(yf & 1)) continue;
       slot[k] = i;
+      row[k] = r;
       const int x0 = cp->x0[i], y = (yf >> 3) + r;
-      const long lin0 = (long)y * W + x0;
-      if ((yf & 6) == 6 && lin0 >= 0 && lin0 + 12 <= npx) {
-        rsum[k] = color_row_run(bgr, lin0);
-      } else if ((yf & 6) == 6) {  // rows reaching past the buffer: pixel by pixel, out-of-buffer reads 0 (Q10)
+      lin[k] = (long)y * W + x0;
+      if ((yf & 6) == 6 && lin[k] >= 0 && lin[k] + 12 <= npx) run |= 1u << k;
+    }
+    // the row loads of all kU items issued together (an item off the common
+    // path loads the frame's first bytes and ignores them), then the sums
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1), aligned(4))) const u32x4 gu4a;
+    u32x4 q0v[kU], q1v[kU];
+    uint32_t d8[kU], mis[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const long bo = (run >> k) & 1u ? 3 * lin[k] : 0;
+      mis[k] = (uint32_t)(bo & 3);
+      const uint8_t* ap = bgr + (bo - mis[k]);
+      q0v[k] = *(gu4a*)ap;
+      q1v[k] = *(gu4a*)(ap + 16);
+      d8[k] = *(gu32*)(ap + 32);
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++)
+      if ((run >> k) & 1u) rsum[k] = color_row_words(q0v[k], q1v[k], d8[k], mis[k]);
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      if (slot[k] < 0 || ((run >> k) & 1u)) continue;
+      const int i = slot[k], yf = cp->yf[i];
+      if ((yf & 6) == 6) {  // rows reaching past the buffer: pixel by pixel, out-of-buffer reads 0 (Q10)
         int rs = 0;
         for (int ox = 0; ox < 10; ox++) {
-          const long lin = lin0 + ox;
+          const long l = lin[k] + ox;
           int b = 0, g = 0, rr = 0;
-          if (lin >= 0 && lin < npx) {
-            const uint32_t pv = load_bgr(bgr, lin, npx);
+          if (l >= 0 && l < npx) {
+            const uint32_t pv = load_bgr(bgr, l, npx);
             b = (int)(pv & 0xffu);
             g = (int)((pv >> 8) & 0xffu);
             rr = (int)((pv >> 16) & 0xffu);
@@ -4015,7 +4045,7 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
         rsum[k] = rs;
       } else {
         const int h = i / ngr;
-        rsum[k] = color_row_exact(pose_of(h), green + 3 * (i - h * ngr), cm, bgr, W, H, r);
+        rsum[k] = color_row_exact(pose_of(h), green + 3 * (i - h * ngr), cm, bgr, W, H, row[k]);
       }
     }
 #pragma unroll
