@@ -641,7 +641,9 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // drawing thread), so the copy overlaps the RPP kernels still queued on s;
   // s waits for it only before the scoring kernels. d_gauss / h_gauss are free:
   // the previous batch's call synchronised s, which had waited on this copy.
-  static const bool zc = getenv("MANTIS_GAUSS_COPY") == nullptr;  // A/B: the side-stream copy
+  // default: the side-stream copy (score stage 11.13 / 11.34 -> 10.95 / 10.97 ms per 4096
+  // frames in a 6-context A/B); MANTIS_GAUSS_ZEROCOPY=1: k_score_init reads the pinned buffer
+  static const bool zc = getenv("MANTIS_GAUSS_ZEROCOPY") != nullptr;
   if (!zc) {
     HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
     HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));

@@ -3957,9 +3957,13 @@ __device__ __attribute__((noinline)) int color_row_exact(const Xf& T, const doub
 }
 // COLOR errors of nh hypotheses (pose_of(h) = FP64 c2w) into err[h]; the whole
 // block calls it (nh * ngr <= kColorPairs)
+// MK_SCORE_TICKS == 3 (diagnostics): the ends of COLOR's projection and row
+// phases into ctk[1], ctk[2] (k_score_final's ticks, 10 ns from ctk0)
+#define MK_CTICK(k) \
+  if (ctk && threadIdx.x == 0) ctk[1 + (k)] = (int32_t)(wall_clock64() - ctk0);
 template <int NT, class PoseOf>
 __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const double* green, int ngr, const Cam& cm,
-                                         const uint8_t* bgr, int W, int H, ColorPairs* cp, double* err) {
+                                         const uint8_t* bgr, int W, int H, ColorPairs* cp, double* err, int32_t* ctk = nullptr, uint64_t ctk0 = 0) {
   const int tid = threadIdx.x;
   const int np = nh * ngr;
   const long npx = (long)W * H;
@@ -3981,60 +3985,34 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
     cp->acc[i] = 0;
   }
   __syncthreads();
+  MK_CTICK(0);
   // (pair, row) items, row-major over the pairs so a wave's lanes add into
   // different pairs; 4 items per thread per trip (their row loads in flight together)
   const int ni = 10 * np;
   constexpr int kU = 4;
   for (int q0 = tid; q0 < ni; q0 += kU * NT) {
-    int rsum[kU], slot[kU], row[kU];
-    long lin[kU];
-    uint32_t run = 0;  // bit k: item k takes the realigned-row path
+    int rsum[kU], slot[kU];
 #pragma unroll
     for (int k = 0; k < kU; k++) {
       const int q = q0 + k * NT;
       slot[k] = -1;
       rsum[k] = 0;
-      row[k] = 0;
-      lin[k] = 0;
       if (q >= ni) continue;
       const int r = q / np, i = q - r * np;
       const int yf = cp->yf[i];
       if (!(yf & 1)) continue;
       slot[k] = i;
-      row[k] = r;
       const int x0 = cp->x0[i], y = (yf >> 3) + r;
-      lin[k] = (long)y * W + x0;
-      if ((yf & 6) == 6 && lin[k] >= 0 && lin[k] + 12 <= npx) run |= 1u << k;
-    }
-    // the row loads of all kU items issued together (an item off the common
-    // path loads the frame's first bytes and ignores them), then the sums
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(1), aligned(4))) const u32x4 gu4a;
-    u32x4 q0v[kU], q1v[kU];
-    uint32_t d8[kU], mis[kU];
-#pragma unroll
-    for (int k = 0; k < kU; k++) {
-      const long bo = (run >> k) & 1u ? 3 * lin[k] : 0;
-      mis[k] = (uint32_t)(bo & 3);
-      const uint8_t* ap = bgr + (bo - mis[k]);
-      q0v[k] = *(gu4a*)ap;
-      q1v[k] = *(gu4a*)(ap + 16);
-      d8[k] = *(gu32*)(ap + 32);
-    }
-#pragma unroll
-    for (int k = 0; k < kU; k++)
-      if ((run >> k) & 1u) rsum[k] = color_row_words(q0v[k], q1v[k], d8[k], mis[k]);
-#pragma unroll
-    for (int k = 0; k < kU; k++) {
-      if (slot[k] < 0 || ((run >> k) & 1u)) continue;
-      const int i = slot[k], yf = cp->yf[i];
-      if ((yf & 6) == 6) {  // rows reaching past the buffer: pixel by pixel, out-of-buffer reads 0 (Q10)
+      const long lin0 = (long)y * W + x0;
+      if ((yf & 6) == 6 && lin0 >= 0 && lin0 + 12 <= npx) {
+        rsum[k] = color_row_run(bgr, lin0);
+      } else if ((yf & 6) == 6) {  // rows reaching past the buffer: pixel by pixel, out-of-buffer reads 0 (Q10)
         int rs = 0;
         for (int ox = 0; ox < 10; ox++) {
-          const long l = lin[k] + ox;
+          const long lin = lin0 + ox;
           int b = 0, g = 0, rr = 0;
-          if (l >= 0 && l < npx) {
-            const uint32_t pv = load_bgr(bgr, l, npx);
+          if (lin >= 0 && lin < npx) {
+            const uint32_t pv = load_bgr(bgr, lin, npx);
             b = (int)(pv & 0xffu);
             g = (int)((pv >> 8) & 0xffu);
             rr = (int)((pv >> 16) & 0xffu);
@@ -4045,7 +4023,7 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
         rsum[k] = rs;
       } else {
         const int h = i / ngr;
-        rsum[k] = color_row_exact(pose_of(h), green + 3 * (i - h * ngr), cm, bgr, W, H, row[k]);
+        rsum[k] = color_row_exact(pose_of(h), green + 3 * (i - h * ngr), cm, bgr, W, H, r);
       }
     }
 #pragma unroll
@@ -4053,6 +4031,7 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
       if (slot[k] >= 0) atomicAdd(&cp->acc[slot[k]], rsum[k]);
   }
   __syncthreads();
+  MK_CTICK(1);
   for (int h = tid; h < nh; h += NT) {
     double total = 0;
     int n = 0;
@@ -4978,7 +4957,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   const uint64_t tk0 = wall_clock64();
   int32_t* tk = const_cast<FrameState*>(st)[f].ticks;
 #define MK_STICK(k) \
-  if (tid == 0) tk[k] = (int32_t)(wall_clock64() - tk0);
+  if (tid == 0 && (MK_SCORE_TICKS != 3 || ((k) != 1 && (k) != 2))) tk[k] = (int32_t)(wall_clock64() - tk0);
 #else
 #define MK_STICK(k)
 #endif
@@ -5120,7 +5099,11 @@ __global__ __launch_bounds__(NT) void k_score_final(
 #endif
   if (!MK_COLOR_WAVE && 80 * lmk.ng <= kColorPairs) {
     block_score_color<NT>([&](int h) -> const Xf& { return P[h].c2w; }, 80, green, lmk.ng, fd.cam, fd.bgr, W, H,
-                          &cpairs, yset_err);
+                          &cpairs, yset_err
+#if defined(MK_SCORE_TICKS) && MK_SCORE_TICKS == 3
+                          , tk, tk0
+#endif
+                          );
   } else {
     ColorLds* cls = (ColorLds*)&cpairs;
     for (int j = wave; j < 80; j += (NT / 64)) {

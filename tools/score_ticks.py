@@ -5,7 +5,8 @@ Phases: shift tasks, unsure drain, top-20, yaw-set build, COLOR windows, publish
 With "pf" (a library built with -DMK_SCORE_TICKS=2): k_score_pf (the particle filter)'s
 phases summed over its iterations: mask staging, particle poses, screened
 tasks, unsure drain, per-particle sums, argmin.
-usage: MANTIS_AMD_LIB=abvar/ticks.so python tools/score_ticks.py [pf] [rigs]"""
+With "color" (-DMK_SCORE_TICKS=3): COLOR's projection, row and sum phases.
+usage: MANTIS_AMD_LIB=abvar/ticks.so python tools/score_ticks.py [pf | color] [rigs]"""
 import os
 import sys
 
@@ -15,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main(rigs, pf=False):
+def main(rigs, pf=False, color=False):
     import mantis_amd as M
     from mantis_amd import synth
 
@@ -47,6 +48,12 @@ def main(rigs, pf=False):
         if m.frame_debug(i).n_hyps > 0:
             tk.append(fc[10:16].astype(np.float64) * 0.01)  # 10 ns ticks -> us
     tk = np.array(tk)
+    if color:  # MK_SCORE_TICKS=3: slots 1, 2 hold COLOR's projection / row phase ends
+        for nm, a, b in (("COLOR project", 3, 1), ("COLOR rows", 1, 2), ("COLOR sums", 2, 4)):
+            d = tk[:, b] - tk[:, a]
+            print(f"{nm:14s} median {np.median(d):8.1f} us  p90 {np.percentile(d, 90):8.1f} us")
+        m.close()
+        return
     if pf:  # per-phase sums already
         d = tk
         tk = np.cumsum(tk, axis=1)
@@ -62,6 +69,6 @@ def main(rigs, pf=False):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    pf = bool(a) and a[0] == "pf"
-    a = a[1:] if pf else a
-    main(int(a[0]) if a else 256, pf)
+    mode = a[0] if a and a[0] in ("pf", "color") else ""
+    a = a[1:] if mode else a
+    main(int(a[0]) if a else 256, mode == "pf", mode == "color")
