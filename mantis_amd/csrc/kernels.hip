@@ -4116,10 +4116,11 @@ __device__ inline PoseF rfl(const PoseF& P) {
 // only when the queue is full). States: 0 out, 1 in frame (pixel in the
 // buffer), 2 unsure, 3 in frame past the end of the buffer (cvRound == rows:
 // reads as black).
-template <int U, class MK>
-__device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int lb, int le, const ScreenCam& sc, int W,
-                                        int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
-                                        const double* lmd, const Cam* cmp, long long& s_out, int& n_out) {
+// LM(k, l): landmark l (already clamped to [lb, le)) of slot k of the trip
+template <int U, class MK, class LM>
+__device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int lb, int le, const ScreenCam& sc, int W,
+                                          int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
+                                          const double* lmd, const Cam* cmp, long long& s_out, int& n_out) {
   const int lane = threadIdx.x & 63;
   const int last = W * H - 1;
   int s = 0, n = 0;  // per lane: <= 12 landmarks x 3 * 255^2, exact in int32
@@ -4128,7 +4129,7 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
 #pragma unroll
     for (int k = 0; k < U; k++) {
       const int l = b0 + lane + 64 * k;
-      const float4 L = lmf[l < le ? l : le - 1];
+      const float4 L = lm_at(k, l < le ? l : le - 1);
       int x, y;
       const int t = screen_project(P, L.x, L.y, L.z, L.w, sc, W, H, &x, &y);
       st[k] = l < le ? t : SCR_OUT;
@@ -4200,6 +4201,38 @@ __device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int l
   s_out = wave_sum(s);
   n_out = wave_sum(n);
 }
+template <int U, class MK>
+__device__ inline void wave_sums_screen(const PoseF& P, const float4* lmf, int lb, int le, const ScreenCam& sc, int W,
+                                        int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
+                                        const double* lmd, const Cam* cmp, long long& s_out, int& n_out) {
+  wave_sums_screen_t<U>(P, [&](int, int l) { return lmf[l]; }, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp,
+                        s_out, n_out);
+}
+// A wave whose tasks all cover the same landmark slice [lb, le) of at most
+// 64 U landmarks (the scorers' (hypothesis, half) tasks when the block's wave
+// count is even) keeps that slice in registers for all of them instead of
+// reading it from LDS on every trip: WaveLms::load once, then sums().
+template <int U>
+struct WaveLms {
+  float4 L[U];
+  int lb, le;
+  __device__ void load(const float4* lmf, int lb_, int le_) {
+    lb = lb_;
+    le = le_;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const int l = lb + lane + 64 * k;
+      L[k] = lmf[l < le ? l : le - 1];
+    }
+  }
+  template <class MK>
+  __device__ void sums(const PoseF& P, const ScreenCam& sc, int W, int H, const uint8_t* bgr, const MK& mask, UQueue q,
+                       int tag, const Xf* Tx, const double* lmd, const Cam* cmp, long long& s_out, int& n_out) const {
+    wave_sums_screen_t<U>(P, [&](int k, int) { return L[k]; }, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp, s_out,
+                          n_out);
+  }
+};
 // The same trip split in two halves so a wave can keep one trip's pixel
 // loads in flight while it projects the next (software pipelining over a
 // wave's tasks): screen_issue projects the trip's landmarks, queues the unsure
@@ -4621,6 +4654,14 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   const UQueue q{uqe, &uqn, kPfQueue};
   const MaskLds mlds{(lds_cu32*)pf_mask, bits::words(W)};
   const MaskBits mglb{fm, bits::words(W), W};
+  // a wave's tasks are (particle, slice wave % SPLIT): its slice of the
+  // landmarks stays in registers for every task and iteration
+  static_assert(kW % SPLIT == 0 && 64 * kScrUnroll * SPLIT >= 768, "one register trip per slice");
+  WaveLms<kScrUnroll> wl;
+  {
+    const int h = wave % SPLIT;
+    wl.load(lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT);
+  }
   for (int it = 0; it < iterations; it++) {
     if (tid < particles) {
       Xf w2c, c2w;
@@ -4657,15 +4698,11 @@ __global__ __launch_bounds__(NT) void k_score_pf(
                                     fd.bgr, mglb, q, lmk.xyz, &frames[f].cam, task, done);
 #else
     for (int task = __builtin_amdgcn_readfirstlane(wave); task < particles * SPLIT; task += kW) {
-      const int j = task / SPLIT, h = task - j * SPLIT;
+      const int j = task / SPLIT;
       long long sum;
       int cnt;
-      if (LM)
-        wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr,
-                                     mlds, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
-      else
-        wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr,
-                                     mglb, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+      if (LM) wl.sums(Pf[j], fd.scam, W, H, fd.bgr, mlds, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+      else wl.sums(Pf[j], fd.scam, W, H, fd.bgr, mglb, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
       if (lane == 0) {
         Ps[task] = (unsigned long long)sum;
         Pn[task] = cnt;
@@ -4779,12 +4816,17 @@ __global__ __launch_bounds__(NT) void k_score_pf_part(
   __syncthreads();
   const UQueue q{uqe, &uqn, kPfQueue};
   const MaskBits mglb{mbits + (size_t)f * bstride, bits::words(W), W};
+  static_assert(kW % SPLIT == 0 && 64 * kScrUnroll * SPLIT >= 768, "one register trip per slice");
+  WaveLms<kScrUnroll> wl;
+  {
+    const int h = wave % SPLIT;
+    wl.load(lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT);
+  }
   for (int task = __builtin_amdgcn_readfirstlane(wave); task < np * SPLIT; task += kW) {
-    const int j = task / SPLIT, h = task - j * SPLIT;
+    const int j = task / SPLIT;
     long long sum;
     int cnt;
-    wave_sums_screen<kScrUnroll>(Pf[j], lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT, fd.scam, W, H, fd.bgr, mglb, q, j,
-                                 &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+    wl.sums(Pf[j], fd.scam, W, H, fd.bgr, mglb, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
     if (lane == 0) {
       atomicAdd(&Ps[j], (unsigned long long)sum);
       atomicAdd(&Pn[j], cnt);
@@ -4900,12 +4942,14 @@ __global__ __launch_bounds__(NT) void k_score_shift_part(
   }
   __syncthreads();
   const UQueue q{uqe, &uqn, kTailQueue};
+  static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
+  WaveLms<kScrUnroll> wl;
+  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
   for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * ns; t += NT / 64) {
-    const int j = t >> 1, h = t & 1;
+    const int j = t >> 1;
     long long sum;
     int n;
-    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, nl * h / 2, nl * (h + 1) / 2, fd.scam, W, H, fd.bgr, mask,
-                                 q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
+    wl.sums(posef_from(P[j].c2w), fd.scam, W, H, fd.bgr, mask, q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
     if (lane == 0) {
       atomicAdd(&hs[j], (unsigned long long)sum);
       atomicAdd(&hn[j], n);
@@ -5002,12 +5046,14 @@ __global__ __launch_bounds__(NT) void k_score_final(
         }
       });
 #else
+  static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
+  WaveLms<kScrUnroll> wl;
+  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
   for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * NS; t += (NT / 64)) {
-    const int j = t >> 1, h = t & 1;
+    const int j = t >> 1;
     long long sum;
     int n;
-    wave_sums_screen<kScrUnroll>(posef_from(P[j].c2w), lmf, nl * h / 2, nl * (h + 1) / 2, fd.scam, W, H, fd.bgr, mask,
-                                 q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
+    wl.sums(posef_from(P[j].c2w), fd.scam, W, H, fd.bgr, mask, q, j, &P[j].c2w, lmk.xyz, &frames[f].cam, sum, n);
     if (lane == 0) {
       atomicAdd(&hs[j], (unsigned long long)sum);
       atomicAdd(&hn[j], n);
