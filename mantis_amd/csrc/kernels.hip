@@ -4505,14 +4505,24 @@ __global__ __launch_bounds__(NT) void k_score_init(
         }
       });
 #else
-  for (int h = __builtin_amdgcn_readfirstlane(wave); h < C; h += (NT / 64)) {
+  // tasks = (hypothesis, half of the landmarks), a wave's half in registers
+  // (as in the particle filter and the shifts); the halves' sums add exactly
+  for (int h = tid; h < C; h += NT) {
+    hs[h] = 0;
+    hn[h] = 0;
+  }
+  __syncthreads();
+  static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
+  WaveLms<kScrUnroll> wl;
+  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
+  for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * C; t += (NT / 64)) {
+    const int h = t >> 1;
     long long s;
     int n;
-    wave_sums_screen<kScrUnroll>(posef_from(Hh[h].c2w), lmf, 0, nl, fd.scam, W, H, fd.bgr, mask, q, h,
-                                 &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
+    wl.sums(posef_from(Hh[h].c2w), fd.scam, W, H, fd.bgr, mask, q, h, &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
     if (lane == 0) {
-      hs[h] = (unsigned long long)s;
-      hn[h] = n;
+      atomicAdd(&hs[h], (unsigned long long)s);
+      atomicAdd(&hn[h], n);
     }
   }
 #endif
