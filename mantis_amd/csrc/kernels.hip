@@ -1949,40 +1949,63 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
                                                     int cap) {
   const int f = blockIdx.y, lane = threadIdx.x & 63;
   const int ya = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN_RPW, yb = min(ya + RUN_RPW, Hp);
+  if (ya >= Hp) return;
   const int32_t* r = rowb + (size_t)f * rstride;
   const uint16_t* X = rx + (size_t)f * plane;
   int32_t* L = lab + (size_t)f * plane;
-  for (int y = ya; y < yb; y++) {
-  const int by = r[y], ny = r[y + 1] - by;
-  for (int j = lane; j < ny; j += 64) {
-    const int id = by + j;
+  // the wave's rows' run bases in one load (lane q: row ya + q, q <= rows);
+  // its runs are the contiguous ids [base of ya, base of yb), taken 64 at a
+  // time whatever their rows (no pass per row)
+  const int nrow = yb - ya;
+  const int rbq = lane <= nrow ? r[ya + lane] : 0x7fffffff;
+  const int g0 = __builtin_amdgcn_readlane(rbq, 0), g1 = __builtin_amdgcn_readlane(rbq, nrow);
+  const int nruns = r[Hp];
+  const uint64_t below = (1ull << lane) - 1;
+  for (int id = g0 + lane; __ballot(id < g1); id += 64) {
+    const bool live = id < g1;
+    // row of run id: the last row base <= id
+    int y = ya, by = g0;
+#pragma unroll
+    for (int k = 1; k < RUN_RPW; k++) {
+      const int bk = __builtin_amdgcn_readlane(rbq, k);
+      if (k < nrow && bk <= id) { y = ya + k; by = bk; }
+    }
+    const int j = id - by;
     // a root is a run whose label is itself: one load (a find would walk, and
     // path-halve, the chain of every non-root; halving never makes a non-root
     // point to itself, so the test is exact while other lanes compress).
     // Run 0 (ring) is the outside background.
-    if (id == 0 || L[id] != id) continue;
-    const int key = y * Wp + X[id];
+    const bool root = live && id != 0 && L[id] == id;
     Border b;
-    b.key = key;
-    if (j & 1) {
-      b.start = key; b.hole = 0; b.parent = key;
-    } else {
-      // hole: the run on its left is foreground; its component's root run
-      // starts at the key of the enclosing outer border
-      const int pr = uf_find_c(L, id - 1);
-      const int py = run_at_row(r, Hp, pr);
-      b.start = key - 1; b.hole = 1; b.parent = py * Wp + X[pr];
+    if (root) {
+      const int key = y * Wp + X[id];
+      b.key = key;
+      if (j & 1) {
+        b.start = key; b.hole = 0; b.parent = key;
+      } else {
+        // hole: the run on its left is foreground; its component's root run
+        // starts at the key of the enclosing outer border
+        const int pr = uf_find_c(L, id - 1);
+        const int py = run_at_row(r, Hp, pr);
+        b.start = key - 1; b.hole = 1; b.parent = py * Wp + X[pr];
+      }
     }
-    const int idx = atomicAdd(&st[f].n_borders, 1);
+    // one counter atomic per wave trip for all its roots
+    const uint64_t m = __ballot(root);
+    if (!m) continue;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&st[f].n_borders, __popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (!root) continue;
+    const int idx = base + __popcll(m & below);
     if (idx < cap) {
       borders[(size_t)f * cap + idx] = b;
       // border index of the root run, above the labels (k_seg_plan; it checks the fit)
-      const int nruns = r[Hp];
       if (2 * (size_t)nruns <= plane) L[nruns + id] = idx;
     } else {
       atomicOr(&st[f].overflow, 1);
     }
-  }
   }
 }
 
