@@ -41,7 +41,7 @@ __global__ __launch_bounds__(1024) void k_argmin(const double* __restrict__ err,
 }
 
 // Batched dense scoring (mantis_score_argmin_batch): one launch over every
-// frame's hypothesis block (blockIdx.y = frame, kApiHyps hypotheses per block,
+// frame's hypothesis block (blockIdx.y = frame, kDenseHyps hypotheses per block,
 // the screened fast scorer of k_score_api), then one argmin block per frame.
 struct DenseJob {
   const uint8_t* mask;  // W*H bytes or null
@@ -54,10 +54,13 @@ __global__ __launch_bounds__(64 * kApiHyps) void k_score_api_batch(const FrameDe
                                                                    double* __restrict__ err, int32_t* __restrict__ nproj) {
   const int f = blockIdx.y;
   const DenseJob J = jobs[f];
-  if ((int)blockIdx.x * kApiHyps >= J.n) return;
+  if ((int)blockIdx.x * kDenseHyps >= J.n) return;
   const FrameDesc fd = frames[f];
-  if (J.mask) score_api_fast(fd, &frames[f].cam, MaskBytes{J.mask}, lmk, J.c2w, J.n, err + J.err_off, nproj + J.err_off);
-  else score_api_fast(fd, &frames[f].cam, MaskNone{}, lmk, J.c2w, J.n, err + J.err_off, nproj + J.err_off);
+  if (J.mask)
+    score_api_fast<kDenseHyps>(fd, &frames[f].cam, MaskBytes{J.mask}, lmk, J.c2w, J.n, err + J.err_off,
+                               nproj + J.err_off);
+  else
+    score_api_fast<kDenseHyps>(fd, &frames[f].cam, MaskNone{}, lmk, J.c2w, J.n, err + J.err_off, nproj + J.err_off);
 }
 __global__ __launch_bounds__(1024) void k_argmin_batch(const DenseJob* __restrict__ jobs, const double* __restrict__ err,
                                                        double* __restrict__ out2) {
@@ -261,7 +264,7 @@ mantis_status mantis_score_argmin_batch(void* ctx, const mantis_image* imgs, int
   Landmarks L = lmk_of(c);
   mark(c, "start");
   if (maxn > 0)
-    k_score_api_batch<<<dim3((maxn + kApiHyps - 1) / kApiHyps, n_frames), 64 * kApiHyps, 0, c->s>>>(
+    k_score_api_batch<<<dim3((maxn + kDenseHyps - 1) / kDenseHyps, n_frames), 64 * kApiHyps, 0, c->s>>>(
         c->d_frames, d_jobs, L, c->d_dense_err, c->d_dense_np);
   mark(c, "score_dense");
   k_argmin_batch<<<n_frames, 1024, 0, c->s>>>(d_jobs, c->d_dense_err, c->d_pairs);

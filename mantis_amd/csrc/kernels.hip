@@ -5322,33 +5322,45 @@ __global__ __launch_bounds__(256) void k_rig_weight(const FrameDesc* __restrict_
 }
 
 // ================================================ standalone scoring API
-// Fast errors: kApiHyps hypotheses per block (one wave each, screened, one
-// drain per block); COLOR errors: one wave per hypothesis, exact FP64.
-constexpr int kApiHyps = 16, kApiQueue = 512;
-template <class MK>
+// Fast errors: HPB hypotheses per block of kApiHyps waves, tasks =
+// (hypothesis, half of the landmarks) with a wave's half in registers
+// (WaveLms), one drain per block: k_score_api (a call's few hundred
+// hypotheses, HPB = 16: many blocks) and the dense batch (thousands per
+// frame, HPB = 64: the landmark staging, barriers and drain shared by four
+// times as many). COLOR errors: one wave per hypothesis, exact FP64.
+constexpr int kApiHyps = 16, kApiQueue = 1024, kDenseHyps = 64;
+template <int HPB, class MK>
 __device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const MK& mask, Landmarks lmk,
                                       const double* c2w, int n, double* err, int32_t* nproj) {
+  constexpr int NW = kApiHyps;  // waves per block
+  static_assert(NW % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int h0 = blockIdx.x * kApiHyps, h = h0 + wave;
+  const int h0 = blockIdx.x * HPB, nh = min(HPB, n - h0);
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   __shared__ float4 lmf[768];
-  __shared__ unsigned long long hs[kApiHyps];
-  __shared__ int32_t hn[kApiHyps];
+  __shared__ unsigned long long hs[HPB];
+  __shared__ int32_t hn[HPB];
   __shared__ uint32_t uqe[kApiQueue];
   __shared__ int32_t uqn;
   for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
+  for (int i = tid; i < HPB; i += blockDim.x) {
+    hs[i] = 0;
+    hn[i] = 0;
+  }
   if (tid == 0) uqn = 0;
   __syncthreads();
   const UQueue q{uqe, &uqn, kApiQueue};
-  if (h < n) {
-    const Xf* T = (const Xf*)(c2w + 12 * (size_t)__builtin_amdgcn_readfirstlane(h));  // R[9], t[3] = mk::Xf
+  WaveLms<kScrUnroll> wl;
+  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
+  for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * nh; t += NW) {
+    const int j = t >> 1;
+    const Xf* T = (const Xf*)(c2w + 12 * (size_t)(h0 + j));  // R[9], t[3] = mk::Xf
     long long s;
     int c;
-    wave_sums_screen<kScrUnroll>(posef_from(*T), lmf, 0, nl, fd.scam, fd.w, fd.h, fd.bgr, mask, q, wave, T,
-                                 lmk.xyz, cmp, s, c);
+    wl.sums(posef_from(*T), fd.scam, fd.w, fd.h, fd.bgr, mask, q, j, T, lmk.xyz, cmp, s, c);
     if (lane == 0) {
-      hs[wave] = (unsigned long long)s;
-      hn[wave] = c;
+      atomicAdd(&hs[j], (unsigned long long)s);
+      atomicAdd(&hn[j], c);
     }
   }
   __syncthreads();
@@ -5359,10 +5371,10 @@ __device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const
                 atomicAdd(&hn[t], 1);
               });
   __syncthreads();
-  if (tid < kApiHyps && h0 + tid < n) {
-    const int c = hn[tid];
-    err[h0 + tid] = c <= 0 ? DBL_MAX : (double)(long long)hs[tid] / ((double)c * 1.1);
-    nproj[h0 + tid] = c;
+  for (int i = tid; i < nh; i += blockDim.x) {
+    const int c = hn[i];
+    err[h0 + i] = c <= 0 ? DBL_MAX : (double)(long long)hs[i] / ((double)c * 1.1);
+    nproj[h0 + i] = c;
   }
 }
 __global__ __launch_bounds__(64 * kApiHyps) void k_score_api(const FrameDesc* __restrict__ frames, const uint8_t* mask,
@@ -5371,8 +5383,8 @@ __global__ __launch_bounds__(64 * kApiHyps) void k_score_api(const FrameDesc* __
                                                              int32_t* __restrict__ nproj) {
   const FrameDesc fd = frames[0];
   if (fast) {
-    if (mask) score_api_fast(fd, &frames[0].cam, MaskBytes{mask}, lmk, c2w, n, err, nproj);
-    else score_api_fast(fd, &frames[0].cam, MaskNone{}, lmk, c2w, n, err, nproj);
+    if (mask) score_api_fast<kApiHyps>(fd, &frames[0].cam, MaskBytes{mask}, lmk, c2w, n, err, nproj);
+    else score_api_fast<kApiHyps>(fd, &frames[0].cam, MaskNone{}, lmk, c2w, n, err, nproj);
     return;
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
