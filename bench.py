@@ -235,15 +235,33 @@ def make_ctx(M, rk, **cfg):
 
 
 def lib_sha16():
-    """First 16 hex digits of the running product library's SHA-256: PMC
-    summaries record it, and the bench line uses a summary only when it
-    matches (a stale profile of another build is never mixed in)."""
+    """First 16 hex digits of the running product library's SHA-256 (hipcc
+    output is not bit-reproducible: a rebuild of the same sources differs)."""
     import hashlib
 
     try:
         return hashlib.sha256(open(os.path.join(ROOT, "mantis_amd", "libmantis_amd.so"), "rb").read()).hexdigest()[:16]
     except OSError:
         return None
+
+
+def src_sha16(root=None):
+    """First 16 hex digits of the SHA-256 over the library's sources (every
+    file under mantis_amd/csrc, include/*.h, the Makefile): the build identity
+    PMC summaries record. The bench line uses a summary only when it matches,
+    so a profile of other code is never mixed in, while a rebuild of the same
+    sources (hipcc's output differs byte-wise from build to build) keeps it."""
+    import glob
+    import hashlib
+
+    root = root or ROOT
+    files = sorted(glob.glob(os.path.join(root, "mantis_amd", "csrc", "*")) + glob.glob(os.path.join(root, "include", "*.h"))
+                   + [os.path.join(root, "Makefile")])
+    h = hashlib.sha256()
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.relpath(f, root).encode() + b"\0" + open(f, "rb").read() + b"\0")
+    return h.hexdigest()[:16]
 
 
 def cpu_model():
@@ -452,15 +470,16 @@ def run_config3(a, rk, cpu):
                      "hysteresis": ("k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
                      "morph": ("k_morph",)}
     digest = lib_sha16()
+    src_digest = src_sha16()
 
     def pmc_for(path):
-        """A committed PMC summary, only when it was collected on this very
-        library build (its lib_sha16 = the running libmantis_amd.so's)."""
+        """A committed PMC summary, only when it was collected on a library
+        built from these very sources (its src_sha16 = this tree's)."""
         try:
             pj = json.load(open(os.path.join(ROOT, path)))
         except (OSError, ValueError):
             return None
-        return pj if pj.get("lib_sha16") == digest else None
+        return pj if pj.get("src_sha16") == src_digest else None
 
     def roofline(stage, avg=avg, kavg=kavg):
         if stage not in avg or stage not in work:
@@ -616,6 +635,7 @@ def run_config3(a, rk, cpu):
                               "context's host thread incl. the cv::RNG gaussian draws); / ms_per_step = cores busy"),
             "host_cores_busy": round(host_cpu_s / el_local, 3),
             "lib_sha16": digest,
+            "src_sha16": src_digest,
             "host_ingest": ingest,
             "roofline": roof,
             "roofline_frontend": roof_front,

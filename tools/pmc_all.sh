@@ -6,8 +6,8 @@
 # L2 hits / misses, HBM reads (FETCH_SIZE) and writes (WRITE_SIZE) in passes of
 # their own. Per kernel: the launches with the largest grid (the batch
 # launches), counters averaged per launch, FETCH_SIZE / WRITE_SIZE in bytes.
-# Writes gpurun_out/pmc_$TAG.json with the library's lib_sha16 (bench.py uses
-# a summary only for the build it was collected on).
+# Writes gpurun_out/pmc_$TAG.json with the library's lib_sha16 and its sources'
+# src_sha16 (bench.py uses a summary only for the sources it was collected on).
 # usage: tools/pmc_all.sh TAG [bench args...]   (default: --contexts 1 --rigs 256)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; mkdir -p gpurun_out
@@ -90,8 +90,11 @@ fr = None
 m = re.search(r"--rigs\s+(\d+)", bargs)
 if m:
     fr = 4 * int(m.group(1))
-sha = hashlib.sha256(open(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "mantis_amd", "libmantis_amd.so"), "rb").read()).hexdigest()[:16]
-doc = {"lib_sha16": sha, "bench_args": bargs, "frames_per_launch": fr,
+root = os.environ.get("GRAFT_REPO_ROOT", ".")
+sha = hashlib.sha256(open(os.path.join(root, "mantis_amd", "libmantis_amd.so"), "rb").read()).hexdigest()[:16]
+sys.path.insert(0, root)
+from bench import src_sha16
+doc = {"lib_sha16": sha, "src_sha16": src_sha16(root), "bench_args": bargs, "frames_per_launch": fr,
        "note": "per kernel: batch launches (largest grid), counters averaged per launch; FETCH_SIZE_bytes as "
                "reported (gfx950: 1/2 of the bytes of 16-B coalesced reads, MI355X_MICROARCH.md), WRITE_SIZE_bytes "
                "as reported; valu_issue_frac = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x duration)",
