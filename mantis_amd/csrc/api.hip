@@ -149,6 +149,7 @@ struct Ctx {
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
+  int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
   bool pf_split = true;    // small batches: each particle-filter iteration over several blocks per frame
                            // (k_score_pf_part); MANTIS_PF_SPLIT=0 keeps one block per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
@@ -414,8 +415,11 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     mark(c, "canny_nms/k_canny");
   }
   // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
+  // mark values 4..255 (the denser bands' flags are <= 3); the flag plane is cleared when they wrap
+  c->hyst_epoch = c->hyst_epoch >= 255 ? 4 : c->hyst_epoch + 1;
+  if (c->hyst_epoch == 4) HIP_OK(hipMemsetAsync(c->d_strong, 0, c->fstride * (size_t)c->F, c->s));
   HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
-              HB_ROWS * ((W + 1) / 2), c->d_st};
+              HB_ROWS * ((W + 1) / 2), c->d_st, c->hyst_epoch};
   // list counters |A|, |B| of every frame (rowb[H + 1], rowb[H + 2])
   HIP_OK(hipMemset2DAsync(c->d_rowb + H + 1, c->rstride * sizeof(int32_t), 0, 2 * sizeof(int32_t), n, c->s));
   const int WWb = bits::words(W);
@@ -903,6 +907,10 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   }
   if (cfg.max_width > 8190) {
     g_create_err = "max_width: at most 8190 (the hysteresis bands hold a row's worst-case runs in LDS)";
+    return MANTIS_ERR_ARG;
+  }
+  if ((int64_t)((cfg.max_height + HB_ROWS - 1) / HB_ROWS) * HB_ROWS * ((cfg.max_width + 1) / 2) >= (1 << 24)) {
+    g_create_err = "max_width x max_height: at most 2^25 pixels (hysteresis run ids and their band row share a word)";
     return MANTIS_ERR_ARG;
   }
   if (cfg.max_quads != kMaxQuads) {

@@ -1033,13 +1033,16 @@ __device__ inline bool run_strong(const uint32_t* srow, int a, int b) {
 struct HystRuns {  // per-frame planes (frame f at + f * stride)
   uint32_t* x;     // run extents: start | end << 16 (seam rows, list B runs; every run of a dense band)
   int32_t* lab;    // run labels
-  uint8_t* flag;   // per root: bit 2 = the global component holds a strong pixel (denser bands: bits 0 / 1
-                   // = strong / reaches a seam, per band root)
+  uint8_t* flag;   // per root: == epoch: the global component holds a strong pixel (denser bands: bits 0 / 1
+                   // = strong / reaches a seam, per band root, values <= 3)
   int32_t* rowb;   // per row: its first run's index inside the band; [H + 1], [H + 2] = |A|, |B|;
                    // [H + 3 + b] = runs of band b
   size_t x_stride, lab_stride, flag_stride, rstride, half;
   int bs;          // run ids per band: run i of band b is b * bs + i (bs = band rows x ceil(W / 2))
   FrameState* st;  // diagnostics only (MK_HYST_TICKS: phase ends of one band per frame into st[f].ticks)
+  int epoch;       // this call's mark value, 4..255: a root is marked when its flag byte equals it, so the
+                   // band kernel never clears the flags of its roots (a scattered byte per root); the host
+                   // clears the plane when the value wraps
 };
 
 // Per band of HB_ROWS rows: unions in LDS (labels = band roots, written to
@@ -1235,7 +1238,7 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
           const int a = X[j] & 0xffff, b = X[j] >> 16;
           for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
         }
-        hyst_push(lists, cnt + 1, j, fb == 2, true, top);
+        hyst_push(lists, cnt + 1, j | (q << 24), fb == 2, true, top);  // list B: run id | its band row << 24
         hyst_push(lists, cnt, j, root == j && fb == 3, false, top);
       }
     __syncthreads();
@@ -1283,18 +1286,19 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
       const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
 #endif
       // global labels / extents only where a later kernel looks: the band's
-      // first and last rows (seam unions), list B runs (fb == 2: k_hyst_fix)
-      // and band roots (finds end there; their flag byte is what k_hyst_mark /
-      // k_hyst_fix use)
-      const bool seam_row = q == 0 || q == nr - 1;
-      if (seam_row || fb == 2 || root == j) L[g0 + j] = g0 + root;
+      // seam rows (its first / last row where another band lies beyond:
+      // k_hyst_seam's unions), list B runs (fb == 2: k_hyst_fix) and the roots
+      // of components that reach a seam (finds end there; their flag byte is
+      // what k_hyst_mark / k_hyst_fix use) -- no later kernel finds its way to
+      // the other roots
+      const bool seam_row = edge_row(q);
+      if (seam_row || fb == 2 || (root == j && (fb & 2))) L[g0 + j] = g0 + root;
       if (seam_row || fb == 2) X[g0 + j] = Xl[j];
-      if (root == j) fl[g0 + j] = 0;
       if (fb & 1) {
         const int a = Xl[j] & 0xffff, b = Xl[j] >> 16;
         for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&Ew[q * WW + w], span_mask(w, a, b));
       }
-      hyst_push(lists, cnt + 1, g0 + j, fb == 2, true, top);
+      hyst_push(lists, cnt + 1, (g0 + j) | (q << 24), fb == 2, true, top);
       hyst_push(lists, cnt, g0 + j, root == j && fb == 3, false, top);
     }
   }
@@ -1326,7 +1330,7 @@ __global__ __launch_bounds__(256) void k_hyst_mark(HystRuns hr, int H) {
   uint8_t* fl = hr.flag + (size_t)f * hr.flag_stride;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int root = uf_find_c(L, A[i]);
-    if (!(fl[root] & 4)) atomicOr((uint32_t*)(fl + (root & ~3)), 4u << (8 * (root & 3)));
+    if (fl[root] != (uint8_t)hr.epoch) fl[root] = (uint8_t)hr.epoch;  // byte stores of one value: races are benign
   }
 }
 
@@ -1342,17 +1346,11 @@ __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restr
   const uint32_t* X = hr.x + (size_t)f * hr.x_stride;
   const int WW = bits::words(W);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const int j = Bl[-i];
-    if (!(fl[uf_find_c(L, j)] & 4)) continue;
-    const int band = j / hr.bs, l = j - band * hr.bs;
-    int lo = band * HB_ROWS, hi = min(H, lo + HB_ROWS) - 1;  // row of run j: largest y of the band with rb[y] <= l
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (rb[mid] <= l) lo = mid;
-      else hi = mid - 1;
-    }
+    const int e = Bl[-i], j = e & 0xffffff;  // run id | band row << 24 (ids < 2^24: bands x bs)
+    if (fl[uf_find_c(L, j)] != (uint8_t)hr.epoch) continue;
+    const int y = (j / hr.bs) * HB_ROWS + (e >> 24);
     const int a = X[j] & 0xffff, b = X[j] >> 16;
-    uint32_t* eb = ebits + (size_t)f * bstride + (size_t)lo * WW;
+    uint32_t* eb = ebits + (size_t)f * bstride + (size_t)y * WW;
     for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&eb[w], span_mask(w, a, b));
   }
 }

@@ -115,3 +115,17 @@ def test_create_without_gpu_fails_loudly():
     assert msg and b"GPU" in msg
     with pytest.raises(M.MantisError):
         M.Mantis()
+
+
+def test_create_rejects_oversized_frames():
+    """Hysteresis run ids and their band row share a list word: configs past
+    2^25 pixels are refused at creation (before any device call, so this runs
+    without a GPU too)."""
+    import mantis_amd as M
+
+    cfg = M.default_config()
+    cfg.max_width, cfg.max_height = 8190, 4200
+    h = C.c_void_p()
+    st = M.lib().mantis_create(C.byref(cfg), C.byref(h))
+    assert st == 1 and not h.value  # MANTIS_ERR_ARG
+    assert b"2^25" in M.lib().mantis_last_error(None)
