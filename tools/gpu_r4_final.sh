@@ -3,11 +3,19 @@
 # the CPU baseline), one-context kernel trace; PART=b: rocprofv3 kernel trace +
 # stats of the default command, batch-launch averages, and the config 2 / 5 / 4
 # legs; PART=d: every kernel's PMC summary (tools/pmc_all.sh, digest-tagged:
-# bench.py reads traffic / VALU issue from it for this build only).
+# bench.py reads traffic / VALU issue from it for these sources only); PART=da:
+# d, then a with that summary in place.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; O=gpurun_out/r04_final; mkdir -p $O
 export TMPDIR=/tmp
-if [ "$PART" = "a" ]; then
+if [ "$PART" = "d" ] || [ "$PART" = "da" ]; then
+  bash tools/pmc_all.sh r04 > $O/pmc.log 2>&1 || { echo pmc failed; tail -20 $O/pmc.log; exit 1; }
+  cp gpurun_out/pmc_r04.json $O/pmc_r04.json
+  tail -3 $O/pmc.log
+  # the bench line below reads this summary (same sources) for traffic / VALU issue
+  [ "$PART" = "da" ] && cp gpurun_out/pmc_r04.json profiles/r04_pmc.json
+fi
+if [ "$PART" = "a" ] || [ "$PART" = "da" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1; tail -2 $O/gpu_tests.txt
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && tail -1 $O/smoke.txt || { echo smoke failed; tail -5 $O/smoke.txt; exit 1; }
   timeout -k 10 700 python -u bench.py > $O/bench_default.log 2>&1 || { echo bench failed; tail -5 $O/bench_default.log; exit 1; }
@@ -29,15 +37,10 @@ if [ "$PART" = "b" ]; then
     grep '^{' $O/bench_c$leg.log | tail -1 > $O/bench_c$leg.json; cut -c1-160 $O/bench_c$leg.json
   done
 fi
-if [ "$PART" = "a" ] || [ "$PART" = "c" ]; then
+if [ "$PART" = "a" ] || [ "$PART" = "da" ] || [ "$PART" = "c" ]; then
   # one context: the kernels' own durations without the other contexts' blocks
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$R/$O/prof_c1" -o run -- python3 "$R/bench.py" --no-cpu --contexts 1 --steps 3 --warmup 1 --latency-iters 3 --ingest-steps 0 > "$R/$O/prof_c1.log" 2>&1) || { echo prof c1 failed; tail -5 $O/prof_c1.log; exit 1; }
   python3 tools/prof_summary.py $O/prof_c1 $O/rocprof_stats_c1.md > /dev/null
   python3 tools/kern_avg.py $O/prof_c1/run_kernel_trace.csv 40 $O/batch_launch_avg_c1.json > $O/batch_launch_avg_c1.txt
   head -30 $O/batch_launch_avg_c1.txt
-fi
-if [ "$PART" = "d" ]; then
-  bash tools/pmc_all.sh r04 > $O/pmc.log 2>&1 || { echo pmc failed; tail -20 $O/pmc.log; exit 1; }
-  cp gpurun_out/pmc_r04.json $O/pmc_r04.json
-  tail -3 $O/pmc.log
 fi
