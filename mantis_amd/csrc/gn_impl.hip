@@ -50,7 +50,8 @@ __global__ __launch_bounds__(256) void k_gn_accum(const double* __restrict__ Twb
 // to cell-centre correspondence per quad (gn_quad_obs, mk_gn.h). The list is
 // compacted in item order (block scan), so the MFMA sums are reproducible.
 
-// The rig GN runs as: k_rig_gn_obs (correspondences, once, with the fused
+// The rig GN runs as (camera-sharded; one GPU: the same block functions in
+// one launch, k_rig_gn_fused): k_rig_gn_obs (correspondences, once, with the fused
 // pose) then, per iteration, k_rig_gn_acc (one block per rig builds M^T M with
 // MFMA into a kGnSlot accumulator slot) -> [ncclAllReduce of every rig's slot
 // when the rig's cameras are sharded over ranks] -> k_rig_gn_step (one lane
@@ -63,18 +64,15 @@ __global__ __launch_bounds__(256) void k_gn_accum(const double* __restrict__ Twb
 
 // one rig, one block of 256: the accepted correspondences of this rank's
 // cameras in item order (camera, quad), compacted by a block scan
-__global__ __launch_bounds__(256) void k_rig_gn_obs(const FrameDesc* __restrict__ frames,
-                                                    const FrameState* __restrict__ st,
-                                                    const QuadRec* __restrict__ quads,
-                                                    const GnCam* __restrict__ gncam, RigGnIO* io, int cams_local,
-                                                    double* __restrict__ obs_all, int obs_cap, double half,
-                                                    double spacing) {
+// (R: the rig's state, in global memory or a block's LDS copy)
+__device__ inline void gn_obs_block(const FrameDesc* __restrict__ frames, const FrameState* __restrict__ st,
+                                    const QuadRec* __restrict__ quads, const GnCam* __restrict__ gncam, RigGnIO& R,
+                                    int rig, int cams_local, double* obs_all, int obs_cap, double half,
+                                    double spacing) {
   __shared__ double T[16];
   __shared__ int32_t scan[256];
   __shared__ int32_t nobs_s;
-  const int rig = blockIdx.x, t = threadIdx.x;
-  RigGnIO& R = io[rig];
-  if (!R.valid) return;
+  const int t = threadIdx.x;
   if (t < 16) T[t] = R.Twb[t];
   __syncthreads();
   const GnCam* cams = gncam + (size_t)rig * cams_local;
@@ -129,22 +127,26 @@ __global__ __launch_bounds__(256) void k_rig_gn_obs(const FrameDesc* __restrict_
     R.cost0 = R.cost = 0;
   }
 }
+__global__ __launch_bounds__(256) void k_rig_gn_obs(const FrameDesc* __restrict__ frames,
+                                                    const FrameState* __restrict__ st,
+                                                    const QuadRec* __restrict__ quads,
+                                                    const GnCam* __restrict__ gncam, RigGnIO* io, int cams_local,
+                                                    double* __restrict__ obs_all, int obs_cap, double half,
+                                                    double spacing) {
+  RigGnIO& R = io[blockIdx.x];
+  if (!R.valid) return;
+  gn_obs_block(frames, st, quads, gncam, R, blockIdx.x, cams_local, obs_all, obs_cap, half, spacing);
+}
 
 // one rig, one block of 256: M^T M of M = [J | r] over this rank's
 // correspondences about the current pose (4 waves, v_mfma_f64_16x16x4f64, 4
 // residual rows per instruction), summed over the waves in a fixed order
-__global__ __launch_bounds__(256) void k_rig_gn_acc(const GnCam* __restrict__ gncam, const RigGnIO* __restrict__ io,
-                                                    int cams_local, const double* __restrict__ obs_all, int obs_cap,
-                                                    double* __restrict__ acc_all) {
+// (out: the rig's kGnSlot accumulator slot, global or LDS)
+__device__ inline void gn_acc_block(const GnCam* __restrict__ gncam, const RigGnIO& R, int rig, int cams_local,
+                                    const double* obs_all, int obs_cap, double* out) {
   __shared__ double red[4][16][16];
-  const int rig = blockIdx.x, t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const RigGnIO& R = io[rig];
-  double* out = acc_all + (size_t)rig * kGnSlot;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n_obs = R.n_obs_local;
-  if (!R.valid || R.done) {
-    if (t < kGnSlot) out[t] = 0.0;
-    return;
-  }
   const GnCam* cams = gncam + (size_t)rig * cams_local;
   const double* obs = obs_all + (size_t)rig * obs_cap * 6;
   double Rt[9], tw[3];
@@ -179,15 +181,22 @@ __global__ __launch_bounds__(256) void k_rig_gn_acc(const GnCam* __restrict__ gn
     out[t] = v;
   }
 }
+__global__ __launch_bounds__(256) void k_rig_gn_acc(const GnCam* __restrict__ gncam, const RigGnIO* __restrict__ io,
+                                                    int cams_local, const double* __restrict__ obs_all, int obs_cap,
+                                                    double* __restrict__ acc_all) {
+  const int rig = blockIdx.x;
+  const RigGnIO& R = io[rig];
+  double* out = acc_all + (size_t)rig * kGnSlot;
+  if (!R.valid || R.done) {
+    if (threadIdx.x < kGnSlot) out[threadIdx.x] = 0.0;
+    return;
+  }
+  gn_acc_block(gncam, R, rig, cams_local, obs_all, obs_cap, out);
+}
 
 // one lane per rig: the summed system -> Cholesky solve -> T_w_b Exp(delta)
-__global__ __launch_bounds__(64) void k_rig_gn_step(RigGnIO* io, const double* __restrict__ acc_all, int n_rigs,
-                                                    int it) {
-  const int rig = blockIdx.x * 64 + threadIdx.x;
-  if (rig >= n_rigs) return;
-  RigGnIO& R = io[rig];
+__device__ inline void gn_step_one(RigGnIO& R, const double* acc, int it) {
   if (!R.valid || R.done) return;
-  const double* acc = acc_all + (size_t)rig * kGnSlot;
   if (it == 0) {
     R.n_obs = (int)acc[28];
     if (R.n_obs < 6) {  // too few correspondences over the rig: keep the fused pose
@@ -208,6 +217,41 @@ __global__ __launch_bounds__(64) void k_rig_gn_step(RigGnIO* io, const double* _
     if (dn < 1e-24) R.done = 1;
   }
   R.iterations = it + 1;
+}
+__global__ __launch_bounds__(64) void k_rig_gn_step(RigGnIO* io, const double* __restrict__ acc_all, int n_rigs,
+                                                    int it) {
+  const int rig = blockIdx.x * 64 + threadIdx.x;
+  if (rig >= n_rigs) return;
+  gn_step_one(io[rig], acc_all + (size_t)rig * kGnSlot, it);
+}
+
+// Single-GPU rig GN in one launch: one block per rig runs the correspondence
+// pass and every iteration (accumulators -> solve -> update) on an LDS copy of
+// the rig's state, stopping when the rig converges. The same block functions
+// as the three-kernel sequence above (which the camera-sharded path keeps for
+// its per-iteration all-reduce), so the results are bit-identical; what goes
+// is 2 launches per iteration (the single-rig latency path's GN stage).
+__global__ __launch_bounds__(256) void k_rig_gn_fused(const FrameDesc* __restrict__ frames,
+                                                      const FrameState* __restrict__ st,
+                                                      const QuadRec* __restrict__ quads,
+                                                      const GnCam* __restrict__ gncam, RigGnIO* io, int cams_local,
+                                                      double* obs_all, int obs_cap, double half, double spacing,
+                                                      int iters) {
+  __shared__ RigGnIO S;
+  __shared__ double acc[kGnSlot];
+  const int rig = blockIdx.x, t = threadIdx.x;
+  if (t == 0) S = io[rig];
+  __syncthreads();
+  if (!S.valid) return;
+  gn_obs_block(frames, st, quads, gncam, S, rig, cams_local, obs_all, obs_cap, half, spacing);
+  __syncthreads();
+  for (int it = 0; it < iters && !S.done; it++) {
+    gn_acc_block(gncam, S, rig, cams_local, obs_all, obs_cap, acc);
+    __syncthreads();
+    if (t == 0) gn_step_one(S, acc, it);
+    __syncthreads();
+  }
+  if (t == 0) io[rig] = S;
 }
 
 }  // namespace mk
@@ -261,16 +305,25 @@ mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, 
   HIP_OK(hipMemcpyAsync(c->d_rigio, io.data(), sizeof(RigGnIO) * n_rigs, hipMemcpyHostToDevice, c->s));
   const double spacing = c->cfg.grid_spacing, half = 4.5 * spacing;  // lines at -1.44 + 0.32 k, k = 0..9
   mark(c, "start");
-  k_rig_gn_obs<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cams_local,
-                                          c->d_gnobs, obs_cap, half, spacing);
-  for (int it = 0; it < c->cfg.gn_iterations; it++) {
-    k_rig_gn_acc<<<n_rigs, 256, 0, c->s>>>(c->d_gncam, c->d_rigio, cams_local, c->d_gnobs, obs_cap, c->d_gnacc);
-    if (use_comm) {
-      ncclResult_t r = ncclAllReduce(c->d_gnacc, c->d_gnacc, (size_t)n_rigs * kGnSlot, ncclFloat64, ncclSum,
-                                     (ncclComm_t)c->comm, c->s);
-      if (r != ncclSuccess) { c->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+  // small batches (latency): one launch, rig_gn 0.21 -> 0.17 ms at one rig per
+  // call; large ones keep the three kernels (1024 rigs: 0.62 vs 0.89 ms fused).
+  // MANTIS_GN_SEPARATE: the three-kernel sequence always (A/B)
+  static const bool separate = getenv("MANTIS_GN_SEPARATE") != nullptr;
+  if (!use_comm && !separate && n <= c->fc_small_frames) {
+    k_rig_gn_fused<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cams_local,
+                                              c->d_gnobs, obs_cap, half, spacing, c->cfg.gn_iterations);
+  } else {
+    k_rig_gn_obs<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cams_local,
+                                            c->d_gnobs, obs_cap, half, spacing);
+    for (int it = 0; it < c->cfg.gn_iterations; it++) {
+      k_rig_gn_acc<<<n_rigs, 256, 0, c->s>>>(c->d_gncam, c->d_rigio, cams_local, c->d_gnobs, obs_cap, c->d_gnacc);
+      if (use_comm) {
+        ncclResult_t r = ncclAllReduce(c->d_gnacc, c->d_gnacc, (size_t)n_rigs * kGnSlot, ncclFloat64, ncclSum,
+                                       (ncclComm_t)c->comm, c->s);
+        if (r != ncclSuccess) { c->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r); return MANTIS_ERR_COMM; }
+      }
+      k_rig_gn_step<<<(n_rigs + 63) / 64, 64, 0, c->s>>>(c->d_rigio, c->d_gnacc, n_rigs, it);
     }
-    k_rig_gn_step<<<(n_rigs + 63) / 64, 64, 0, c->s>>>(c->d_rigio, c->d_gnacc, n_rigs, it);
   }
   mark(c, "rig_gn");
   HIP_OK(hipGetLastError());

@@ -3707,10 +3707,10 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
     for (int c = 1; c < nclus; c++)
       if (csize[c] > csize[b]) b = c;
     best_c = nclus > 0 ? b : -1;
+    // the best cluster's members in index order: positions here (flag[] is
+    // free again), the record copies below by the whole block
     int k = 0;
-    HypRec* Hh = hyps + (size_t)f * kMaxHyps;
-    for (int j = 0; j < n; j++)
-      if (best_c >= 0 && cid[j] == best_c) Hh[k++] = G[j];
+    for (int j = 0; j < n; j++) flag[j] = (best_c >= 0 && cid[j] == best_c) ? k++ : -1;
     nC = k;
     st[f].n_gen = n;
     st[f].n_hyps = k;
@@ -3718,6 +3718,10 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
     dbg[f].n_gen = n;
     dbg[f].n_hyps = k;
   }
+  __syncthreads();
+  HypRec* Hh = hyps + (size_t)f * kMaxHyps;
+  for (int j = tid; j < n; j += blockDim.x)
+    if (flag[j] >= 0) Hh[flag[j]] = G[j];
 }
 
 // prefix over frames: draws of the shared cv::RNG stream happen only for
