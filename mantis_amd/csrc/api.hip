@@ -175,6 +175,13 @@ struct Ctx {
   int32_t* d_octl = nullptr;  // [2][2]: entries, next
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
+  // small batches (latency): ObjPose jobs per wave and rounds (MANTIS_OP_LANES_SMALL, MANTIS_OP_ROUNDS_SMALL).
+  // One job per wave in one round: a lane's chain no longer waits on the other
+  // lanes' divergent paths (rpp_first 3.49 / 3.50 -> 2.87-2.96 ms, p50 8.24 / 8.54
+  // -> 7.72-8.00 ms at one 4-camera rig per call, profiles/r04_p50_objpose_lanes.txt;
+  // 64 jobs per wave in one round: 9.1 ms)
+  int op_lanes_small = 1, op_rounds_small = 1;
+  int s1b_spread_small = 1;  // k_rpp_s1b lanes per item for small batches (MANTIS_S1B_SPREAD_SMALL: 1, 2, 4 ... 64)
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
   int canny_strip = 2;  // k_canny_strip: 2 = 8 columns per lane where W % 8 == 0, 1 = 4 columns; 0 = tiles (MANTIS_CANNY_STRIP)
   // the same for batches of at most fc_small_frames frames (the rig-latency
@@ -544,8 +551,8 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
 // previous one spilled, the last runs every job to the end.
 template <int MODE>
 mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::Refine* rf, const int32_t* jobs,
-                                 RppQueue* q, FrameState* st, int paired) {
-  const int rounds = std::max(1, c->op_rounds);
+                                 RppQueue* q, FrameState* st, int paired, int lanes = 64, int rounds = 0) {
+  if (rounds <= 0) rounds = std::max(1, c->op_rounds);
   if ((size_t)blocks * 256 > (size_t)c->op_cap) blocks = (unsigned)(c->op_cap / 256);  // a pool holds a grid's lanes
   for (int r = 0; r < rounds; r++) {
     const int in = (r + 1) & 1, out = r & 1;
@@ -556,6 +563,8 @@ mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::R
     rd.first = r == 0;
     rd.last = r == rounds - 1;
     rd.spill_below = c->op_spill;
+    rd.lanes = lanes;
+    rd.pad = 0;
     if (!rd.last) HIP_OK(hipMemsetAsync(rd.out.ctl, 0, 2 * sizeof(int32_t), c->s));
     k_objpose_q<MODE><<<blocks, 256, 0, c->s>>>(items, rf, jobs, q, st, paired, rd);
   }
@@ -564,15 +573,22 @@ mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::R
 
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
                        RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads,
-                       bool paired) {
+                       bool paired, bool small = false) {
   const int pr = paired ? 1 : 0;
-  run_objpose_rounds<0>(c, objpose_blocks(c, paired ? expected_items / 2 : expected_items), items, rf, jobs0, q, st,
-                        pr);
+  // small batches: at most op_lanes_small jobs per wave, the grid sized for that
+  const int lanes = small ? c->op_lanes_small : 64, rounds = small ? c->op_rounds_small : 0;
+  auto blocks_for = [&](size_t jobs) {
+    if (lanes >= 64) return objpose_blocks(c, jobs);
+    return (unsigned)std::max<size_t>(1, std::min<size_t>((jobs + 4 * lanes - 1) / (4 * lanes), (size_t)c->op_cap / 256));
+  };
+  run_objpose_rounds<0>(c, blocks_for(paired ? expected_items / 2 : expected_items), items, rf, jobs0, q, st, pr,
+                        lanes, rounds);
   mark(c, "rpp_first");
-  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
-      items, jobs0, jobs1, q, pr);
+  const int spread = small ? c->s1b_spread_small : 1;
+  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items * spread + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
+      items, jobs0, jobs1, q, pr, spread);
   mark(c, "rpp_2nd");
-  run_objpose_rounds<1>(c, objpose_blocks(c, expected_items * 2), items, rf, jobs1, q, st, 0);
+  run_objpose_rounds<1>(c, blocks_for(expected_items * 2), items, rf, jobs1, q, st, 0, lanes, rounds);
   mark(c, "rpp_cand");
   k_rpp_merge<<<(unsigned)((ni + 255) / 256), 256, 0, c->s>>>(items, ni, rf, out, quads,
                                                                quads ? c->cfg.quad_gn_iterations : 0);
@@ -586,7 +602,7 @@ mantis_status run_pose(Ctx* c, int n) {
   const size_t ni = (size_t)n * kMaxQuads * 2;
   mark(c, "rpp_prep");
   launch_rpp_queues(c, c->d_items, c->d_refine, c->d_jobs0, c->d_jobs1, c->d_rq, c->d_rpp, c->d_st, ni, (size_t)n * 160,
-                    c->d_quads, true);
+                    c->d_quads, true, n <= c->fc_small_frames);
   k_frame_hyps<<<n, 256, 0, c->s>>>(c->d_rpp, c->d_st, c->d_gen, c->d_hyps, c->d_dbg, 0.5, 0.2);
   mark(c, "hyps_cluster");
   HIP_OK(hipGetLastError());
@@ -940,6 +956,12 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_OP_LANES_SMALL")) c->op_lanes_small = std::max(1, std::min(64, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_S1B_SPREAD_SMALL")) {
+    const int v = std::atoi(e);
+    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) c->s1b_spread_small = v;
+  }
+  if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   c->F = cfg.max_cams;

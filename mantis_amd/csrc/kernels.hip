@@ -3309,6 +3309,8 @@ struct OpRound {
   OpPool in, out;  // in: unused in round 0 (the queue's job list instead)
   int32_t cap;     // entries a pool holds (>= the grid's lanes)
   int32_t first, last, spill_below;
+  int32_t lanes;   // lanes per wave that take jobs (64; fewer spreads a small queue over more waves)
+  int32_t pad;
 };
 __device__ inline void op_save(const OpPool& p, int32_t cap, int k, const rpp::OpState& s) {
   double* d = p.state + k;
@@ -3376,11 +3378,13 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
   rpp::OpState s;
   int32_t job = -1;
   bool exhausted = false;
+  const bool eligible = lane < rd.lanes;
+  const int refill_at = min(16, rd.lanes);
 #pragma unroll 1
   while (true) {
-    const uint64_t idle = __ballot(job < 0);
+    const uint64_t idle = __ballot(job < 0 && eligible);
     const int nidle = __popcll(idle);
-    if (!exhausted && nidle >= 16) {
+    if (!exhausted && nidle >= refill_at) {
       const int leader = __ffsll((unsigned long long)idle) - 1;
       int base = 0;
       if (lane == leader) base = atomicAdd(next, nidle);
@@ -3447,9 +3451,13 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
 #define MK_S1B_WPE 2
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MK_S1B_WPE))) void k_rpp_s1b(RppItem* __restrict__ items, const int32_t* __restrict__ jobs0,
-                                                int32_t* __restrict__ jobs1, RppQueue* q, int paired) {
+                                                int32_t* __restrict__ jobs1, RppQueue* q, int paired, int spread) {
   const int n0 = q->n0 << (paired ? 1 : 0);  // paired: both orientations of every first-queue job
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n0; k += gridDim.x * blockDim.x) {
+  // spread > 1 (small batches): one item per `spread` lanes, so an item's
+  // root-finder path does not wait on other items' divergent ones
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g % spread) return;
+  for (int k = g / spread; k < n0; k += gridDim.x * blockDim.x / spread) {
     const int32_t i = paired ? jobs0[k >> 1] + (k & 1) : jobs0[k];
     if (!items[i].active) continue;
     double model[12];
