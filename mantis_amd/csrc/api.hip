@@ -176,11 +176,11 @@ struct Ctx {
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
   // small batches (latency): ObjPose jobs per wave and rounds (MANTIS_OP_LANES_SMALL, MANTIS_OP_ROUNDS_SMALL).
-  // One job per wave in one round: a lane's chain no longer waits on the other
-  // lanes' divergent paths (rpp_first 3.49 / 3.50 -> 2.87-2.96 ms, p50 8.24 / 8.54
-  // -> 7.72-8.00 ms at one 4-camera rig per call, profiles/r04_p50_objpose_lanes.txt;
-  // 64 jobs per wave in one round: 9.1 ms)
-  int op_lanes_small = 1, op_rounds_small = 1;
+  // One job per wave in one round measured faster (rpp_first 3.49 / 3.50 -> 2.87-2.96
+  // ms, p50 8.24 / 8.54 -> 7.72-8.00 ms at one 4-camera rig per call,
+  // profiles/r04_p50_objpose_lanes.txt) but failed the GPU reproducibility tests
+  // (run-to-run rig poses differ): off until that is understood
+  int op_lanes_small = 64, op_rounds_small = 6;
   int s1b_spread_small = 1;  // k_rpp_s1b lanes per item for small batches (MANTIS_S1B_SPREAD_SMALL: 1, 2, 4 ... 64)
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
   int canny_strip = 2;  // k_canny_strip: 2 = 8 columns per lane where W % 8 == 0, 1 = 4 columns; 0 = tiles (MANTIS_CANNY_STRIP)
