@@ -176,10 +176,8 @@ struct Ctx {
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
   // small batches (latency): ObjPose jobs per wave and rounds (MANTIS_OP_LANES_SMALL, MANTIS_OP_ROUNDS_SMALL).
-  // One job per wave in one round measured faster (rpp_first 3.49 / 3.50 -> 2.87-2.96
-  // ms, p50 8.24 / 8.54 -> 7.72-8.00 ms at one 4-camera rig per call,
-  // profiles/r04_p50_objpose_lanes.txt) but failed the GPU reproducibility tests
-  // (run-to-run rig poses differ): off until that is understood
+  // Fewer jobs per wave measured slower once correct (one per wave in one round:
+  // rpp_first 3.28 -> 3.64 / 3.80 ms, profiles/r04_p50_objpose_lanes_fixed.txt)
   int op_lanes_small = 64, op_rounds_small = 6;
   int s1b_spread_small = 1;  // k_rpp_s1b lanes per item for small batches (MANTIS_S1B_SPREAD_SMALL: 1, 2, 4 ... 64)
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)

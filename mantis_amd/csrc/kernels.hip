@@ -3390,7 +3390,7 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
       if (lane == leader) base = atomicAdd(next, nidle);
       base = __shfl(base, leader);
       if (base + nidle >= njobs) exhausted = true;
-      if (job < 0) {
+      if (job < 0 && eligible) {  // only the reserved lanes (idle & eligible) take one
         const int k = base + __popcll(idle & ((1ull << lane) - 1));
         if (k < njobs) {
           if (rd.first) {
