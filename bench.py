@@ -453,8 +453,8 @@ def run_config3(a, rk, cpu):
     work = {
         # BGR read once; candidate and strong-root bit planes written
         "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
-        # candidate bits read, edge bits written
-        "hysteresis": ("hbm", frames_step * (W * H // 4)),
+        # candidate and strong bit planes read, edge bits written
+        "hysteresis": ("hbm", frames_step * (3 * W * H // 8)),
         # edge bits read once; padded detector bits and mask bits written
         "morph": ("hbm", frames_step * (W * H // 8 + (W + 2) * (H + 2) // 8 + W * H // 8)),
         "components": ("hbm", frames_step * (5 * (W + 2) * (H + 2))),
@@ -467,7 +467,7 @@ def run_config3(a, rk, cpu):
     }
     stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_final"),
                      "canny_nms": ("k_canny_strip<2>", "k_canny_strip<1>", "k_canny"),
-                     "hysteresis": ("k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
+                     "hysteresis": ("k_hyst_rec", "k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
                      "morph": ("k_morph",)}
     digest = lib_sha16()
     src_digest = src_sha16()
@@ -511,7 +511,7 @@ def run_config3(a, rk, cpu):
     # HBM traffic and VALU issue from PMC summaries of this same build
     # (tools/pmc_score.sh / tools/pmc_traffic.sh write lib_sha16): per launch =
     # per-frame counters x frames_step; null when no summary matches the build
-    pj = pmc_for(os.path.join("profiles", "r04_pmc.json"))
+    pj = pmc_for(os.path.join("profiles", "r05_pmc.json"))
     pmc_k = {} if pj is None else pj["kernels"]
     pmc_fr = None if pj is None else pj["frames_per_launch"]
 
@@ -531,7 +531,7 @@ def run_config3(a, rk, cpu):
             r["valu_instructions_per_launch"] = int(vi)
             # wave64 VALU instruction = 2 cycles on a SIMD-32 (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
             r["valu_issue_frac"] = round(vi * 2 / (1024 * 2.4e9 * r["avg_launch_ms"] * 1e-3), 4)
-        r["pmc_source"] = "profiles/r04_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step)"
+        r["pmc_source"] = "profiles/r05_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step)"
 
     if roof is not None and dom == "score_pf_yaw":
         roof["bound_note"] = ("FP32 screen + exact FP64 fallback on the VALU, gathers from L2/MALL: frac counts the "

@@ -99,6 +99,7 @@ _SIGS = {
     "mantis_process_batch": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_int32, C.c_int32,
                                        C.POINTER(MantisResult), C.POINTER(MantisCamResult)]),
     "mantis_canny": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p]),
+    "mantis_hysteresis": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
     "mantis_masks": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p, C.c_void_p]),
     "mantis_detect_quads": (C.c_int, [C.c_void_p, C.POINTER(MantisImage), C.c_void_p, C.c_int32,
                                       C.POINTER(C.c_int32)]),
@@ -436,6 +437,14 @@ class Mantis:
     def canny(self, img):
         out = np.zeros((img.height, img.width), np.uint8)
         self._chk(lib().mantis_canny(self.h, C.byref(img), out.ctypes.data), "canny")
+        return out
+
+    def hysteresis(self, cls):
+        """cv::Canny's hysteresis on a class plane (0 none, 1 weak candidate, 2 strong)."""
+        cls = np.ascontiguousarray(cls, np.uint8)
+        h, w = cls.shape
+        out = np.zeros((h, w), np.uint8)
+        self._chk(lib().mantis_hysteresis(self.h, cls.ctypes.data, w, h, out.ctypes.data), "hysteresis")
         return out
 
     def masks(self, img):

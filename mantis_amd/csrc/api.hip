@@ -150,6 +150,8 @@ struct Ctx {
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
+  bool hyst_rec = true;    // hysteresis by bit-parallel reconstruction (k_hyst_rec) where the frame fits it; MANTIS_HYST_REC=0: run CCL
+  size_t hyst_rec_lds = 0;  // dynamic LDS k_hyst_rec may take (a frame's candidate words)
   bool pf_split = true;    // small batches: each particle-filter iteration over several blocks per frame
                            // (k_score_pf_part); MANTIS_PF_SPLIT=0 keeps one block per frame
   uint32_t* d_dbits = nullptr;                                  // padded detector bits
@@ -395,6 +397,9 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
   return MANTIS_OK;
 }
 
+mantis_status run_hyst_ccl(Ctx* c, int n, int W, int H, bool edge_bytes);
+mantis_status run_hysteresis(Ctx* c, int n, int W, int H, bool edge_bytes);
+
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
 mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false, bool det_bytes = false) {
   const size_t P = c->plane;
@@ -419,26 +424,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
                                                         c->vec_ok ? 1 : 0, c->d_b1, c->d_b2, B, tgx, tgy);
     mark(c, "canny_nms/k_canny");
   }
-  // hysteresis run CCL (its planes are free again before the contour CCL reuses them)
-  // mark values 4..255 (the denser bands' flags are <= 3); the flag plane is cleared when they wrap
-  c->hyst_epoch = c->hyst_epoch >= 255 ? 4 : c->hyst_epoch + 1;
-  if (c->hyst_epoch == 4) HIP_OK(hipMemsetAsync(c->d_strong, 0, c->fstride * (size_t)c->F, c->s));
-  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
-              HB_ROWS * ((W + 1) / 2), c->d_st, c->hyst_epoch};
-  // list counters |A|, |B| of every frame (rowb[H + 1], rowb[H + 2])
-  HIP_OK(hipMemset2DAsync(c->d_rowb + H + 1, c->rstride * sizeof(int32_t), 0, 2 * sizeof(int32_t), n, c->s));
-  const int WWb = bits::words(W);
-  k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 3 * sizeof(uint32_t) * HB_ROWS * WWb, c->s>>>(
-      c->d_b1, c->d_b2, B, hr, c->d_eb, W, H);
-  mark(c, "hysteresis/k_hyst_band");
-  const int nseam = (H - 1) / HB_ROWS;
-  if (nseam > 0) k_hyst_seam<<<dim3((nseam + 3) / 4, n), 256, 0, c->s>>>(hr, H);
-  mark(c, "hysteresis/k_hyst_seam");
-  k_hyst_mark<<<dim3(8, n), 256, 0, c->s>>>(hr, H);
-  mark(c, "hysteresis/k_hyst_mark");
-  k_hyst_fix<<<dim3(8, n), 256, 0, c->s>>>(hr, c->d_eb, B, W, H);
-  if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
-  mark(c, "hysteresis/k_hyst_fix");
+  if (mantis_status hs = run_hysteresis(c, n, W, H, edge_bytes); hs != MANTIS_OK) return hs;
   // detector binary (padded bit plane) and clean mask (bit plane), one fused pass
   // the contour stage's frame states are zeroed here: the walker's run
   // numbering writes n_runs
@@ -477,6 +463,49 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   }
   if (det_bytes) k_bits_to_bytes<<<blocks_for((size_t)(W + 2) * (H + 2)), 256, 0, c->s>>>(c->d_dbits, c->d_det, W + 2, H + 2,
                                                                                           dbits_wpw(W + 2));
+  HIP_OK(hipGetLastError());
+  return MANTIS_OK;
+}
+
+// cv::Canny's hysteresis on the candidate / strong planes (d_b1, d_b2) -> edge plane d_eb
+mantis_status run_hysteresis(Ctx* c, int n, int W, int H, bool edge_bytes) {
+  const size_t B = c->bstride;
+  const size_t hr_lds = (size_t)((H + HR_ROWS - 1) / HR_ROWS) * HR_ROWS * bits::words(W) * sizeof(uint32_t);
+  if (c->hyst_rec && bits::words(W) <= 63 && H <= HR_ROWS * HR_MAXW && hr_lds <= c->hyst_rec_lds) {
+    // bit-parallel reconstruction: one block per frame, one wave per HR_ROWS-row band, the candidates in LDS
+    k_hyst_rec<<<n, 64 * ((H + HR_ROWS - 1) / HR_ROWS), hr_lds, c->s>>>(c->d_b1, c->d_b2, c->d_eb, B, W, H, c->d_st);
+    if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
+    mark(c, "hysteresis/k_hyst_rec");
+    HIP_OK(hipGetLastError());
+    return MANTIS_OK;
+  }
+  return run_hyst_ccl(c, n, W, H, edge_bytes);
+}
+
+// hysteresis as a run CCL: frames past the reconstruction kernel's reach
+// (W > 2016, H > 720 or the candidate plane past the LDS) and MANTIS_HYST_REC=0 (its planes are free again
+// before the contour CCL reuses them)
+mantis_status run_hyst_ccl(Ctx* c, int n, int W, int H, bool edge_bytes) {
+  const size_t P = c->plane, B = c->bstride;
+  // mark values 4..255 (the denser bands' flags are <= 3); the flag plane is cleared when they wrap
+  c->hyst_epoch = c->hyst_epoch >= 255 ? 4 : c->hyst_epoch + 1;
+  if (c->hyst_epoch == 4) HIP_OK(hipMemsetAsync(c->d_strong, 0, c->fstride * (size_t)c->F, c->s));
+  HystRuns hr{(uint32_t*)c->d_lroot, c->d_lab, c->d_strong, c->d_rowb, c->lstride / 2, P, c->fstride, c->rstride, P / 2,
+              HB_ROWS * ((W + 1) / 2), c->d_st, c->hyst_epoch};
+  // list counters |A|, |B| of every frame (rowb[H + 1], rowb[H + 2])
+  HIP_OK(hipMemset2DAsync(c->d_rowb + H + 1, c->rstride * sizeof(int32_t), 0, 2 * sizeof(int32_t), n, c->s));
+  const int WWb = bits::words(W);
+  k_hyst_band<<<dim3((H + HB_ROWS - 1) / HB_ROWS, n), HB_THREADS, 3 * sizeof(uint32_t) * HB_ROWS * WWb, c->s>>>(
+      c->d_b1, c->d_b2, B, hr, c->d_eb, W, H);
+  mark(c, "hysteresis/k_hyst_band");
+  const int nseam = (H - 1) / HB_ROWS;
+  if (nseam > 0) k_hyst_seam<<<dim3((nseam + 3) / 4, n), 256, 0, c->s>>>(hr, H);
+  mark(c, "hysteresis/k_hyst_seam");
+  k_hyst_mark<<<dim3(8, n), 256, 0, c->s>>>(hr, H);
+  mark(c, "hysteresis/k_hyst_mark");
+  k_hyst_fix<<<dim3(8, n), 256, 0, c->s>>>(hr, c->d_eb, B, W, H);
+  if (edge_bytes) k_bits_to_bytes<<<blocks_for((size_t)W * H), 256, 0, c->s>>>(c->d_eb, c->d_edge, W, H, 0);
+  mark(c, "hysteresis/k_hyst_fix");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
 }
@@ -678,7 +707,12 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // 720p yes, 1080p no)
   const size_t ml = c->pf_mask_lds;
   constexpr int ppb = std::max(1, kPfThreads / 64 / kPfSplit);  // particles per block (one task per wave)
-  if (c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles) {  // MANTIS_PF_SPLIT
+  // small batches split the filter's iterations over blocks (MANTIS_PF_SPLIT); the
+  // end-of-filter writes (pf_error, the filter's pose) belong to the last
+  // iteration's launch, so a config without iterations runs the one-block kernel
+  const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles &&
+                     c->cfg.iterations > 0;
+  if (split) {
     const int nblk = (c->cfg.particles + ppb - 1) / ppb;
     for (int it = 0; it < c->cfg.iterations; it++)
       k_score_pf_part<kPfThreads, kPfSplit><<<dim3(nblk, n), kPfThreads, 0, c->s>>>(
@@ -693,7 +727,6 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
         c->cfg.iterations);
   mark(c, "score_pf_yaw/k_score_pf");
-  const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles;
   if (split) {  // small batches: the 81 shifts over several blocks per frame first
     constexpr int spb = kScoreTail / 128;
     k_score_shift_part<kScoreTail><<<dim3((81 + spb - 1) / spb, n), kScoreTail, 0, c->s>>>(
@@ -962,6 +995,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
+  if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;
@@ -995,6 +1029,16 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
         hipFuncSetAttribute((const void*)k_score_pf<kPfThreads, kPfSplit, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)ml) == hipSuccess)
       c->pf_mask_lds = ml;
+  }
+  {
+    // k_hyst_rec: the frame's candidate plane in LDS beside its static seam rows
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, (const void*)k_hyst_rec) == hipSuccess) {
+      const size_t budget = 160 * 1024 - a.sharedSizeBytes;
+      if (hipFuncSetAttribute((const void*)k_hyst_rec, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) ==
+          hipSuccess)
+        c->hyst_rec_lds = budget;
+    }
   }
   // hysteresis bands: edge, strong and candidate words of HB_ROWS rows in LDS
   if (hipFuncSetAttribute((const void*)k_hyst_band, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1653,6 +1697,21 @@ mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_ou
   HIP_OK(hipMemcpyAsync(canny_out, c->d_edge, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   for (size_t i = 0; i < (size_t)W * H; i++) canny_out[i] = canny_out[i] ? 255 : 0;
+  return MANTIS_OK;
+}
+
+mantis_status mantis_hysteresis(void* ctx, const uint8_t* cls, int32_t width, int32_t height, uint8_t* edges_out) {
+  Ctx* c = (Ctx*)ctx;
+  if (c) bind_device(c);
+  if (!c || !cls || !edges_out) return MANTIS_ERR_ARG;
+  const int W = width, H = height;
+  if (W <= 2 || H <= 2 || W > c->Wmax || H > c->Hmax) { c->err = "image size outside [3, max]"; return MANTIS_ERR_ARG; }
+  HIP_OK(hipMemcpyAsync(c->d_edge, cls, (size_t)W * H, hipMemcpyHostToDevice, c->s));
+  k_cls_to_bits<<<blocks_for((size_t)bits::words(W) * H), 256, 0, c->s>>>(c->d_edge, c->d_b1, c->d_b2, W, H);
+  if (mantis_status st = run_hysteresis(c, 1, W, H, true); st != MANTIS_OK) return st;
+  HIP_OK(hipMemcpyAsync(edges_out, c->d_edge, (size_t)W * H, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  for (size_t i = 0; i < (size_t)W * H; i++) edges_out[i] = edges_out[i] ? 255 : 0;
   return MANTIS_OK;
 }
 

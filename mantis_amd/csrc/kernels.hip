@@ -109,30 +109,10 @@ __device__ inline int lds_find(const int* L, int x) {
   while ((p = L[x]) != x) x = p;
   return x;
 }
-#ifndef MK_HB_HALVE  // LDS union-finds (band CCLs) with path halving in their unions' finds
-#define MK_HB_HALVE 0  // measured slower: hysteresis 5.27 -> 5.65, components 3.59 -> 3.82 ms per 4096 frames
-#endif
-// the unions' finds halve the path as uf_find_c does (a non-root slot takes
-// its grandparent; roots change only through the CAS)
-__device__ inline int lds_find_halve(int* L, int x) {
-  while (true) {
-    const int p = L[x];
-    if (p == x) return x;
-    const int g = L[p];
-    if (g == p) return p;
-    L[x] = g;
-    x = g;
-  }
-}
 __device__ inline void lds_union(int* L, int a, int b) {
   while (true) {
-#if MK_HB_HALVE
-    a = lds_find_halve(L, a);
-    b = lds_find_halve(L, b);
-#else
     a = lds_find(L, a);
     b = lds_find(L, b);
-#endif
     if (a == b) return;
     if (a < b) { int t = a; a = b; b = t; }
     int old = atomicCAS(&L[a], a, b);
@@ -1070,37 +1050,17 @@ __device__ inline void hr_row(const int32_t* rb, int H, int bs, int y, int& g, i
 }
 // band-local union-find on 16-bit labels in LDS (roots = smallest id); the
 // link is a 32-bit CAS on the dword holding the 16-bit slot
-// (bits 12..13 of a root's slot hold its band flags once the unions are done,
-// MK_HB_LFLAGS: ids are < HB_CAP = 4096, so the low 12 bits are the link)
+// (bits 12..13 of a root's slot hold its band flags once the unions are done:
+// ids are < HB_CAP = 4096, so the low 12 bits are the link)
 __device__ inline int hb_find(const uint16_t* L, int x) {
   int p;
   while ((p = L[x] & 0xfff) != x) x = p;
   return x;
 }
-// find with path halving (the unions' finds): a non-root slot takes its
-// grandparent, which is still an ancestor, so every find and link stays
-// valid; the 16-bit store leaves the other half of the dword alone, and a
-// concurrent link's CAS on that half sees the change and retries. Roots are
-// the same smallest ids, so the labels do not depend on the halving.
-__device__ inline int hb_find_halve(uint16_t* L, int x) {
-  while (true) {
-    const int p = L[x] & 0xfff;
-    if (p == x) return x;
-    const int g = L[p] & 0xfff;
-    if (g == p) return p;
-    L[x] = (uint16_t)g;
-    x = g;
-  }
-}
 __device__ inline void hb_union(uint16_t* L, int a, int b) {
   while (true) {
-#if MK_HB_HALVE
-    a = hb_find_halve(L, a);
-    b = hb_find_halve(L, b);
-#else
     a = hb_find(L, a);
     b = hb_find(L, b);
-#endif
     if (a == b) return;
     if (a < b) { const int tt = a; a = b; b = tt; }
     uint32_t* wp = (uint32_t*)(L + (a & ~1));
@@ -1150,12 +1110,6 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
                                                           uint32_t* __restrict__ ebits, int W, int H) {
   __shared__ uint16_t Ll[HB_CAP];
   __shared__ uint32_t Xl[HB_CAP];
-#ifndef MK_HB_LFLAGS
-#define MK_HB_LFLAGS 1
-#endif
-#if !MK_HB_LFLAGS
-  __shared__ uint32_t Sl[HB_CAP / 4];  // per root byte: bit 0 strong, bit 1 reaches the band's edge rows
-#endif
   __shared__ int32_t rbl[HB_ROWS + 1];
   extern __shared__ uint32_t Ew[];     // the band's edge words (rows x WW), then its strong words, then its candidates
   const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1247,9 +1201,6 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
   }
   for (int q = wave; q < nr; q += HB_WAVES) hb_emit_runs(Cw + q * WW, WW, (uint16_t*)Xl, rbl[q], lane);
   for (int i = t; i < n; i += HB_THREADS) Ll[i] = (uint16_t)i;
-#if !MK_HB_LFLAGS
-  for (int i = t; i < (n + 3) / 4; i += HB_THREADS) Sl[i] = 0u;
-#endif
   __syncthreads();
   MK_HTICK(2);
   uint16_t* Li = Ll;
@@ -1262,29 +1213,19 @@ __global__ __launch_bounds__(HB_THREADS) void k_hyst_band(const uint32_t* __rest
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
       const int root = hb_find(Ll, j);
       const uint32_t b = (run_strong(Sw + q * WW, Xl[j] & 0xffff, Xl[j] >> 16) ? 1u : 0u) | (edge_row(q) ? 2u : 0u);
-#if MK_HB_LFLAGS
       // the band flags go to bits 12..13 of the root's own slot (its link
       // bits stay == root, so concurrent finds still stop there); a root
       // never stores its own slot, which would drop flags already set
       if (root != j) Ll[j] = (uint16_t)root;
       if (b) atomicOr((uint32_t*)(Ll + (root & ~1)), (b << 12) << (16 * (root & 1)));
-#else
-      Ll[j] = (uint16_t)root;
-      if (b) atomicOr(&Sl[root >> 2], b << (8 * (root & 3)));
-#endif
     }
   }
   __syncthreads();
   MK_HTICK(4);
   for (int q = wave; q < nr; q += HB_WAVES) {
     for (int j = rbl[q] + lane; j < rbl[q + 1]; j += 64) {
-#if MK_HB_LFLAGS
       const int root = Ll[j] & 0xfff;
       const int fb = (Ll[root] >> 12) & 3;
-#else
-      const int root = Ll[j];
-      const int fb = (Sl[root >> 2] >> (8 * (root & 3))) & 3;
-#endif
       // global labels / extents only where a later kernel looks: the band's
       // seam rows (its first / last row where another band lies beyond:
       // k_hyst_seam's unions), list B runs (fb == 2: k_hyst_fix) and the roots
@@ -1352,6 +1293,251 @@ __global__ __launch_bounds__(256) void k_hyst_fix(HystRuns hr, uint32_t* __restr
     const int a = X[j] & 0xffff, b = X[j] >> 16;
     uint32_t* eb = ebits + (size_t)f * bstride + (size_t)y * WW;
     for (int w = a >> 5; w <= (b >> 5); w++) atomicOr(&eb[w], span_mask(w, a, b));
+  }
+}
+
+// ================================= hysteresis as bit-parallel reconstruction
+// cv::Canny's hysteresis (the stack walk from every strong pixel over the
+// 8-connected candidates, QuadDetection.h:212 / HypothesisEvaluation.h:327)
+// marks exactly the candidate components that hold a strong pixel: the
+// morphological reconstruction of the candidate plane C from the strong plane
+// S, the least E with E = (S ∪ dilate8(E)) ∩ C. No labels: one block per frame,
+// wave w owns rows [w HR_ROWS, (w + 1) HR_ROWS) with its band's C and E words
+// in VGPRs (lane = 32-pixel word column, W <= 2016) and reaches the fixpoint
+// with row sweeps:
+//   row fill   every candidate run of a row that holds a seed, as two
+//              additions along the row: c + s carries from each run's lowest
+//              seed to the run's end (rightward), and the same on bit-reversed
+//              words in reversed lane order (leftward); the carries between
+//              words are one 64-bit scalar addition over the lanes' generate /
+//              propagate ballots
+//   sweeps     seed(y) = E(y) ∪ (dilate3(E(y ∓ 1)) ∩ C(y)), then the row fill,
+//              down and up the band alternately until a sweep adds nothing
+//              (each sweep carries a change any distance in its direction)
+//   seams      the bands trade their first / last rows through LDS; a band
+//              whose edge row gains seeds sweeps again; the block stops when
+//              no band gains any (__syncthreads_or)
+// C and S are read once and E written once: 3 W H / 8 bytes per frame.
+#ifndef MK_HR_ROWS
+#define MK_HR_ROWS 45
+#endif
+constexpr int HR_ROWS = MK_HR_ROWS, HR_MAXW = 16;  // rows per wave; waves per block (frames up to 720 rows)
+// 8-neighbour row dilation of a row's words (lanes past the row hold 0; lane
+// 0's left and lane 63's right neighbour wrap to lanes past the row)
+__device__ inline uint32_t hr_dil3(uint32_t e) {
+  return e | __builtin_amdgcn_alignbit(e, dpp_from_left(e), 31) | __builtin_amdgcn_alignbit(dpp_from_right(e), e, 1);
+}
+// carry into lane i (bit i) of a word-wise addition whose lanes generate G / propagate P
+__device__ inline uint64_t hr_carries(uint64_t G, uint64_t P) {
+  const uint64_t A = G | P;
+  return (A + G) ^ A ^ G;
+}
+// word-wise addition across the row's lanes: carry out of each lane's c + s as
+// a lane mask (v_add_co's carry, straight into an SGPR pair), and t + the
+// carry into the lane (v_addc_co's carry-in operand is the lane mask k)
+__device__ inline uint32_t hr_add(uint32_t c, uint32_t s, uint64_t& g) {
+  uint32_t t;
+  asm("v_add_co_u32 %0, %1, %2, %3" : "=v"(t), "=s"(g) : "v"(c), "v"(s));
+  return t;
+}
+__device__ inline uint32_t hr_addc(uint32_t t, uint64_t k) {
+  uint32_t u;
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %2, 0, %3" : "=v"(u), "=s"(co) : "v"(t), "s"(k));
+  return u;
+}
+// every candidate run of the row (this lane's word c) that holds a seed bit of s (s ⊆ c)
+__device__ inline uint32_t hr_fill(uint32_t c, uint32_t s) {
+  uint64_t gr, gl;
+  const uint32_t t = hr_add(c, s, gr);  // rightward: each run from its lowest seed to its end
+  const uint32_t rt = s | ((hr_addc(t, hr_carries(gr, __ballot(t == 0xffffffffu))) ^ c ^ s) & c);
+  const uint32_t cr = __builtin_bitreverse32(c), sr = __builtin_bitreverse32(s);
+  const uint32_t u = hr_add(cr, sr, gl);  // leftward: the same on the reversed row (carries from lane i + 1 into lane i)
+  const uint64_t kl = __builtin_bitreverse64(
+      hr_carries(__builtin_bitreverse64(gl), __builtin_bitreverse64(__ballot(u == 0xffffffffu))));
+  const uint32_t lf = __builtin_bitreverse32(sr | ((hr_addc(u, kl) ^ cr ^ sr) & cr));
+  return rt | lf;
+}
+__global__ __launch_bounds__(64 * HR_MAXW) void k_hyst_rec(const uint32_t* __restrict__ cbits,
+                                                           const uint32_t* __restrict__ sbits,
+                                                           uint32_t* __restrict__ ebits, size_t bstride, int W,
+                                                           int H, FrameState* st) {
+  __shared__ uint32_t xt[HR_MAXW][64], xb[HR_MAXW][64];  // every band's first / last row of E
+  extern __shared__ uint32_t hr_c[];                     // the bands' candidate words (waves x HR_ROWS x WW)
+  const int f = blockIdx.x, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), nwv = blockDim.x >> 6;
+  const int WW = bits::words(W);
+  const int y0 = wave * HR_ROWS, nr = min(HR_ROWS, H - y0);  // nr >= 1: nwv = ceil(H / HR_ROWS)
+  const bool on = lane < WW;
+  const uint32_t vm = on ? bits::valid(lane, W) : 0u;
+  // band bases are wave-uniform (scalar); the lane's word offset is 32-bit
+  const size_t band = (size_t)f * bstride + (size_t)y0 * WW;
+  const gu32* cb = gwords(cbits + band);
+  const gu32* sb = gwords(sbits + band);
+  // C goes to LDS, E stays in VGPRs. The band's LDS slice holds its WW word
+  // columns HR_ROWS words apart (lane-major: the rows of a lane are one base
+  // VGPR plus immediate offsets, and the odd pitch keeps the lanes on distinct
+  // banks); rows past the frame hold 0, so the sweeps leave their E 0 and the
+  // up sweep reaches a short band's last row with the zero row below it. Every
+  // global load is issued (rows past the frame re-read its last row, lanes past
+  // the row word 0; the row test and vm zero the extra words), and lanes past
+  // the row read lane 0's LDS column and drop it (onm).
+  const int lw = on ? lane : 0;
+  const uint32_t onm = on ? ~0u : 0u;
+  uint32_t* cl = hr_c + (y0 * WW + lw * HR_ROWS);
+  uint32_t e[HR_ROWS];
+#pragma unroll
+  for (int r = 0; r < HR_ROWS; r++) {
+    const int o = min(r, nr - 1) * WW + lw;
+    const uint32_t cw = r < nr ? cb[o] & vm : 0u;
+    e[r] = sb[o] & cw;
+    if (on) cl[r] = cw;
+  }
+  const auto c = [&](int r) -> uint32_t { return cl[r] & onm; };
+  uint32_t top = 0u, bot = 0u;  // the rows of E above / below the band (the neighbours' edge rows)
+  // Sweep windows: a down sweep re-examines row r only if the row above it
+  // (row -1: top) changed since r was last made consistent from above, i.e.
+  // it starts below the first row the previous sweep changed, runs through the
+  // row after its last one, and goes on past it while rows keep changing; an
+  // up sweep likewise from below (row HR_ROWS: bot). [clo, chi] are the rows
+  // the previous sweep changed; a sweep that changes nothing ends the settle.
+  // The very first sweep fills every seeded row (S is not run-closed yet) and
+  // the up sweep after it examines every row.
+  bool go = true, down = true, all = true, pend_bot = false;
+  int clo = -1, chi = HR_ROWS - 1;
+#ifdef MK_HYST_TICKS  // diagnostics (tools/hyst_ticks.py rec): seam rounds, sweeps, filled rows, phase ticks
+  __shared__ int hs_cnt[3];
+  const uint64_t tk0 = wall_clock64();
+  int n_sweeps = 0, n_fills = 0, n_rounds = 0, t_settle = 0;
+  if (threadIdx.x < 3) hs_cnt[threadIdx.x] = 0;
+#endif
+  while (true) {
+    while (go) {
+      asm volatile("" ::: "memory");  // the LDS reads of C stay in the sweeps (hoisted, they would take the VGPRs back)
+      int nlo = HR_ROWS + 1, nhi = -2;  // rows this sweep changes
+      bool live = false;                // the previous row of this sweep changed
+      if (down) {
+        const int from = clo + 1, upto = chi + 1;
+#pragma unroll
+        for (int r = 0; r < HR_ROWS; r++) {
+          if (r < from) continue;
+          const uint32_t cw = c(r);
+          if (r > upto && !live) break;
+          const uint32_t sd = e[r] | (hr_dil3(r == 0 ? top : e[r - 1]) & cw);
+          live = false;
+          if (__ballot(all ? sd != 0u : sd != e[r])) {
+#ifdef MK_HYST_TICKS
+            n_fills++;
+#endif
+            const uint32_t n = hr_fill(cw, sd);
+            if (__ballot(n != e[r])) {
+              live = true;
+              nlo = min(nlo, r);
+              nhi = r;
+            }
+            e[r] = n;
+          }
+        }
+      } else {
+        const int from = chi - 1, upto = clo - 1;
+#pragma unroll
+        for (int r = HR_ROWS - 1; r >= 0; r--) {
+          if (r > from) continue;
+          const uint32_t cw = c(r);
+          if (r < upto && !live) break;
+          const uint32_t sd = e[r] | (hr_dil3(r == HR_ROWS - 1 ? bot : e[r + 1]) & cw);
+          live = false;
+          if (__ballot(sd != e[r])) {
+#ifdef MK_HYST_TICKS
+            n_fills++;
+#endif
+            const uint32_t n = hr_fill(cw, sd);
+            if (__ballot(n != e[r])) {
+              live = true;
+              nhi = max(nhi, r);
+              nlo = r;
+            }
+            e[r] = n;
+          }
+        }
+      }
+#ifdef MK_HYST_TICKS
+      n_sweeps++;
+#endif
+      if (all) {
+        all = false;
+        clo = 0;
+        chi = HR_ROWS;
+      } else {
+        clo = nlo;
+        chi = nhi;
+        if (pend_bot) {  // the up sweep after a seam round's first (down) sweep also takes the bottom seeds
+          pend_bot = false;
+          if (clo > chi) clo = HR_ROWS;
+          chi = HR_ROWS;
+        }
+      }
+      go = clo <= chi;
+      down = !down;
+    }
+#ifdef MK_HYST_TICKS
+    if (n_rounds++ == 0) t_settle = (int)(wall_clock64() - tk0);
+#endif
+    // seams: a band whose first / last row gains seeds from its neighbour sweeps again
+    xt[wave][lane] = e[0];
+    xb[wave][lane] = e[HR_ROWS - 1];  // read only by the next band: this band is full then
+    __syncthreads();
+    top = wave > 0 ? xb[wave - 1][lane] : 0u;
+    bot = wave + 1 < nwv ? xt[wave + 1][lane] : 0u;
+    const bool nt = __ballot((hr_dil3(top) & c(0) & ~e[0]) != 0u) != 0;
+    const bool nb = __ballot((hr_dil3(bot) & c(HR_ROWS - 1) & ~e[HR_ROWS - 1]) != 0u) != 0;
+    go = nt || nb;
+    down = nt;
+    pend_bot = nt && nb;
+    clo = nt ? -1 : HR_ROWS;
+    chi = nt ? -1 : HR_ROWS;
+    if (!__syncthreads_or(go)) break;
+  }
+#ifdef MK_HYST_TICKS
+  if (lane == 0) {
+    atomicMax(&hs_cnt[0], n_sweeps);
+    atomicAdd(&hs_cnt[1], n_sweeps);
+    atomicAdd(&hs_cnt[2], n_fills);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st[f].ticks[0] = n_rounds;         // seam rounds (1: the first settle sufficed)
+    st[f].ticks[1] = hs_cnt[0];        // most sweeps of one band
+    st[f].ticks[2] = hs_cnt[1];        // sweeps of all bands
+    st[f].ticks[3] = hs_cnt[2];        // row fills of all bands
+    st[f].ticks[4] = t_settle;         // first settle (wave 0), 10 ns ticks
+    st[f].ticks[5] = (int)(wall_clock64() - tk0);
+  }
+#endif
+  // the store offsets are recomputed here rather than kept alive from the loads
+  int lo = lane, nrs = nr;
+  asm volatile("" : "+v"(lo), "+s"(nrs));
+  uint32_t* eb = ebits + band;
+#pragma unroll
+  for (int r = 0; r < HR_ROWS; r++)
+    if (lo < WW && r < nrs) eb[r * WW + lo] = e[r];
+}
+
+// mantis_hysteresis stage entry: class bytes (0 none, 1 weak candidate, 2
+// strong) -> the candidate / strong bit planes (a strong byte is a candidate)
+__global__ __launch_bounds__(256) void k_cls_to_bits(const uint8_t* __restrict__ cls, uint32_t* __restrict__ cb,
+                                                     uint32_t* __restrict__ sb, int W, int H) {
+  const int WW = bits::words(W);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < WW * H; k += gridDim.x * blockDim.x) {
+    const int y = k / WW, w = k - y * WW;
+    uint32_t cw = 0, sw = 0;
+    for (int b = 0; b < 32 && 32 * w + b < W; b++) {
+      const uint8_t v = cls[(size_t)y * W + 32 * w + b];
+      cw |= (uint32_t)(v != 0) << b;
+      sw |= (uint32_t)(v == 2) << b;
+    }
+    cb[k] = cw;
+    sb[k] = sw;
   }
 }
 
@@ -4138,11 +4324,6 @@ __device__ inline void block_score_color(const PoseOf& pose_of, int nh, const do
 #define MK_SCR_UNROLL 6
 #endif
 constexpr int kScrUnroll = MK_SCR_UNROLL;  // landmarks per lane in flight (their pixel loads overlap)
-#ifndef MK_SCORE_PIPE2
-// scorers' tasks software-pipelined (screen_issue / screen_finish): measured
-// slower (score stage 11.0 / 11.2 -> 11.8 / 11.8 ms per 4096 frames, A/B/A/B)
-#define MK_SCORE_PIPE2 0
-#endif
 struct UQueue {
   uint32_t* e;  // entries: tag << 16 | landmark
   int32_t* n;   // entries pushed (past cap: those were recomputed in place)
@@ -4218,11 +4399,7 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
     // needed), so the U loads of a lane are in flight together
     uint32_t mw[U];
 #pragma unroll
-#ifdef MK_PF_EXP_NOMASK  // cost experiment (wrong results): no mask lookups, every pixel a hit
-    for (int k = 0; k < U; k++) mw[k] = 0xffffffffu;
-#else
     for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
-#endif
     uint32_t pv[U];
     int hm[U];
 #pragma unroll
@@ -4231,11 +4408,7 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
       hm[k] = hit ? -1 : 0;
       const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
       typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
-#ifdef MK_PF_EXP_NOPIX  // cost experiment (wrong results): no pixel gathers
-      pv[k] = (uint32_t)off;
-#else
       pv[k] = *(gu32u*)(bgr + off);
-#endif
     }
     // the terms as masks, not selects: every loaded value is consumed, so the
     // compiler keeps the U loads unconditional (in flight together) instead
@@ -4309,129 +4482,6 @@ struct WaveLms {
                           n_out);
   }
 };
-// The same trip split in two halves so a wave can keep one trip's pixel
-// loads in flight while it projects the next (software pipelining over a
-// wave's tasks): screen_issue projects the trip's landmarks, queues the unsure
-// ones and issues the mask / pixel loads; screen_finish turns the loaded
-// pixels into the integer sum and count. A task is one trip (le - lb <=
-// 64 U landmarks). Same terms and sums as wave_sums_screen.
-template <int U>
-struct ScrPend {
-  uint32_t pv[U];        // loaded pixel dword per slot
-  uint32_t hit, in, lst; // bit k: mask hit / SCR_IN / last pixel of the frame (read one byte early)
-  int s, n;              // terms added in place (the queue was full)
-};
-template <int U, class MK>
-__device__ inline void screen_issue(const PoseF& P, const float4* lmf, int lb, int le, const ScreenCam& sc, int W,
-                                    int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
-                                    const double* lmd, const Cam* cmp, ScrPend<U>& pd) {
-  const int lane = threadIdx.x & 63;
-  const int last = W * H - 1;
-  int st[U], lin[U], px[U], py[U];
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    const int l = lb + lane + 64 * k;
-    const float4 L = lmf[l < le ? l : le - 1];
-    int x, y;
-    const int t = screen_project(P, L.x, L.y, L.z, L.w, sc, W, H, &x, &y);
-    st[k] = l < le ? t : SCR_OUT;
-    const bool in = st[k] == SCR_IN;
-    px[k] = in ? x : 0;
-    py[k] = in ? y : 0;
-    lin[k] = in ? y * W + x : 0;
-  }
-  uint32_t mw[U];
-#pragma unroll
-  for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
-  pd.hit = pd.in = pd.lst = 0u;
-  pd.s = pd.n = 0;
-  int cu = 0;
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    const bool hit = st[k] == SCR_IN && mask.test(mw[k], px[k]);
-    const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
-    typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
-    pd.pv[k] = *(gu32u*)(bgr + off);
-    pd.hit |= (hit ? 1u : 0u) << k;
-    pd.in |= (st[k] == SCR_IN ? 1u : 0u) << k;
-    pd.lst |= (lin[k] == last ? 1u : 0u) << k;
-    cu += st[k] == SCR_UNSURE;
-  }
-  if (__ballot(cu > 0)) {  // wave-aggregated queue append: one LDS atomic
-    const int incl = wave_incl_scan(cu, lane);
-    int base = 0;
-    if (lane == 63) base = atomicAdd(q.n, incl);
-    base = __builtin_amdgcn_readlane(base, 63);
-    int idx = base + incl - cu;
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      if (st[k] != SCR_UNSURE) continue;
-      const int l = lb + lane + 64 * k;
-      if (idx < q.cap) {
-        q.e[idx] = ((uint32_t)tag << 16) | (uint32_t)l;
-      } else {
-        int e;
-        if (exact_term(*Tx, lmd + 3 * l, *cmp, W, H, bgr, mask, e)) { pd.n++; pd.s += e; }
-      }
-      idx++;
-    }
-  }
-}
-template <int U>
-__device__ inline void screen_finish(const ScrPend<U>& pd, long long& s_out, int& n_out) {
-  int s = pd.s, n = pd.n;
-#pragma unroll
-  for (int k = 0; k < U; k++) {
-    const uint32_t v = (pd.lst >> k) & 1u ? pd.pv[k] >> 8 : pd.pv[k];
-    const uint32_t d = ~v & 0xffffffu;
-    const int term = (int)__builtin_amdgcn_udot4(d, d, 0u, false);
-    constexpr int kBlack = 3 * 255 * 255;
-    const int hm = -(int)((pd.hit >> k) & 1u), im = -(int)((pd.in >> k) & 1u);
-    const int e = kBlack ^ ((term ^ kBlack) & hm);
-    n -= im;
-    s += e & im;
-  }
-  // wave totals in int32 (<= 64 lanes x 12 landmarks x 3 * 255^2 < 2^31)
-  s_out = wave_sum(s);
-  n_out = wave_sum(n);
-}
-// A wave's tasks t = first, first + stride, ... < ntasks, each one trip,
-// pipelined: task t's pixel loads are in flight while task t + stride is
-// projected. task(t, P, lb, le, tag, Tx) describes task t (pose, landmark
-// range, queue tag, exact pose); done(t, sum, count) takes its result (all lanes).
-template <int U, class MK, class Task, class Done>
-__device__ inline void wave_tasks_screen(int first, int stride, int ntasks, const float4* lmf, const ScreenCam& sc,
-                                         int W, int H, const uint8_t* bgr, const MK& mask, UQueue q,
-                                         const double* lmd, const Cam* cmp, const Task& task, const Done& done) {
-  int t = first;
-  if (t >= ntasks) return;
-  ScrPend<U> cur;
-  {
-    PoseF P;
-    int lb, le, tag;
-    const Xf* Tx;
-    task(t, P, lb, le, tag, Tx);
-    screen_issue<U>(P, lmf, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp, cur);
-  }
-  while (true) {
-    const int tn = t + stride;
-    ScrPend<U> nxt;
-    if (tn < ntasks) {
-      PoseF P;
-      int lb, le, tag;
-      const Xf* Tx;
-      task(tn, P, lb, le, tag, Tx);
-      screen_issue<U>(P, lmf, lb, le, sc, W, H, bgr, mask, q, tag, Tx, lmd, cmp, nxt);
-    }
-    long long sum;
-    int cnt;
-    screen_finish<U>(cur, sum, cnt);
-    done(t, sum, cnt);
-    if (tn >= ntasks) break;
-    cur = nxt;
-    t = tn;
-  }
-}
 // the block recomputes the queued landmarks exactly: add(tag, term) for those
 // in frame (pose_of(tag) = the tag's FP64 c2w)
 template <class MK, class PoseOf, class Add>
@@ -4556,31 +4606,6 @@ __global__ __launch_bounds__(NT) void k_score_init(
   const int C = st[f].n_hyps;
   // evaluateHypotheses(hyps, cleaned): screened pass, then the unsure landmarks exactly
   const UQueue q{uqe, &uqn, kInitQueue};
-#if MK_SCORE_PIPE2
-  // tasks = (hypothesis, half of the landmarks), one trip each, pipelined
-  for (int h = tid; h < C; h += NT) {
-    hs[h] = 0;
-    hn[h] = 0;
-  }
-  __syncthreads();
-  wave_tasks_screen<kScrUnroll>(
-      __builtin_amdgcn_readfirstlane(wave), NT / 64, 2 * C, lmf, fd.scam, W, H, fd.bgr, mask, q, lmk.xyz,
-      &frames[f].cam,
-      [&](int t, PoseF& P, int& lb, int& le, int& tag, const Xf*& Tx) {
-        const int h = t >> 1, k = t & 1;
-        P = posef_from(Hh[h].c2w);
-        lb = nl * k / 2;
-        le = nl * (k + 1) / 2;
-        tag = h;
-        Tx = &Hh[h].c2w;
-      },
-      [&](int t, long long sum, int cnt) {
-        if (lane == 0) {
-          atomicAdd(&hs[t >> 1], (unsigned long long)sum);
-          atomicAdd(&hn[t >> 1], cnt);
-        }
-      });
-#else
   // tasks = (hypothesis, half of the landmarks), a wave's half in registers
   // (as in the particle filter and the shifts); the halves' sums add exactly
   for (int h = tid; h < C; h += NT) {
@@ -4601,7 +4626,6 @@ __global__ __launch_bounds__(NT) void k_score_init(
       atomicAdd(&hn[h], n);
     }
   }
-#endif
   __syncthreads();
   block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return Hh[t].c2w; },
               [&](int t, int e) {
@@ -4761,28 +4785,6 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     MK_PTICK(1);
     // SPLIT waves per particle (landmark slices; integer sums, so the
     // partials combine exactly in any order); a wave's tasks pipelined
-#if MK_SCORE_PIPE2
-    const auto task = [&](int t, PoseF& P, int& lb, int& le, int& tag, const Xf*& Tx) {
-      const int j = t / SPLIT, h = t - j * SPLIT;
-      P = Pf[j];
-      lb = nl * h / SPLIT;
-      le = nl * (h + 1) / SPLIT;
-      tag = j;
-      Tx = &Pc[j];
-    };
-    const auto done = [&](int t, long long sum, int cnt) {
-      if (lane == 0) {
-        Ps[t] = (unsigned long long)sum;
-        Pn[t] = cnt;
-      }
-    };
-    if (LM)
-      wave_tasks_screen<kScrUnroll>(__builtin_amdgcn_readfirstlane(wave), kW, particles * SPLIT, lmf, fd.scam, W, H,
-                                    fd.bgr, mlds, q, lmk.xyz, &frames[f].cam, task, done);
-    else
-      wave_tasks_screen<kScrUnroll>(__builtin_amdgcn_readfirstlane(wave), kW, particles * SPLIT, lmf, fd.scam, W, H,
-                                    fd.bgr, mglb, q, lmk.xyz, &frames[f].cam, task, done);
-#else
     for (int task = __builtin_amdgcn_readfirstlane(wave); task < particles * SPLIT; task += kW) {
       const int j = task / SPLIT;
       long long sum;
@@ -4794,7 +4796,6 @@ __global__ __launch_bounds__(NT) void k_score_pf(
         Pn[task] = cnt;
       }
     }
-#endif
     __syncthreads();
     MK_PTICK(2);
     const auto pose_of = [&](int t) -> const Xf& { return Pc[t]; };
@@ -5113,25 +5114,6 @@ __global__ __launch_bounds__(NT) void k_score_final(
   // tasks = (shift, half of the landmarks): 162 one-trip tasks over the waves
   // instead of 81 two-trip ones (the last round of whole hypotheses kept one
   // wave busy); the halves' integer sums combine exactly
-#if MK_SCORE_PIPE2
-  wave_tasks_screen<kScrUnroll>(
-      __builtin_amdgcn_readfirstlane(wave), NT / 64, 2 * NS, lmf, fd.scam, W, H, fd.bgr, mask, q, lmk.xyz,
-      &frames[f].cam,
-      [&](int t, PoseF& Pp, int& lb, int& le, int& tag, const Xf*& Tx) {
-        const int j = t >> 1, h = t & 1;
-        Pp = posef_from(P[j].c2w);
-        lb = nl * h / 2;
-        le = nl * (h + 1) / 2;
-        tag = j;
-        Tx = &P[j].c2w;
-      },
-      [&](int t, long long sum, int cnt) {
-        if (lane == 0) {
-          atomicAdd(&hs[t >> 1], (unsigned long long)sum);
-          atomicAdd(&hn[t >> 1], cnt);
-        }
-      });
-#else
   static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
   WaveLms<kScrUnroll> wl;
   wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
@@ -5145,7 +5127,6 @@ __global__ __launch_bounds__(NT) void k_score_final(
       atomicAdd(&hn[j], n);
     }
   }
-#endif
   __syncthreads();
   MK_STICK(0);
   block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return P[t].c2w; },
@@ -5222,14 +5203,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   MK_STICK(3);
   const double* green = lmk.xyz + 3 * (lmk.nw + lmk.nr);
   __shared__ double yset_err[80];
-#ifdef MK_DIAG_NO_COLOR  // timing diagnostic only: wrong results
-  if (tid < 80) yset_err[tid] = 1.0 + tid;
-  __syncthreads();
-#else
-#ifndef MK_COLOR_WAVE
-#define MK_COLOR_WAVE 0
-#endif
-  if (!MK_COLOR_WAVE && 80 * lmk.ng <= kColorPairs) {
+  if (80 * lmk.ng <= kColorPairs) {
     block_score_color<NT>([&](int h) -> const Xf& { return P[h].c2w; }, 80, green, lmk.ng, fd.cam, fd.bgr, W, H,
                           &cpairs, yset_err
 #if defined(MK_SCORE_TICKS) && MK_SCORE_TICKS == 3
@@ -5246,7 +5220,6 @@ __global__ __launch_bounds__(NT) void k_score_final(
     }
     __syncthreads();
   }
-#endif
   MK_STICK(4);
   if (tid == 0) {
     double best_error = DBL_MAX;

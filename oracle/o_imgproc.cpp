@@ -102,6 +102,14 @@ Img8 canny(const Img8& g, int low, int high) {
         MP(x, y) = 0;
       }
     }
+  return hysteresis_walk(map, W, H, stack);
+}
+
+// cv::Canny's hysteresis: from every strong pixel on the stack, the 8-neighbours
+// still marked candidate (0) become edges (2) and are pushed in turn
+// (OpenCV imgproc canny.cpp, the CANNY_POP loop); map is (W+2) x (H+2) with a ring of 1
+Img8 hysteresis_walk(std::vector<uint8_t>& map, int W, int H, std::vector<std::pair<int, int>>& stack) {
+  auto MP = [&](int x, int y) -> uint8_t& { return map[(size_t)(y + 1) * (W + 2) + (x + 1)]; };
   while (!stack.empty()) {
     auto [x, y] = stack.back();
     stack.pop_back();
@@ -116,6 +124,25 @@ Img8 canny(const Img8& g, int low, int high) {
   for (int y = 0; y < H; y++)
     for (int x = 0; x < W; x++) o.at(x, y) = MP(x, y) == 2 ? 255 : 0;
   return o;
+}
+
+// the same walk on a class plane (0 none, 1 weak candidate, 2 strong), pushed in raster order
+Img8 hysteresis(const Img8& cls) {
+  const int W = cls.w, H = cls.h;
+  std::vector<uint8_t> map((size_t)(W + 2) * (H + 2), 1);
+  std::vector<std::pair<int, int>> stack;
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      const uint8_t v = cls.at(x, y);
+      uint8_t& m = map[(size_t)(y + 1) * (W + 2) + (x + 1)];
+      if (v == 2) {
+        m = 2;
+        stack.push_back({x, y});
+      } else {
+        m = v == 1 ? 0 : 1;
+      }
+    }
+  return hysteresis_walk(map, W, H, stack);
 }
 
 static Img8 morph_rect(const Img8& s, int r, bool dil) {

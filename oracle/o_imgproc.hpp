@@ -39,6 +39,9 @@ Img8 gauss3x3(const Img8& src);
 // Canny with 3x3 Sobel (REPLICATE), L1 magnitude, TG22 NMS, hysteresis.
 // Pixels outside the image have magnitude 0, so border pixels may be edges.
 Img8 canny(const Img8& gray, int low, int high);
+// cv::Canny's hysteresis alone on a class plane (0 none, 1 weak candidate, 2 strong)
+Img8 hysteresis(const Img8& cls);
+Img8 hysteresis_walk(std::vector<uint8_t>& map, int W, int H, std::vector<std::pair<int, int>>& stack);
 // Morphology with a (2r+1)x(2r+1) rectangle; the border never contributes
 // (default DBL_MAX border and BORDER_REPLICATE are equivalent for rect max/min).
 Img8 dilate_rect(const Img8& src, int r);

@@ -551,6 +551,12 @@ void orc_canny(const uint8_t* bgr, int32_t w, int32_t h, int32_t step, uint8_t* 
   Img8 c = orc::canny(gauss3x3(bgr2gray(bgr, w, h, step)), CANNY_LOW, 3 * CANNY_LOW);
   std::memcpy(out, c.d.data(), c.d.size());
 }
+void orc_hysteresis(const uint8_t* cls, int32_t w, int32_t h, uint8_t* out) {
+  Img8 c(w, h);
+  std::memcpy(c.d.data(), cls, c.d.size());
+  Img8 e = orc::hysteresis(c);
+  std::memcpy(out, e.d.data(), e.d.size());
+}
 void orc_detector_binary(const uint8_t* canny, int32_t w, int32_t h, uint8_t* out) {
   Img8 c(w, h);
   std::memcpy(c.d.data(), canny, c.d.size());

@@ -63,6 +63,7 @@ int32_t orc_process_frame(orc_ctx* c, const uint8_t* bgr, int32_t w, int32_t h, 
 void orc_gray(const uint8_t* bgr, int32_t w, int32_t h, int32_t step, uint8_t* out);
 void orc_blur(const uint8_t* gray, int32_t w, int32_t h, uint8_t* out);
 void orc_canny(const uint8_t* bgr, int32_t w, int32_t h, int32_t step, uint8_t* out); /* gray+blur+Canny(50,150) */
+void orc_hysteresis(const uint8_t* cls, int32_t w, int32_t h, uint8_t* out);          /* Canny's hysteresis walk on 0/1/2 classes */
 void orc_detector_binary(const uint8_t* canny, int32_t w, int32_t h, uint8_t* out);   /* dilate x2, erode x1 */
 void orc_clean_mask(const uint8_t* canny, int32_t w, int32_t h, uint8_t* mask);       /* cleanImageByEdge mask */
 /* LIST/CCOMP contours: writes points (x,y pairs) and per-contour [offset,count,is_hole]; returns #contours or -1 */

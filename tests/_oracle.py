@@ -137,6 +137,15 @@ def canny(bgr):
     return out
 
 
+def hysteresis(cls):
+    """cv::Canny's hysteresis walk on a class plane (0 none, 1 weak candidate, 2 strong)."""
+    cls = np.ascontiguousarray(cls, np.uint8)
+    h, w = cls.shape
+    out = np.zeros((h, w), np.uint8)
+    lib().orc_hysteresis(_p(cls, C.c_uint8), C.c_int32(w), C.c_int32(h), _p(out, C.c_uint8))
+    return out
+
+
 def gray(bgr):
     h, w = bgr.shape[:2]
     out = np.zeros((h, w), np.uint8)

@@ -449,6 +449,55 @@ def test_full_pipeline_matches_oracle(mantis, frames, landmark_map):
     assert mantis.rng_state == orc.rng_state, "cv::RNG stream must advance exactly as the reference's"
 
 
+def test_small_batch_objpose_queue_settings(frames, landmark_map):
+    """The rig-latency ObjPose queues (k_objpose_q: RPP.cpp:66-208's ObjPose as a
+    job queue) at every public setting of MANTIS_OP_LANES_SMALL (jobs per wave)
+    x MANTIS_OP_ROUNDS_SMALL (tail-compaction rounds): one 4-camera rig, every
+    camera result and frame record byte-identical to the default context's, and
+    the one-job-per-wave single-round setting against the oracle. Round 4's
+    job-duplication failure (non-reserved lanes took jobs) lived on this path."""
+    import mantis_amd as M
+
+    K, D = synth.intrinsics()
+    imgs = [M.make_image(fr[0], K, D) for fr in frames[:4]]
+
+    def run(env):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            m = M.Mantis(max_cams=4, max_width=1280, max_height=720)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+        try:
+            assert M.lib().mantis_small_batch_frames(m.h) >= 4
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+            rig, cams = m.process(imgs, rigs=1)
+            return (bytes(rig[0]), [bytes(c) for c in cams], [bytes(m.frame_debug(f)) for f in range(4)],
+                    m.rng_state, [m.frame_debug(f) for f in range(4)])
+        finally:
+            m.close()
+
+    ref = run({})
+    for lanes in ("1", "4", "64"):
+        for rounds in ("1", "6"):
+            got = run({"MANTIS_OP_LANES_SMALL": lanes, "MANTIS_OP_ROUNDS_SMALL": rounds})
+            tag = f"lanes {lanes} rounds {rounds}"
+            assert got[0] == ref[0], f"{tag}: rig result differs"
+            for f in range(4):
+                assert got[1][f] == ref[1][f], f"{tag}: camera {f} result differs"
+                assert got[2][f] == ref[2][f], f"{tag}: camera {f} frame record differs"
+            assert got[3] == ref[3], f"{tag}: cv::RNG state differs"
+            if lanes == "1" and rounds == "1":
+                orc = O.Oracle(*landmark_map, seed=1)
+                for f, fr in enumerate(frames[:4]):
+                    _cmp_debug(got[4][f], orc.process(fr[0], K, D), f"{tag} frame {f}")
+
+
 def test_throughput_mode_kernels_match_latency_mode(frames, landmark_map):
     """Large batches take other kernel shapes (border walks from L2 instead of an
     LDS copy of the bit plane, 256-thread contour blocks): force them on a small

@@ -825,13 +825,17 @@ def _debug_valid(d):
     return out
 
 
-def test_throughput_and_latency_kernel_paths_agree(landmark_map):
+@pytest.mark.parametrize("iters", [10, 0])
+def test_throughput_and_latency_kernel_paths_agree(landmark_map, iters):
     """Batches above CUs / 4 frames take the throughput kernels (strip Canny,
     the morphology walker that numbers the runs, the L2 border walks, 256-thread
-    contour blocks); one rig at a time takes the latency ones (tile Canny,
-    segmented walker + run kernels, LDS border walks, 1024-thread contour
+    contour blocks, one particle-filter block per frame); one rig at a time
+    takes the latency ones (tile Canny, segmented walker + run kernels, LDS
+    border walks, 1024-thread contour blocks, the filter's iterations split over
     blocks), which the oracle tests cover. The same 72 rendered frames through
-    both: every camera result, frame record and the cv::RNG state bit-identical."""
+    both: every camera result, frame record and the cv::RNG state bit-identical.
+    iterations = 0 (no filter iteration: the one-block kernel's end-of-filter
+    writes on both paths) as well as the default 10."""
     import mantis_amd as M
 
     W, H, CAMS, RIGS = 1280, 720, 4, 18
@@ -844,8 +848,8 @@ def test_throughput_and_latency_kernel_paths_agree(landmark_map):
         for c in range(CAMS):
             Twc = Twb @ ext[c]
             cams.append(synth.make_cam(Twc[:3, :3], Twc[:3, 3], W, H))
-    mb = M.Mantis(max_cams=RIGS * CAMS, max_width=W, max_height=H)
-    ms = M.Mantis(max_cams=CAMS, max_width=W, max_height=H)
+    mb = M.Mantis(max_cams=RIGS * CAMS, max_width=W, max_height=H, iterations=iters)
+    ms = M.Mantis(max_cams=CAMS, max_width=W, max_height=H, iterations=iters)
     try:
         assert RIGS * CAMS > M.lib().mantis_small_batch_frames(mb.h)
         for m in (mb, ms):

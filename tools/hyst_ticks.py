@@ -3,6 +3,9 @@
 median / p90 of each phase over the frames (wall clock: the block shares its
 CU with others, so the phases' shares matter more than their sums).
 Phases: planes to LDS, run counts + row bases, run extents + label init, row unions, finds + band flags, global writes + lists (the edge-word store after them is not timed).
+With k_hyst_rec (the default path) the six values are instead: seam rounds,
+most sweeps of one band, sweeps of all bands, row fills of all bands, first
+settle and whole-kernel ticks.
 usage: MANTIS_AMD_LIB=abvar/hticks.so python tools/hyst_ticks.py [rigs]"""
 import os
 import sys
@@ -39,6 +42,14 @@ def main(rigs):
                          width=W, height=H) for i in range(n)]
     m.process(imgs, rigs=rigs)
     m.process(imgs, rigs=rigs)
+    if os.environ.get("MANTIS_HYST_REC", "1") != "0":
+        v = np.array([m.frame_counters(i)[10:16] for i in range(n)], np.float64)
+        names = ["seam rounds", "max sweeps/band", "sweeps (all)", "row fills", "settle us", "total us"]
+        v[:, 4:] *= 0.01
+        for j, nm in enumerate(names):
+            print(f"{nm:16s} median {np.median(v[:, j]):9.1f}  p90 {np.percentile(v[:, j], 90):9.1f}  max {v[:, j].max():9.1f}")
+        m.close()
+        return
     tk = []
     for i in range(n):
         fc = m.frame_counters(i)
