@@ -996,6 +996,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
+  // tests: start the run CCL's mark epoch near its wrap (4..255; the flag plane is cleared at the wrap)
+  if (const char* e = std::getenv("MANTIS_HYST_EPOCH0")) c->hyst_epoch = std::max(3, std::min(255, std::atoi(e)));
   c->F = cfg.max_cams;
   c->Wmax = cfg.max_width;
   c->Hmax = cfg.max_height;

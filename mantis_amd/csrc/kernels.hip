@@ -1716,7 +1716,7 @@ __global__ __launch_bounds__(MB_THREADS) void k_morph(const uint32_t* __restrict
   const int nr = ye - yb;
   for (int k = t; k < nr * WW; k += nt) {
     const int w = k / nr, y = yb + (k - w * nr);
-    M[bits::tiled_word(y, w, WW)] = A[(y - y0) * WW + w];
+    M[bits::tiled_word(y, w, bits::tiled_rows(H))] = A[(y - y0) * WW + w];
   }
 }
 
@@ -1809,7 +1809,7 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   const int lane = threadIdx.x & 63;
   const int f = gw / nseg, sg = gw - f * nseg;
   const int ys = sg * seg_rows, ye = min(H, ys + seg_rows);
-  const int WW = bits::words(W), wpw = dbits_wpw(W + 2);
+  const int WW = bits::words(W), wpw = dbits_wpw(W + 2), Hp = bits::tiled_rows(H);
   const uint32_t vm = lane < WW ? bits::valid(lane, W) : 0u;  // valid pixels of this lane's word
   const uint32_t* E = eb + (size_t)f * bstride;
   uint32_t* D = dbits + (size_t)f * dstride;
@@ -1898,8 +1898,8 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     s6.push2((a0 & vm) | ~vm, in(i - 21), (a1 & vm) | ~vm, in(i - 20), b0, b1);
     s7.push2((b0 & vm) | ~vm, in(i - 26), (b1 & vm) | ~vm, in(i - 25), a0, a1);
     const int y = i - MB_HALO;
-    if (y >= ys && y < ye && lane < WW) M[bits::tiled_word(y, lane, WW)] = a0 & vm;
-    if (y + 1 >= ys && y + 1 < ye && lane < WW) M[bits::tiled_word(y + 1, lane, WW)] = a1 & vm;
+    if (y >= ys && y < ye && lane < WW) M[bits::tiled_word(y, lane, Hp)] = a0 & vm;
+    if (y + 1 >= ys && y + 1 < ye && lane < WW) M[bits::tiled_word(y + 1, lane, Hp)] = a1 & vm;
   }
   if (RUNS) {
     emit_runs(0u, H + 1);
@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(256) void k_bits_to_bytes(const uint32_t* __restric
   const int WW = wpw > 0 ? wpw : bits::words(W);
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < W * H; k += gridDim.x * blockDim.x) {
     const int y = k / W, x = k - y * W;
-    const size_t i = wpw < 0 ? bits::tiled_word(y, x >> 5, WW) : (size_t)y * WW + (x >> 5);
+    const size_t i = wpw < 0 ? bits::tiled_word(y, x >> 5, bits::tiled_rows(H)) : (size_t)y * WW + (x >> 5);
     out[k] = (uint8_t)((src[i] >> (x & 31)) & 1u);
   }
 }
@@ -4026,17 +4026,18 @@ struct MaskBytes {
 // beside the kernel's static LDS: a 720p plane is 115 KB): ds_read lookups
 // instead of mask-word gathers through the L1
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
-__device__ inline int tiled_word32(int y, int w, int WW) { return (((y >> 5) * WW + w) << 5) + (y & 31); }
+// lookups of word (y, x >> 5) of the tiled plane (bits::tiled_word) in 32-bit
+// arithmetic: x, y >= 0 and a plane holds < 2^31 words
 struct MaskLds {
   lds_cu32* m;
-  int WW;
-  __device__ uint32_t word(int, int x, int y) const { return m[tiled_word32(y, x >> 5, WW)]; }
+  int Hp;  // bits::tiled_rows(H)
+  __device__ uint32_t word(int, int x, int y) const { return m[(x >> 5) * Hp + y]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 struct MaskBits {
   const uint32_t* m;
-  int WW, W;
-  __device__ uint32_t word(int, int x, int y) const { return m[tiled_word32(y, x >> 5, WW)]; }
+  int Hp, W;
+  __device__ uint32_t word(int, int x, int y) const { return m[(x >> 5) * Hp + y]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 // B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
@@ -4379,7 +4380,6 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
                                           int H, const uint8_t* bgr, const MK& mask, UQueue q, int tag, const Xf* Tx,
                                           const double* lmd, const Cam* cmp, long long& s_out, int& n_out) {
   const int lane = threadIdx.x & 63;
-  const int last = W * H - 1;
   int s = 0, n = 0;  // per lane: <= 12 landmarks x 3 * 255^2, exact in int32
   for (int b0 = lb; b0 < le; b0 += 64 * U) {  // wave-uniform trips
     int st[U], lin[U], px[U], py[U];
@@ -4400,16 +4400,23 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
     uint32_t mw[U];
 #pragma unroll
     for (int k = 0; k < U; k++) mw[k] = mask.word(lin[k], px[k], py[k]);
+    // a hit's pixel is interior (lin >= W + 1), so the dword one byte before
+    // it (the previous pixel's R, then B, G, R) is inside the buffer for every
+    // pixel, the frame's last included: one load form, the value >> 8
     uint32_t pv[U];
     int hm[U];
 #pragma unroll
     for (int k = 0; k < U; k++) {
       const bool hit = st[k] == SCR_IN && mask.test(mw[k], px[k]);
       hm[k] = hit ? -1 : 0;
-      const int off = hit ? 3 * lin[k] - (lin[k] == last ? 1 : 0) : 0;
+      const uint32_t off = hit ? 3u * (uint32_t)lin[k] - 1u : 0u;  // 32-bit offset from the scalar base
       typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
-      pv[k] = *(gu32u*)(bgr + off);
+      pv[k] = *(gu32u*)(gbytes(bgr) + off);
     }
+    // every load issued, none sunk into a branch behind its mask test: the U
+    // loads of a lane stay in flight together
+#pragma unroll
+    for (int k = 0; k < U; k++) asm volatile("" : "+v"(pv[k]));
     // the terms as masks, not selects: every loaded value is consumed, so the
     // compiler keeps the U loads unconditional (in flight together) instead
     // of sinking each into a branch with its own wait
@@ -4417,8 +4424,7 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
 #pragma unroll
     for (int k = 0; k < U; k++) {
       cu += st[k] == SCR_UNSURE;
-      const uint32_t v = lin[k] == last ? pv[k] >> 8 : pv[k];
-      const uint32_t d = ~v & 0xffffffu;  // 255 - B, 255 - G, 255 - R as bytes
+      const uint32_t d = ~(pv[k] >> 8) & 0xffffffu;  // 255 - B, 255 - G, 255 - R as bytes
       const int term = (int)__builtin_amdgcn_udot4(d, d, 0u, false);  // sum of their squares (v_dot4_u32_u8)
       constexpr int kBlack = 3 * 255 * 255;  // masked out
       const int e = kBlack ^ ((term ^ kBlack) & hm[k]);
@@ -4574,7 +4580,7 @@ __global__ __launch_bounds__(NT) void k_score_init(
   }
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
   mantis_cam_result& R = res[f];
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
@@ -4762,8 +4768,8 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   MK_PTICK(0);
   const float* gs = gauss + st[f].gauss_offset;
   const UQueue q{uqe, &uqn, kPfQueue};
-  const MaskLds mlds{(lds_cu32*)pf_mask, bits::words(W)};
-  const MaskBits mglb{fm, bits::words(W), W};
+  const MaskLds mlds{(lds_cu32*)pf_mask, bits::tiled_rows(H)};
+  const MaskBits mglb{fm, bits::tiled_rows(H), W};
   // a wave's tasks are (particle, slice wave % SPLIT): its slice of the
   // landmarks stays in registers for every task and iteration
   static_assert(kW % SPLIT == 0 && 64 * kScrUnroll * SPLIT >= 768, "one register trip per slice");
@@ -4902,7 +4908,7 @@ __global__ __launch_bounds__(NT) void k_score_pf_part(
   if (tid == 0) uqn = 0;
   __syncthreads();
   const UQueue q{uqe, &uqn, kPfQueue};
-  const MaskBits mglb{mbits + (size_t)f * bstride, bits::words(W), W};
+  const MaskBits mglb{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
   static_assert(kW % SPLIT == 0 && 64 * kScrUnroll * SPLIT >= 768, "one register trip per slice");
   WaveLms<kScrUnroll> wl;
   {
@@ -5005,7 +5011,7 @@ __global__ __launch_bounds__(NT) void k_score_shift_part(
   if (!st[f].reaches_pf) return;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   constexpr int NS = 81, kMaxSpb = NT / 128 > 0 ? NT / 128 : 1;  // shifts per block: two tasks each, one per wave
   __shared__ float4 lmf[768];
@@ -5065,7 +5071,7 @@ __global__ __launch_bounds__(NT) void k_score_final(
   if (!st[f].reaches_pf) return;
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const MaskBits mask{mbits + (size_t)f * bstride, bits::words(W), W};
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
   mantis_cam_result& R = res[f];
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;

@@ -17,11 +17,13 @@ namespace bits {
 
 MK_HD int words(int W) { return (W + 31) >> 5; }
 // Tiled mask plane (the scorers' cleanImageByEdge mask): word (y, w) -- 32
-// pixels of row y -- at ((y / 32) * WW + w) * 32 + y % 32, so one 128-byte
-// line holds a 32 x 32 pixel tile and a pixel neighbourhood touches a few
-// lines instead of one line per row. Rows padded to a multiple of 32.
-MK_HD size_t tiled_word(int y, int w, int WW) { return ((size_t)(y >> 5) * WW + w) * 32 + (y & 31); }
-MK_HD size_t tiled_words(int W, int H) { return (size_t)words(W) * (((size_t)H + 31) & ~(size_t)31); }
+// pixels of row y -- at w * Hp + y, word columns of Hp = H rounded up to 32
+// rows, so one 128-byte line holds a 32 x 32 pixel tile and a pixel
+// neighbourhood touches a few lines instead of one line per row; a lookup is
+// (x >> 5) * Hp + y (one multiply-add, no 64-bit index).
+MK_HD int tiled_rows(int H) { return (H + 31) & ~31; }
+MK_HD size_t tiled_word(int y, int w, int Hp) { return (size_t)w * Hp + y; }
+MK_HD size_t tiled_words(int W, int H) { return (size_t)words(W) * tiled_rows(H); }
 
 // mask of the valid pixels of word w
 MK_HD uint32_t valid(int w, int W) {

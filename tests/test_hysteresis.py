@@ -140,3 +140,40 @@ def test_hysteresis_device_paths_match_oracle(rec):
             assert len(bad) == 0, f"{name} (MANTIS_HYST_REC={rec}): {len(bad)} px differ, first {bad[:8].tolist()}"
     finally:
         m.close()
+
+
+@pytest.mark.gpu
+def test_ccl_epoch_wrap_stays_bit_exact():
+    """The run CCL marks strong seam components with a per-call epoch byte and
+    clears its flag plane only when the epoch wraps (255 -> 4): start the epoch
+    at 252 (MANTIS_HYST_EPOCH0) and run the CCL path across the wrap on frames
+    whose components reach band seams, each call bit-exact against the oracle
+    (the wrap was never reached by a test)."""
+    import mantis_amd as M
+    from mantis_amd import synth
+
+    env = {"MANTIS_HYST_REC": "0", "MANTIS_HYST_EPOCH0": "252"}
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        m = M.Mantis(max_cams=1, max_width=1280, max_height=720)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+    try:
+        rng = np.random.default_rng(99)
+        K, D = synth.intrinsics()
+        for call in range(8):  # epochs 253, 254, 255, 4 (plane cleared), 5, ...
+            base = rng.integers(0, 256, (720 // 6 + 2, 1280 // 6 + 2, 3)).astype(np.float64)
+            img = np.repeat(np.repeat(base, 6, 0), 6, 1)[:720, :1280]
+            img = np.clip(img + rng.normal(0, 20, img.shape), 0, 255).astype(np.uint8)
+            got = m.canny(M.make_image(img, K, D))
+            ref = O.canny(img)
+            assert np.array_equal(got, ref), f"call {call}: {np.count_nonzero(got != ref)} px differ"
+            cls = _cases()[call % 4][1]
+            assert np.array_equal(m.hysteresis(cls), O.hysteresis(cls)), f"call {call}: hysteresis stage differs"
+    finally:
+        m.close()
