@@ -147,6 +147,7 @@ struct Ctx {
   int morph_bh = 48;       // k_morph output rows per band (MB_BH, or MB_BH_NARROW at wide max_width)
   int morph_walk = 1 << 20;  // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
+  bool tiles_done = false;   // this batch's tiled detector plane was written by the walker
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
@@ -398,6 +399,11 @@ mantis_status stage_frames(Ctx* c, const mantis_image* cams, int n, int& W, int&
 }
 
 mantis_status run_hyst_ccl(Ctx* c, int n, int W, int H, bool edge_bytes);
+// border walks on an LDS copy of the padded plane (small batches) or on the tiled plane in L2
+bool trace_on_lds(const Ctx* c, int n, int Wp, int Hp) {
+  const size_t tb_lds = (size_t)dbits_wpw(Wp) * Hp * sizeof(uint32_t);
+  return c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames;
+}
 mantis_status run_hysteresis(Ctx* c, int n, int W, int H, bool edge_bytes);
 
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
@@ -438,6 +444,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
 #endif
   c->runs_done = false;
+  c->tiles_done = false;
   if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 63) {
     // register walker: one wave per (frame, row segment); with one segment per
     // frame it also numbers the detector runs (k_run_count / scan / emit)
@@ -445,7 +452,11 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     // walk down a whole frame is ~1 ms of dependent steps)
     const int seg = n <= c->fc_small_frames ? c->morph_walk_small : c->morph_walk;
     const int nseg = (H + seg - 1) / seg, nwv = nseg * n;
-    const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st};
+    // the walker also writes the tiled plane when the L2 border walker will read it
+    const bool tiles = !trace_on_lds(c, n, W + 2, H + 2);
+    const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st,
+                      tiles ? (uint64_t*)c->d_tbits : nullptr, c->tstride};
+    c->tiles_done = tiles;
     if (nseg == 1) {
       k_morph_walk<true><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
                                                                       c->dstride, seg, nseg, nwv, wr);
@@ -530,13 +541,14 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   const size_t tb_lds = (size_t)dbits_wpw(Wp) * Hp * sizeof(uint32_t);
   k_seg_plan<<<n, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, c->d_borders,
                                   c->d_st, c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders, c->seg_m);
-  if (c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames) {
+  if (trace_on_lds(c, n, Wp, Hp)) {
     k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_scratch,
                                                    c->pool_cap, Wp, Hp, kMaxBorders, c->d_rowb, c->rstride, rx, P);
   } else {
     const int wpw = dbits_wpw(Wp);
-    k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, 32 * wpw * sizeof(uint32_t), c->s>>>(c->d_dbits, c->dstride, c->d_tbits,
-                                                                                  c->tstride, wpw, Hp);
+    if (!c->tiles_done)  // the morphology walker wrote them already
+      k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, 32 * wpw * sizeof(uint32_t), c->s>>>(c->d_dbits, c->dstride,
+                                                                                    c->d_tbits, c->tstride, wpw, Hp);
     k_trace_borders<<<n, 64 * MK_TB_WAVES, 0, c->s>>>(c->d_tbits, c->tstride, c->d_borders, c->d_st, c->d_scratch, c->pool_cap, Wp,
                                         kMaxBorders, c->d_rowb, c->rstride, rx, P);
   }

@@ -1799,6 +1799,12 @@ struct WalkRuns {
   int32_t* lab;
   size_t plane;
   FrameState* st;
+  // the same padded rows as the border walks' tiled plane (k_tile_bits' layout:
+  // the 64-bit window of words w, w + 1 of row py at ((py / 32) wpw + w) 32 +
+  // py % 32), written here instead of by a pass of its own; null: not needed
+  // (the LDS border walker of small batches reads the row-major plane)
+  uint64_t* tb;
+  size_t tstride;  // uint32 words per frame
 };
 template <bool RUNS>
 __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
@@ -1814,9 +1820,17 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   const uint32_t* E = eb + (size_t)f * bstride;
   uint32_t* D = dbits + (size_t)f * dstride;
   uint32_t* M = mbits + (size_t)f * bstride;
+  uint64_t* TB = wr.tb ? (uint64_t*)((uint32_t*)wr.tb + (size_t)f * wr.tstride) : nullptr;
+  // a padded row's word and the next lane's into the tiled plane
+  const auto tile = [&](uint32_t v, int py) {
+    const uint32_t nx = dpp_from_right(v);  // lanes past the row hold 0
+    if (TB && lane < wpw) TB[((size_t)(py >> 5) * wpw + lane) * 32 + (py & 31)] = (uint64_t)v | ((uint64_t)nx << 32);
+  };
   // padded detector ring rows (zero) by the first / last segment
   if (sg == 0 && lane < wpw) D[lane] = 0u;
   if (ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
+  if (sg == 0) tile(0u, 0);
+  if (ye == H) tile(0u, H + 1);
   int32_t* RB = RUNS ? wr.rowb + (size_t)f * wr.rstride : nullptr;
   uint16_t* RX = RUNS ? wr.rx + (size_t)f * wr.plane : nullptr;
   int32_t* RL = RUNS ? wr.lab + (size_t)f * wr.plane : nullptr;
@@ -1882,10 +1896,12 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
       const uint32_t v0 = lane < wpw ? (b0 << 1) | (p0 >> 31) : 0u, v1 = lane < wpw ? (b1 << 1) | (p1 >> 31) : 0u;
       if (y >= ys && y < ye) {
         if (lane < wpw) D[(size_t)(y + 1) * wpw + lane] = v0;
+        tile(v0, y + 1);
         if (RUNS) emit_runs(v0, y + 1);
       }
       if (y + 1 >= ys && y + 1 < ye) {
         if (lane < wpw) D[(size_t)(y + 2) * wpw + lane] = v1;
+        tile(v1, y + 2);
         if (RUNS) emit_runs(v1, y + 2);
       }
     }

@@ -116,26 +116,33 @@ def test_detector_binary_and_mask_bit_exact(mantis, frames):
         assert np.array_equal(mask, ref_mask), f"clean mask differs: {np.count_nonzero(mask != ref_mask)} px"
 
 
-@pytest.mark.parametrize("walk", ["1048576", "180", "64", "7", "0"])
-def test_morphology_kernels_bit_exact(walk):
+@pytest.mark.parametrize("walk,trace_lds", [("1048576", None), ("180", None), ("64", None), ("7", None), ("0", None),
+                                             ("1048576", "0"), ("64", "0"), ("0", "0")])
+def test_morphology_kernels_bit_exact(walk, trace_lds):
     """Both morphology kernels (k_morph_walk: one wave per frame row segment,
     stage windows in registers, MANTIS_MORPH_WALK = segment rows; with one
     segment per frame it also numbers the detector runs for the contour CCL;
     k_morph: LDS bands, MANTIS_MORPH_WALK=0) against the oracle's detector
     binary and cleanImageByEdge mask, and the contours that follow against
     findContours: widths ending mid-word, segments shorter than the 29-row
-    reach, frames shorter than it, blob noise and i.i.d. noise."""
+    reach, frames shorter than it, blob noise and i.i.d. noise. With
+    MANTIS_TRACE_LDS_FRAMES=0 the borders are walked on the tiled plane in L2,
+    which the walker writes as it goes (round 5) and k_tile_bits after k_morph."""
     import mantis_amd as M
 
-    saved = os.environ.get("MANTIS_MORPH_WALK")
-    os.environ["MANTIS_MORPH_WALK"] = walk
+    env = {"MANTIS_MORPH_WALK": walk}
+    if trace_lds is not None:
+        env["MANTIS_TRACE_LDS_FRAMES"] = trace_lds
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         mt = M.Mantis(max_cams=1, max_width=1920, max_height=1080, max_contour_points=1 << 21)
     finally:
-        if saved is None:
-            os.environ.pop("MANTIS_MORPH_WALK")
-        else:
-            os.environ["MANTIS_MORPH_WALK"] = saved
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     rng = np.random.default_rng(17)
     K, D = synth.intrinsics()
     try:
