@@ -34,7 +34,9 @@
 //    (Horner with FMAs over theta^2 with one rounding, coefficients rounded to
 //    FP32: the cancellation in F is what M measures), charged
 //    crel = max(24, 1.25 (8 + 9 M)) u |u - cx|; the final add 0.5 u |u|,
-//    charged 2 u |u|.
+//    charged 2 u |u| <= 2 u (|u - cx| + |cx|): with the constant parts folded
+//    (round 5) eps = sens ez / |p| + (crel + 2u)(|du| + |dv|) + 16u sens +
+//    2u (|cx| + |cy|), five operations.
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -48,9 +50,12 @@ struct ScreenCam {
   float k[4];
   float sens;   // 2.2 * S px per radian (see above); +inf disables the screen (every landmark unsure)
   float crel;   // relative error charge of the scale chain, max(24, 1.25 (8 + 9 M)) u (see above)
-  float pad[2];
+  // the bound's constant parts folded (round 5): |u| <= |du| + |cx| turns
+  // crel (|du| + |dv|) + 2u (|u| + |v|) + sens 16u into
+  // c2 (|du| + |dv|) + e0, with c2 = crel + 2u and e0 = sens 16u + 2u (|cx| + |cy|), both rounded up
+  float c2, e0;
 };
-struct PoseF {   // c2w as FP32: rows of R, t, |t|_1
+struct PoseF {   // c2w as FP32: rows of R, t, and 6u |t|_1 (the pose's part of the camera-point bound ez)
   float R[9];
   float t[3];
   float tn;
@@ -64,7 +69,7 @@ MK_HD PoseF posef_from(const Xf& T) {
   PoseF p;
   for (int k = 0; k < 9; k++) p.R[k] = (float)T.R[k];
   for (int k = 0; k < 3; k++) p.t[k] = (float)T.t[k];
-  p.tn = (float)((fabs(T.t[0]) + fabs(T.t[1]) + fabs(T.t[2])) * 1.0000001);
+  p.tn = (float)((fabs(T.t[0]) + fabs(T.t[1]) + fabs(T.t[2])) * (6.0 * 5.9604644775390625e-8) * 1.000001);
   p.pad[0] = p.pad[1] = p.pad[2] = 0.f;
   return p;
 }
@@ -102,7 +107,7 @@ MK_HD ScrUV screen_uv(const PoseF& P, float X, float Y, float Z, float xn, const
   const float x = fmaf(P.R[0], X, fmaf(P.R[1], Y, fmaf(P.R[2], Z, P.t[0])));
   const float y = fmaf(P.R[3], X, fmaf(P.R[4], Y, fmaf(P.R[5], Z, P.t[1])));
   const float z = fmaf(P.R[6], X, fmaf(P.R[7], Y, fmaf(P.R[8], Z, P.t[2])));
-  const float ez = (6.0f * kScrU) * (xn + P.tn);
+  const float ez = xn + P.tn;  // 6u (|X|_1 + |t|_1), both parts pre-scaled (screen_landmark, posef_from)
   if (!(z > ez)) {
     r.state = z < -ez ? 0 : 2;
     return r;
@@ -125,8 +130,7 @@ MK_HD ScrUV screen_uv(const PoseF& P, float X, float Y, float Z, float xn, const
   const float du = c.fx * (x * sc), dv = c.fy * (y * sc);
   r.u = du + c.cx;
   r.v = dv + c.cy;
-  r.eps = fmaf(c.sens, fmaf(ez, rinv, 16.0f * kScrU),
-               fmaf(c.crel, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(r.u) + fabsf(r.v))));
+  r.eps = fmaf(c.sens * ez, rinv, fmaf(c.c2, fabsf(du) + fabsf(dv), c.e0));
   r.state = 1;
   return r;
 }
@@ -147,7 +151,7 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   const float x = fmaf(P.R[0], X, fmaf(P.R[1], Y, fmaf(P.R[2], Z, P.t[0])));
   const float y = fmaf(P.R[3], X, fmaf(P.R[4], Y, fmaf(P.R[5], Z, P.t[1])));
   const float z = fmaf(P.R[6], X, fmaf(P.R[7], Y, fmaf(P.R[8], Z, P.t[2])));
-  const float ez = (6.0f * kScrU) * (xn + P.tn);
+  const float ez = xn + P.tn;  // 6u (|X|_1 + |t|_1), both parts pre-scaled (screen_landmark, posef_from)
   const float rho2 = fmaf(x, x, y * y);
   const float z2 = z * z;
   const float rinv = scr_rsq(rho2 + z2);
@@ -162,12 +166,17 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   const float sc = thd * irho;
   const float du = c.fx * (x * sc), dv = c.fy * (y * sc);
   const float u = du + c.cx, v = dv + c.cy;
-  const float eps = fmaf(c.sens, fmaf(ez, rinv, 16.0f * kScrU),
-                         fmaf(c.crel, fabsf(du) + fabsf(dv), (2.0f * kScrU) * (fabsf(u) + fabsf(v))));
+  const float eps = fmaf(c.sens * ez, rinv, fmaf(c.c2, fabsf(du) + fabsf(dv), c.e0));
   // z certainly > 0, off the optical axis, and a bound below 1/4 px: the FP32
   // values are meaningful (NaN / inf fail every comparison)
   const bool valid = (int)(z > ez) & (int)(rho2 > 1e-12f * z2) & (int)(eps < 0.25f);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // v_cvt_i32_f32 is defined for every input (NaN -> 0, out of range saturates);
+  // a value that is not `valid` decides nothing below
+  const float ru = rintf(u), rv = rintf(v);
+#else
   const float ru = rintf(valid ? u : 0.f), rv = rintf(valid ? v : 0.f);  // (int) of NaN / huge is UB on the host
+#endif
   const int iu = (int)ru, iv = (int)rv;
   const bool round_ok = (int)(fabsf(u - ru) < 0.5f - eps) & (int)(fabsf(v - rv) < 0.5f - eps);
   const bool interior = (int)((unsigned)(iu - 1) < (unsigned)(W - 1)) & (int)((unsigned)(iv - 1) < (unsigned)(H - 1));
@@ -179,12 +188,13 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   return sure ? SCR_IN : (out ? SCR_OUT : SCR_UNSURE);
 }
 
-// landmark as the screen reads it: FP32 coordinates and |X|_1 rounded up
+// landmark as the screen reads it: FP32 coordinates and 6u |X|_1 rounded up
+// (the landmark's part of the camera-point bound ez)
 MK_HD void screen_landmark(const double* X, float* o) {
   o[0] = (float)X[0];
   o[1] = (float)X[1];
   o[2] = (float)X[2];
-  o[3] = (float)((fabs(X[0]) + fabs(X[1]) + fabs(X[2])) * 1.0000001);
+  o[3] = (float)((fabs(X[0]) + fabs(X[1]) + fabs(X[2])) * (6.0 * 5.9604644775390625e-8) * 1.000001);
 }
 
 // Host: the screen constants of a camera, from bounds derived over [0, pi/2]
@@ -236,7 +246,6 @@ MK_HD ScreenCam screen_cam_from(const Cam& cm) {
   ScreenCam s;
   s.fx = (float)cm.fx; s.fy = (float)cm.fy; s.cx = (float)cm.cx; s.cy = (float)cm.cy;
   for (int k = 0; k < 4; k++) s.k[k] = (float)cm.k[k];
-  s.pad[0] = s.pad[1] = 0.f;
   bool ok = cm.fx > 0 && cm.fy > 0 && cm.fx < 1e30 && cm.fy < 1e30;  // also false for NaN
   // the fp32 coefficients must reproduce theta_d closely: |k| bounded
   for (int k = 0; k < 4; k++) ok = ok && fabs(cm.k[k]) < 1.0;
@@ -245,6 +254,10 @@ MK_HD ScreenCam screen_cam_from(const Cam& cm) {
   const double f = fmax(cm.fx, cm.fy);
   s.sens = ok ? (float)(2.2 * b.S * f) : INFINITY;
   s.crel = (float)(fmax(24.0, 1.25 * (8.0 + 9.0 * b.M)) * 5.9604644775390625e-8);
+  const double u = 5.9604644775390625e-8;
+  s.c2 = (float)(((double)s.crel + 2 * u) * 1.000001);
+  s.e0 = ok ? (float)((16 * u * (double)s.sens + 2 * u * (fabs((double)s.cx) + fabs((double)s.cy))) * 1.000001)
+            : INFINITY;
   return s;
 }
 
