@@ -148,6 +148,7 @@ struct Ctx {
   int morph_walk = 1 << 20;  // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
   bool tiles_done = false;   // this batch's tiled detector plane was written by the walker
+  bool walk_tiles = false;   // MANTIS_WALK_TILES=1: the walker writes it (else k_tile_bits)
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
@@ -452,8 +453,11 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     // walk down a whole frame is ~1 ms of dependent steps)
     const int seg = n <= c->fc_small_frames ? c->morph_walk_small : c->morph_walk;
     const int nseg = (H + seg - 1) / seg, nwv = nseg * n;
-    // the walker also writes the tiled plane when the L2 border walker will read it
-    const bool tiles = !trace_on_lds(c, n, W + 2, H + 2);
+    // MANTIS_WALK_TILES=1: the walker also writes the tiled plane the L2 border
+    // walker reads (measured slower: morph 2.4 -> 3.8 ms per 4096 frames for
+    // border_trace 4.65 -> 4.3: its 8-byte scattered row stores cost more than
+    // k_tile_bits' staged pass)
+    const bool tiles = c->walk_tiles && !trace_on_lds(c, n, W + 2, H + 2);
     const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st,
                       tiles ? (uint64_t*)c->d_tbits : nullptr, c->tstride};
     c->tiles_done = tiles;
@@ -1008,6 +1012,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
+  if (const char* e = std::getenv("MANTIS_WALK_TILES")) c->walk_tiles = e[0] == '1';
   // tests: start the run CCL's mark epoch near its wrap (4..255; the flag plane is cleared at the wrap)
   if (const char* e = std::getenv("MANTIS_HYST_EPOCH0")) c->hyst_epoch = std::max(3, std::min(255, std::atoi(e)));
   c->F = cfg.max_cams;
