@@ -4630,9 +4630,14 @@ __global__ __launch_bounds__(NT) void k_score_init(
   const UQueue q{uqe, &uqn, kInitQueue};
   // tasks = (hypothesis, half of the landmarks), a wave's half in registers
   // (as in the particle filter and the shifts); the halves' sums add exactly
+  // the first kInitPoses hypotheses' screen poses staged in LDS once (a task
+  // then reads its pose from LDS instead of global memory)
+  constexpr int kInitPoses = 128;
+  __shared__ PoseF pfi[kInitPoses];
   for (int h = tid; h < C; h += NT) {
     hs[h] = 0;
     hn[h] = 0;
+    if (h < kInitPoses) pfi[h] = posef_from(Hh[h].c2w);
   }
   __syncthreads();
   static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
@@ -4642,7 +4647,8 @@ __global__ __launch_bounds__(NT) void k_score_init(
     const int h = t >> 1;
     long long s;
     int n;
-    wl.sums(posef_from(Hh[h].c2w), fd.scam, W, H, fd.bgr, mask, q, h, &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
+    const PoseF P = h < kInitPoses ? pfi[h] : posef_from(Hh[h].c2w);
+    wl.sums(P, fd.scam, W, H, fd.bgr, mask, q, h, &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
     if (lane == 0) {
       atomicAdd(&hs[h], (unsigned long long)s);
       atomicAdd(&hn[h], n);
@@ -5390,10 +5396,12 @@ __device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const
   __shared__ int32_t hn[HPB];
   __shared__ uint32_t uqe[kApiQueue];
   __shared__ int32_t uqn;
+  __shared__ PoseF pf[HPB];  // the block's poses as the screen reads them, staged once
   for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
   for (int i = tid; i < HPB; i += blockDim.x) {
     hs[i] = 0;
     hn[i] = 0;
+    if (i < nh) pf[i] = posef_from(*(const Xf*)(c2w + 12 * (size_t)(h0 + i)));
   }
   if (tid == 0) uqn = 0;
   __syncthreads();
@@ -5405,7 +5413,7 @@ __device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const
     const Xf* T = (const Xf*)(c2w + 12 * (size_t)(h0 + j));  // R[9], t[3] = mk::Xf
     long long s;
     int c;
-    wl.sums(posef_from(*T), fd.scam, fd.w, fd.h, fd.bgr, mask, q, j, T, lmk.xyz, cmp, s, c);
+    wl.sums(pf[j], fd.scam, fd.w, fd.h, fd.bgr, mask, q, j, T, lmk.xyz, cmp, s, c);
     if (lane == 0) {
       atomicAdd(&hs[j], (unsigned long long)s);
       atomicAdd(&hn[j], c);
