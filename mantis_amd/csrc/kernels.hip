@@ -370,14 +370,11 @@ __device__ inline void nms4(const int16_t* mag, const int16_t* gx_s, const int16
       const uint32_t DL = P[2][h], D = C[2][h], DR = P[2][h + 1];
       const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
       const uint32_t B = (HOR & R) | (~HOR & ((VER & D) | (~VER & ((NEG & DL) | (~NEG & DR)))));
+      // push = m > max(A, low, B - [HOR or VER]) (k_canny_strip's form)
       const s16x2 Ms = vpk<s16x2>(M);
-      const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
-      const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
-      const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
-      const uint32_t HV = HOR | VER;
-      const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
-      const uint32_t GTL = upk((LOW - Ms) >> 15);
-      push[h] = GTA & BC & GTL;
+      const s16x2 Bp = vpk<s16x2>(B) + vpk<s16x2>(HOR | VER);
+      const s16x2 T = __builtin_elementwise_max(__builtin_elementwise_max(vpk<s16x2>(A), LOW), Bp);
+      push[h] = upk((T - Ms) >> 15);
       strong[h] = push[h] & upk((HIGH - Ms) >> 15);
     }
     // nibbles: pixel 2h + j <-> bit j of half h's word
@@ -860,14 +857,13 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
       const uint32_t DLw = P[2][k][h], Dd = Cw[2][k][h], DRw = P[2][k][h + 1];
       const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
       const uint32_t B = (HOR & Rr) | (~HOR & ((VER & Dd) | (~VER & ((NEG & DLw) | (~NEG & DRw)))));
+      // push = m > A && m > low && (m >= B horizontally / vertically, m > B on
+      // the diagonals) = m > max(A, low, B - [HOR or VER]): one compare (the
+      // masks are 0 / -1 per half, so adding HOR | VER subtracts 1 there)
       const s16x2 Ms = vpk<s16x2>(Mm);
-      const uint32_t GTA = upk((vpk<s16x2>(A) - Ms) >> 15);
-      const uint32_t GTB = upk((vpk<s16x2>(B) - Ms) >> 15);
-      const uint32_t LTB = upk((Ms - vpk<s16x2>(B)) >> 15);
-      const uint32_t HV = HOR | VER;
-      const uint32_t BC = (HV & ~LTB) | (~HV & GTB);
-      const uint32_t GTL = upk((w.LOW - Ms) >> 15);
-      push[h] = GTA & BC & GTL;
+      const s16x2 Bp = vpk<s16x2>(B) + vpk<s16x2>(HOR | VER);
+      const s16x2 T = __builtin_elementwise_max(__builtin_elementwise_max(vpk<s16x2>(A), w.LOW), Bp);
+      push[h] = upk((T - Ms) >> 15);
       strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
     }
     // nibble of group k (pixel 2h + t <-> bit t of half h)
@@ -5382,7 +5378,10 @@ __global__ __launch_bounds__(256) void k_rig_weight(const FrameDesc* __restrict_
 // hypotheses, HPB = 16: many blocks) and the dense batch (thousands per
 // frame, HPB = 64: the landmark staging, barriers and drain shared by four
 // times as many). COLOR errors: one wave per hypothesis, exact FP64.
-constexpr int kApiHyps = 16, kApiQueue = 1024, kDenseHyps = 64;
+#ifndef MK_DENSE_HYPS
+#define MK_DENSE_HYPS 64
+#endif
+constexpr int kApiHyps = 16, kApiQueue = 1024, kDenseHyps = MK_DENSE_HYPS;
 template <int HPB, class MK>
 __device__ inline void score_api_fast(const FrameDesc& fd, const Cam* cmp, const MK& mask, Landmarks lmk,
                                       const double* c2w, int n, double* err, int32_t* nproj) {
