@@ -382,7 +382,8 @@ def run_config3(a, rk, cpu):
     from concurrent.futures import ThreadPoolExecutor
 
     pool = ThreadPoolExecutor(max_workers=nctx)
-    stage_ms, kern_ms = {}, {}
+    # per-context sums of the stage / kernel events over the timed steps
+    stage_ms_k, kern_ms_k = [{} for _ in range(nctx)], [{} for _ in range(nctx)]
 
     def run_steps(bs, k_steps, record=False):
         """k_steps steps: every context's host thread runs its share of each step
@@ -390,13 +391,13 @@ def run_config3(a, rk, cpu):
         def worker(k):
             for _ in range(k_steps):
                 bs[k].run()
-                if record and k == 0:
-                    for name, ms in m.kernel_times():  # "stage" or "stage/kernel" (hot stages: one event per kernel)
+                if record:
+                    for name, ms in ctxs[k].kernel_times():  # "stage" or "stage/kernel" (hot stages: one event per kernel)
                         st = name.split("/", 1)[0]
-                        stage_ms[st] = stage_ms.get(st, 0.0) + ms
+                        stage_ms_k[k][st] = stage_ms_k[k].get(st, 0.0) + ms
                         if "/" in name:
                             kn = name.split("/", 1)[1]
-                            kern_ms[kn] = kern_ms.get(kn, 0.0) + ms
+                            kern_ms_k[k][kn] = kern_ms_k[k].get(kn, 0.0) + ms
         for f in [pool.submit(worker, k) for k in range(len(bs))]:
             f.result()
 
@@ -408,10 +409,11 @@ def run_config3(a, rk, cpu):
 
     run_steps(batches, a.warmup)
 
-    # ---- timed region: stage / kernel events on context 0's stream; host CPU
-    # time of this process (every context's host thread, the cv::RNG draw
+    # ---- timed region: stage / kernel events on every context's stream; host
+    # CPU time of this process (every context's host thread, the cv::RNG draw
     # threads, the driver's) over the same region
-    m.set_profiling(True)
+    for mc in ctxs:
+        mc.set_profiling(True)
     barrier_sync()
     cpu0 = os.times()
     t0 = time.perf_counter()
@@ -420,7 +422,8 @@ def run_config3(a, rk, cpu):
     el_local = time.perf_counter() - t0
     cpu1 = os.times()
     elapsed = rk.max(el_local)
-    m.set_profiling(False)
+    for mc in ctxs:
+        mc.set_profiling(False)
     host_cpu_s = (cpu1.user - cpu0.user) + (cpu1.system - cpu0.system)
     value = a.rigs * a.steps * rk.world / elapsed
     ms_per_step = elapsed / a.steps * 1e3
@@ -443,13 +446,21 @@ def run_config3(a, rk, cpu):
     s_fast = LANDMARKS * fast_per_frame
     s_slow = 3700.0 * slow_per_frame
 
-    # ---- roofline of the dominant stage (per launch = per step on context 0).
+    # ---- roofline of the dominant stage (per launch = one context's step).
     # Durations are HIP events around each kernel of the stage on the stream it
     # is launched on (the hot stages are marked per kernel), averaged over the
-    # timed steps: dispatch to completion under the other contexts' load, what
-    # rocprofv3 reports per dispatch of the same command.
-    avg = {k: v / a.steps for k, v in stage_ms.items()}
-    kavg = {k: v / a.steps for k, v in kern_ms.items()}
+    # timed steps AND over every context: dispatch to completion under the other
+    # contexts' load, the average rocprofv3 reports over all dispatches of the
+    # same command. Context 0 alone is kept beside it: it submits first in every
+    # step and its launches finish up to 2.5x sooner than the later contexts'
+    # (profiles/r05_duration_sources.txt), which is how r04's line (context 0
+    # only) and rocprofv3 (all contexts) came to differ.
+    def mean_over_ctx(per):
+        keys = set().union(*per)
+        return {k: sum(d.get(k, 0.0) for d in per) / (len(per) * a.steps) for k in keys}
+    avg, kavg = mean_over_ctx(stage_ms_k), mean_over_ctx(kern_ms_k)
+    avg0 = {k: v / a.steps for k, v in stage_ms_k[0].items()}
+    kavg0 = {k: v / a.steps for k, v in kern_ms_k[0].items()}
     work = {
         # BGR read once; candidate and strong-root bit planes written
         "canny_nms": ("hbm", frames_step * (3 * W * H + W * H // 4)),
@@ -505,8 +516,11 @@ def run_config3(a, rk, cpu):
     if roof is not None:
         roof["stages_ms"] = {k: round(v, 4) for k, v in sorted(avg.items(), key=lambda kv: -kv[1])}
         roof["objpose_iterations_per_launch"] = iters
-        roof["duration_source"] = ("HIP events around each kernel of the stage on context 0's stream over the timed "
-                                   "steps (sum of kernels_ms)")
+        roof["duration_source"] = ("HIP events around each kernel of the stage on its context's stream, averaged over "
+                                   "the timed steps and all %d contexts (sum of kernels_ms; rocprofv3's per-dispatch "
+                                   "average of the same command); context0 = the first-submitting context alone" % nctx)
+        r0 = roofline(dom, avg0, kavg0)
+        roof["context0"] = {"avg_launch_ms": r0["avg_launch_ms"], "kernels_ms": r0["kernels_ms"], "frac": r0["frac"]}
     roof_front = roofline("canny_nms")
     # HBM traffic and VALU issue from PMC summaries of this same build
     # (tools/pmc_score.sh / tools/pmc_traffic.sh write lib_sha16): per launch =
@@ -531,7 +545,9 @@ def run_config3(a, rk, cpu):
             r["valu_instructions_per_launch"] = int(vi)
             # wave64 VALU instruction = 2 cycles on a SIMD-32 (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
             r["valu_issue_frac"] = round(vi * 2 / (1024 * 2.4e9 * r["avg_launch_ms"] * 1e-3), 4)
-        r["pmc_source"] = "profiles/r05_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step)"
+        r["pmc_source"] = ("profiles/r05_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step); "
+                           "the x2 is calibrated on gfx950 for every load width the stages issue (4 / 12 / 16 B "
+                           "coalesced, 4-B gathers) and WRITE_SIZE is 1x for full-line stores: profiles/r05_pmc_calib.txt")
 
     if roof is not None and dom == "score_pf_yaw":
         roof["bound_note"] = ("FP32 screen + exact FP64 fallback on the VALU, gathers from L2/MALL: frac counts the "

@@ -324,8 +324,11 @@ __device__ inline void sobel4v(const uint8_t* bl, int16_t* mag, int16_t* gx_s, i
 // difference (v_pk_sub + v_pk_ashr 15), the direction tests are the signs of
 // two 24-bit multiply-adds, the neighbour choice is v_bfi on the pairs. The
 // classes of a group go to cls (byte u: candidate nibble | strong nibble << 4).
-__device__ inline uint32_t sign_pair(int32_t lo, int32_t hi) {  // 0xffff per negative half
-  return __builtin_amdgcn_perm((uint32_t)(hi >> 31), (uint32_t)(lo >> 31), 0x05040100u);
+// 0xffff per negative half: v_perm_b32's selectors 9 / 11 replicate bit 31 of
+// its second / first operand into a byte, so one perm builds both halves
+// (tools/perm_sign_check.hip: identical to the two-shift form on 2^24 pairs)
+__device__ inline uint32_t sign_pair(int32_t lo, int32_t hi) {
+  return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x0B0B0909u);
 }
 __device__ inline void nms4(const int16_t* mag, const int16_t* gx_s, const int16_t* gy_s, int low, int high,
                             uint8_t* cls, int t) {
@@ -748,13 +751,16 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
 #pragma unroll
     for (int k = 0; k < K; k++) {
       const uint32_t aa = top ? R.hba[S][k] : R.hba[S1][k], ab = top ? R.hbb[S][k] : R.hbb[S1][k];  // row -1 = row 1
-      const uint32_t av[4] = {aa & 0xffffu, aa >> 16, ab & 0xffffu, ab >> 16};
-      const uint32_t bv[4] = {R.hba[S2][k] & 0xffffu, R.hba[S2][k] >> 16, R.hbb[S2][k] & 0xffffu, R.hbb[S2][k] >> 16};
-      const uint32_t cv[4] = {R.hba[S][k] & 0xffffu, R.hba[S][k] >> 16, R.hbb[S][k] & 0xffffu, R.hbb[S][k] >> 16};
+      // pixel b: 84 (a + c) + 89 m + 2^15 as three v_dot2_u32_u16 on the packed
+      // u16 pairs themselves, the other half's coefficient 0 (no unpacking)
+      const uint32_t A2[2] = {aa, ab}, B2[2] = {R.hba[S2][k], R.hbb[S2][k]}, C2[2] = {R.hba[S][k], R.hbb[S][k]};
       uint32_t o = 0;
 #pragma unroll
       for (int b = 0; b < 4; b++) {
-        const uint32_t r = (84u * (av[b] + cv[b]) + 89u * bv[b] + (1u << 15)) >> 16;
+        const u16x2 c84 = b & 1 ? u16x2{0, 84} : u16x2{84, 0}, c89 = b & 1 ? u16x2{0, 89} : u16x2{89, 0};
+        uint32_t r = __builtin_amdgcn_udot2(vpk<u16x2>(B2[b >> 1]), c89, 1u << 15, false);
+        r = __builtin_amdgcn_udot2(vpk<u16x2>(C2[b >> 1]), c84, r, false);
+        r = __builtin_amdgcn_udot2(vpk<u16x2>(A2[b >> 1]), c84, r, false) >> 16;
         o |= (r > 255u ? 255u : r) << (8 * b);
       }
       R.bl[S2][k] = o;

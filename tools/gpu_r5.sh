@@ -26,6 +26,7 @@ if [ "$PART" = "b" ]; then
   python3 tools/prof_summary.py $O/prof_default $O/rocprof_stats_default.md > /dev/null
   python3 tools/kern_avg.py $O/prof_default/run_kernel_trace.csv 40 $O/batch_launch_avg_default.json > $O/batch_launch_avg_default.txt
   python3 tools/trace_overlap.py $O/prof_default 18 > $O/trace_overlap_default.txt || true
+  python3 tools/dur_sources.py $O/prof_default $O/prof_default.log > $O/duration_sources.txt || true
   head -12 $O/batch_launch_avg_default.txt
   for leg in 2 5 4; do
     case $leg in
