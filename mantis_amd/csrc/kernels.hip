@@ -327,6 +327,12 @@ __device__ inline void sobel4v(const uint8_t* bl, int16_t* mag, int16_t* gx_s, i
 // 0xffff per negative half: v_perm_b32's selectors 9 / 11 replicate bit 31 of
 // its second / first operand into a byte, so one perm builds both halves
 // (tools/perm_sign_check.hip: identical to the two-shift form on 2^24 pairs)
+// a * b + c, a and b 24-bit signed (b wave-uniform): one v_mad_i32_i24
+__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c) {
+  int32_t r;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
 __device__ inline uint32_t sign_pair(int32_t lo, int32_t hi) {
   return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x0B0B0909u);
 }
@@ -366,7 +372,8 @@ __device__ inline void nms4(const int16_t* mag, const int16_t* gx_s, const int16
       // hor: ay 2^15 < ax TG22; ver: ay 2^15 > ax (TG22 + 2^16)
       const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
       const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
-      const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);  // gx gy < 0: the (up-right, down-left) diagonal
+      uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);  // gx gy < 0: the (up-right, down-left) diagonal
+      asm volatile("" : "+v"(NEG));  // keeps the selects v_bfi (k_canny_strip)
       // neighbour pairs of pixels (2h, 2h+1): left / centre / right columns of each row
       const uint32_t UL = P[0][h], U = C[0][h], UR = P[0][h + 1];
       const uint32_t L = P[1][h], M = C[1][h], R = P[1][h + 1];
@@ -656,7 +663,9 @@ struct StripRegs {
   uint32_t hba[3][K], hbb[3][K];  // horizontal blur, 2 u16 pairs per group
   uint32_t bl[3][K];              // blur, 4 bytes per group
   uint32_t mga[3][K], mgb[3][K];  // L1 magnitude, 2 i16 pairs per group
-  uint32_t gxa[3][K], gxb[3][K], gya[3][K], gyb[3][K];  // Sobel gx / gy
+  // |gx| with the sign of gx ^ gy in bit 15 of each half (NMS's diagonal
+  // choice), |gy|: what the NMS reads, so it takes no absolute values
+  uint32_t gxa[3][K], gxb[3][K], gya[3][K], gyb[3][K];
 };
 template <int K>
 struct StripWave {
@@ -666,6 +675,7 @@ struct StripWave {
   int H, WW, lane;
   bool left_edge, right_edge, inside, store_lane;
   s16x2 LOW, HIGH;
+  int KH, KV;  // -2 TG22, -2 (TG22 + 2^16) (v_mad_i32_i24 operands)
   uint32_t* cb;
   uint32_t* sbp;
   // BGR rows in flight (strip_pf): 1 = row i, 2 = rows i, i+1 (shifted down a
@@ -801,14 +811,14 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
       const s16x2 D2 = vpk<s16x2>(__builtin_amdgcn_perm(DR, vd23[k], 0x05040302u));
       const s16x2 gx01 = S1v - S0v, gx23 = S2v - S1v;
       const s16x2 gy01 = D0 + D1 + (vpk<s16x2>(vd01[k]) << 1), gy23 = D1 + D2 + (vpk<s16x2>(vd23[k]) << 1);
-      const s16x2 m01 = __builtin_elementwise_max(gx01, -gx01) + __builtin_elementwise_max(gy01, -gy01);
-      const s16x2 m23 = __builtin_elementwise_max(gx23, -gx23) + __builtin_elementwise_max(gy23, -gy23);
-      R.mga[S1][k] = upk(m01);
-      R.mgb[S1][k] = upk(m23);
-      R.gxa[S1][k] = upk(gx01);
-      R.gxb[S1][k] = upk(gx23);
-      R.gya[S1][k] = upk(gy01);
-      R.gyb[S1][k] = upk(gy23);
+      const s16x2 ax01 = __builtin_elementwise_max(gx01, -gx01), ay01 = __builtin_elementwise_max(gy01, -gy01);
+      const s16x2 ax23 = __builtin_elementwise_max(gx23, -gx23), ay23 = __builtin_elementwise_max(gy23, -gy23);
+      R.mga[S1][k] = upk(ax01 + ay01);
+      R.mgb[S1][k] = upk(ax23 + ay23);
+      R.gxa[S1][k] = upk(ax01) | ((upk(gx01) ^ upk(gy01)) & 0x80008000u);
+      R.gxb[S1][k] = upk(ax23) | ((upk(gx23) ^ upk(gy23)) & 0x80008000u);
+      R.gya[S1][k] = upk(ay01);
+      R.gyb[S1][k] = upk(ay23);
     }
   } else if (ROWS && m == H) {
 #pragma unroll
@@ -849,25 +859,30 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
     uint32_t push[2], strong[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const uint32_t gxp = h ? R.gxb[S][k] : R.gxa[S][k], gyp = h ? R.gyb[S][k] : R.gya[S][k];
-      const s16x2 X = vpk<s16x2>(gxp), Y = vpk<s16x2>(gyp);
-      const s16x2 AX = __builtin_elementwise_max(X, -X), AY = __builtin_elementwise_max(Y, -Y);
-      const uint32_t ax = upk(AX), ay = upk(AY);
-      const int ax0 = (int)(ax & 0xffffu), ax1 = (int)(ax >> 16);
-      const int ay0 = (int)(ay & 0xffffu) << SHIFT, ay1 = (int)(ay >> 16) << SHIFT;
-      const uint32_t HOR = sign_pair(ay0 - ax0 * TG22, ay1 - ax1 * TG22);
-      const uint32_t VER = sign_pair(ax0 * (TG22 + (1 << (SHIFT + 1))) - ay0, ax1 * (TG22 + (1 << (SHIFT + 1))) - ay1);
-      const uint32_t NEG = upk(vpk<s16x2>(gxp ^ gyp) >> 15);
+      const uint32_t axn = h ? R.gxb[S][k] : R.gxa[S][k], ay = h ? R.gyb[S][k] : R.gya[S][k];
+      const int ax0 = (int)(axn & 0x7fffu), ax1 = (int)((axn >> 16) & 0x7fffu);
+      // OpenCV's tests at twice the scale, each a single v_mad_i32_i24 per
+      // pixel: hor: ay 2^16 < ax 2 TG22; ver: ay 2^16 > ax 2 (TG22 + 2^16).
+      // VERN = ~ver but at gx = gy = 0, where m = 0 never pushes
+      const int ay0 = (int)(ay << 16), ay1 = (int)(ay & 0xffff0000u);
+      // (asm: left to itself the compiler derives VERN from HOR's product
+      // with a shift and a subtract per pixel)
+      const uint32_t HOR = sign_pair(mad24(ax0, w.KH, ay0), mad24(ax1, w.KH, ay1));
+      const uint32_t VERN = sign_pair(mad24(ax0, w.KV, ay0), mad24(ax1, w.KV, ay1));
+      uint32_t NEG = upk(vpk<s16x2>(axn) >> 15);
+      // opaque: seen as a sign mask, the selects below become per-half
+      // compares + v_cndmask + repacking (12 ops per half instead of 2 v_bfi)
+      asm volatile("" : "+v"(NEG));
       const uint32_t UL = P[0][k][h], U = Cw[0][k][h], UR = P[0][k][h + 1];
       const uint32_t L = P[1][k][h], Mm = Cw[1][k][h], Rr = P[1][k][h + 1];
       const uint32_t DLw = P[2][k][h], Dd = Cw[2][k][h], DRw = P[2][k][h + 1];
-      const uint32_t A = (HOR & L) | (~HOR & ((VER & U) | (~VER & ((NEG & UR) | (~NEG & UL)))));
-      const uint32_t B = (HOR & Rr) | (~HOR & ((VER & Dd) | (~VER & ((NEG & DLw) | (~NEG & DRw)))));
+      const uint32_t A = (HOR & L) | (~HOR & ((VERN & ((NEG & UR) | (~NEG & UL))) | (~VERN & U)));
+      const uint32_t B = (HOR & Rr) | (~HOR & ((VERN & ((NEG & DLw) | (~NEG & DRw))) | (~VERN & Dd)));
       // push = m > A && m > low && (m >= B horizontally / vertically, m > B on
       // the diagonals) = m > max(A, low, B - [HOR or VER]): one compare (the
       // masks are 0 / -1 per half, so adding HOR | VER subtracts 1 there)
       const s16x2 Ms = vpk<s16x2>(Mm);
-      const s16x2 Bp = vpk<s16x2>(B) + vpk<s16x2>(HOR | VER);
+      const s16x2 Bp = vpk<s16x2>(B) + vpk<s16x2>(HOR | ~VERN);
       const s16x2 T = __builtin_elementwise_max(__builtin_elementwise_max(vpk<s16x2>(A), w.LOW), Bp);
       push[h] = upk((T - Ms) >> 15);
       strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
@@ -949,6 +964,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 
   const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
   w.LOW = s16x2{(short)lowc, (short)lowc};
   w.HIGH = s16x2{(short)highc, (short)highc};
+  {
+    constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << 15) + 0.5);
+    w.KH = -2 * TG22;
+    w.KV = -(2 * TG22 + (1 << 17));
+  }
   w.bgr = fd.bgr;
   w.loff = (uint32_t)lc * 3u;
   w.rstep = (uint32_t)W * 3u;
