@@ -169,6 +169,19 @@ __device__ inline uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2) {
   return g(d0, LO, HI) | (g(p1, LO, HI) << 8) | (g(p2, LO, HI) << 16) | (g(d2, LO << 8, HI << 8) << 24);
 }
 
+// gray4 as two u16 pairs (pixels 0, 1 and 2, 3): each dot sum is gray << 14
+// plus a fraction under 2^14 and below 2^22, so (s << 2) holds gray in bits
+// 16..23 (k_canny_strip's horizontal blur takes u16 pairs: no byte packing)
+__device__ inline void gray4_pairs(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t& p01, uint32_t& p23) {
+  constexpr uint32_t LO = 0x0023914Cu, HI = 0x00132507u;
+  const uint32_t p1 = __builtin_amdgcn_perm(d1, d0, 0x0c050403u), p2 = __builtin_amdgcn_perm(d2, d1, 0x0c040302u);
+  const auto s = [](uint32_t p, uint32_t lo, uint32_t hi) {
+    return __builtin_amdgcn_udot4(p, lo, (__builtin_amdgcn_udot4(p, hi, 0u, false) << 8) + 8192u, false);
+  };
+  p01 = (s(d0, LO, HI) >> 14) | ((s(p1, LO, HI) << 2) & 0xffff0000u);
+  p23 = (s(p2, LO, HI) >> 14) | ((s(d2, LO << 8, HI << 8) << 2) & 0xffff0000u);
+}
+
 // Interior tiles, four horizontally adjacent pixels per work-item: every
 // stencil stage reads aligned dwords / qwords of LDS rows and writes one, so
 // the per-pixel byte gathers and index arithmetic of the generic path go. All
@@ -661,7 +674,7 @@ constexpr int strip_pf() { return K == 2 ? MK_CANNY_PF : 1; }
 template <int K>
 struct StripRegs {
   uint32_t hba[3][K], hbb[3][K];  // horizontal blur, 2 u16 pairs per group
-  uint32_t bl[3][K];              // blur, 4 bytes per group
+  uint32_t bla[3][K], blb[3][K];  // blur, 2 u16 pairs per group
   uint32_t mga[3][K], mgb[3][K];  // L1 magnitude, 2 i16 pairs per group
   // |gx| with the sign of gx ^ gy in bit 15 of each half (NMS's diagonal
   // choice), |gy|: what the NMS reads, so it takes no absolute values
@@ -676,6 +689,7 @@ struct StripWave {
   bool left_edge, right_edge, inside, store_lane;
   s16x2 LOW, HIGH;
   int KH, KV;  // -2 TG22, -2 (TG22 + 2^16) (v_mad_i32_i24 operands)
+  uint32_t TWO;  // (2, 2) in an SGPR the compiler cannot see through: x 2 + y stays one v_pk_mad
   uint32_t* cb;
   uint32_t* sbp;
   // BGR rows in flight (strip_pf): 1 = row i, 2 = rows i, i+1 (shifted down a
@@ -725,25 +739,29 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
   constexpr int S1 = (S + 1) % 3, S2 = (S + 2) % 3;  // slots of rows i-2 / i+1, i-1
   constexpr int SHIFT = 15;
   constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
-  const u16x2 c84 = {84, 84}, c89 = {89, 89}, two = {2, 2};
+  const u16x2 c84 = {84, 84}, c89 = {89, 89};
   const int H = w.H;
   // ---- gray and horizontal blur of input row i
   if (!ROWS || i < H) {
-    uint32_t g[K];
+    uint32_t g01[K], g23[K];  // gray as u16 pairs: pixels (0, 1), (2, 3) of each group
     {
       const uint32_t(&nx)[K][3] = strip_row<K, S>(w);
 #pragma unroll
-      for (int k = 0; k < K; k++) g[k] = gray4(nx[k][0], nx[k][1], nx[k][2]);
+      for (int k = 0; k < K; k++) gray4_pairs(nx[k][0], nx[k][1], nx[k][2], g01[k], g23[k]);
     }
     strip_advance<K, S>(w, i);
-    uint32_t gl = dpp_from_left(g[K - 1]), gr = dpp_from_right(g[0]);
-    if (EDGE && w.left_edge) gl = g[0] << 16;       // gray(-1) = gray(1)
-    if (EDGE && w.right_edge) gr = g[K - 1] >> 16;  // gray(W) = gray(W-2)
+    // the left group's (2, 3) pair, the right group's (0, 1) pair
+    uint32_t gl = dpp_from_left(g23[K - 1]), gr = dpp_from_right(g01[0]);
+    if (EDGE && w.left_edge) gl = g01[0];        // gray(-1) = gray(1): the high half
+    if (EDGE && w.right_edge) gr = g23[K - 1];   // gray(W) = gray(W-2): the low half
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const Taps4 tp = taps4(k ? g[k - 1] : gl, g[k], k + 1 < K ? g[k + 1] : gr);
-      const u16x2 o01 = (vpk<u16x2>(tp.l01) + vpk<u16x2>(tp.q01)) * c84 + vpk<u16x2>(tp.m01) * c89;
-      const u16x2 o23 = (vpk<u16x2>(tp.q01) + vpk<u16x2>(tp.q23)) * c84 + vpk<u16x2>(tp.m23) * c89;
+      const uint32_t l23 = k ? g23[k - 1] : gl, r01 = k + 1 < K ? g01[k + 1] : gr;
+      const u16x2 l01 = vpk<u16x2>(__builtin_amdgcn_perm(g01[k], l23, 0x05040302u));     // pixels -1, 0
+      const u16x2 q01 = vpk<u16x2>(__builtin_amdgcn_perm(g23[k], g01[k], 0x05040302u));  // 1, 2
+      const u16x2 q23 = vpk<u16x2>(__builtin_amdgcn_perm(r01, g23[k], 0x05040302u));     // 3, 4
+      const u16x2 o01 = (l01 + q01) * c84 + vpk<u16x2>(g01[k]) * c89;
+      const u16x2 o23 = (q01 + q23) * c84 + vpk<u16x2>(g23[k]) * c89;
       R.hba[S][k] = upk(o01);
       R.hbb[S][k] = upk(o23);
     }
@@ -764,20 +782,30 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
       // pixel b: 84 (a + c) + 89 m + 2^15 as three v_dot2_u32_u16 on the packed
       // u16 pairs themselves, the other half's coefficient 0 (no unpacking)
       const uint32_t A2[2] = {aa, ab}, B2[2] = {R.hba[S2][k], R.hbb[S2][k]}, C2[2] = {R.hba[S][k], R.hbb[S][k]};
-      uint32_t o = 0;
+      uint32_t o[2];
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const u16x2 c84 = b & 1 ? u16x2{0, 84} : u16x2{84, 0}, c89 = b & 1 ? u16x2{0, 89} : u16x2{89, 0};
-        uint32_t r = __builtin_amdgcn_udot2(vpk<u16x2>(B2[b >> 1]), c89, 1u << 15, false);
-        r = __builtin_amdgcn_udot2(vpk<u16x2>(C2[b >> 1]), c84, r, false);
-        r = __builtin_amdgcn_udot2(vpk<u16x2>(A2[b >> 1]), c84, r, false) >> 16;
-        o |= (r > 255u ? 255u : r) << (8 * b);
+      for (int p = 0; p < 2; p++) {
+        uint32_t r[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const u16x2 c84 = h ? u16x2{0, 84} : u16x2{84, 0}, c89 = h ? u16x2{0, 89} : u16x2{89, 0};
+          r[h] = __builtin_amdgcn_udot2(vpk<u16x2>(B2[p]), c89, 1u << 15, false);
+          r[h] = __builtin_amdgcn_udot2(vpk<u16x2>(C2[p]), c84, r[h], false);
+          r[h] = __builtin_amdgcn_udot2(vpk<u16x2>(A2[p]), c84, r[h], false);
+        }
+        // the high halves (sum >> 16, at most 257) as a u16 pair, clamped to 255
+        const u16x2 q = vpk<u16x2>(__builtin_amdgcn_perm(r[1], r[0], 0x07060302u));
+        o[p] = upk(__builtin_elementwise_min(q, (u16x2){255, 255}));
       }
-      R.bl[S2][k] = o;
+      R.bla[S2][k] = o[0];
+      R.blb[S2][k] = o[1];
     }
   } else if (ROWS && j == H) {
 #pragma unroll
-    for (int k = 0; k < K; k++) R.bl[S2][k] = R.bl[S1][k];  // row H = row H-1 (replicate), for the Sobel of row H-1
+    for (int k = 0; k < K; k++) {  // row H = row H-1 (replicate), for the Sobel of row H-1
+      R.bla[S2][k] = R.bla[S1][k];
+      R.blb[S2][k] = R.blb[S1][k];
+    }
   }
   // ---- Sobel of row m = i - 2 (blur rows m-1, m, m+1 = slots S, S1, S2)
   const int m = i - 2;
@@ -785,13 +813,12 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
     uint32_t vs01[K], vs23[K], vd01[K], vd23[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const uint32_t a = ROWS && m == 0 ? R.bl[S1][k] : R.bl[S][k];  // row -1 = row 0
-      const uint32_t b = R.bl[S1][k], c = R.bl[S2][k];
-      const u16x2 A01 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c010c00u)), A23 = vpk<u16x2>(__builtin_amdgcn_perm(a, a, 0x0c030c02u));
-      const u16x2 B01 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c010c00u)), B23 = vpk<u16x2>(__builtin_amdgcn_perm(b, b, 0x0c030c02u));
-      const u16x2 C01 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c010c00u)), C23 = vpk<u16x2>(__builtin_amdgcn_perm(c, c, 0x0c030c02u));
-      vs01[k] = upk(A01 + C01 + B01 * two);
-      vs23[k] = upk(A23 + C23 + B23 * two);
+      const bool top = ROWS && m == 0;  // row -1 = row 0
+      const u16x2 A01 = vpk<u16x2>(top ? R.bla[S1][k] : R.bla[S][k]), A23 = vpk<u16x2>(top ? R.blb[S1][k] : R.blb[S][k]);
+      const u16x2 B01 = vpk<u16x2>(R.bla[S1][k]), B23 = vpk<u16x2>(R.blb[S1][k]);
+      const u16x2 C01 = vpk<u16x2>(R.bla[S2][k]), C23 = vpk<u16x2>(R.blb[S2][k]);
+      vs01[k] = upk(B01 * vpk<u16x2>(w.TWO) + (A01 + C01));
+      vs23[k] = upk(B23 * vpk<u16x2>(w.TWO) + (A23 + C23));
       vd01[k] = upk(vpk<s16x2>(upk(C01)) - vpk<s16x2>(upk(A01)));
       vd23[k] = upk(vpk<s16x2>(upk(C23)) - vpk<s16x2>(upk(A23)));
     }
@@ -810,7 +837,8 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
       const s16x2 D1 = vpk<s16x2>(__builtin_amdgcn_perm(vd23[k], vd01[k], 0x05040302u));
       const s16x2 D2 = vpk<s16x2>(__builtin_amdgcn_perm(DR, vd23[k], 0x05040302u));
       const s16x2 gx01 = S1v - S0v, gx23 = S2v - S1v;
-      const s16x2 gy01 = D0 + D1 + (vpk<s16x2>(vd01[k]) << 1), gy23 = D1 + D2 + (vpk<s16x2>(vd23[k]) << 1);
+      const s16x2 gy01 = vpk<s16x2>(vd01[k]) * vpk<s16x2>(w.TWO) + (D0 + D1);
+      const s16x2 gy23 = vpk<s16x2>(vd23[k]) * vpk<s16x2>(w.TWO) + (D1 + D2);
       const s16x2 ax01 = __builtin_elementwise_max(gx01, -gx01), ay01 = __builtin_elementwise_max(gy01, -gy01);
       const s16x2 ax23 = __builtin_elementwise_max(gx23, -gx23), ay23 = __builtin_elementwise_max(gy23, -gy23);
       R.mga[S1][k] = upk(ax01 + ay01);
@@ -856,7 +884,7 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
   uint32_t cw = 0, sw = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    uint32_t push[2], strong[2];
+    uint32_t dp[2], ds[2];  // per half: sign bits = push / strong
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint32_t axn = h ? R.gxb[S][k] : R.gxa[S][k], ay = h ? R.gyb[S][k] : R.gya[S][k];
@@ -884,14 +912,15 @@ __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int
       const s16x2 Ms = vpk<s16x2>(Mm);
       const s16x2 Bp = vpk<s16x2>(B) + vpk<s16x2>(HOR | ~VERN);
       const s16x2 T = __builtin_elementwise_max(__builtin_elementwise_max(vpk<s16x2>(A), w.LOW), Bp);
-      push[h] = upk((T - Ms) >> 15);
-      strong[h] = push[h] & upk((w.HIGH - Ms) >> 15);
+      dp[h] = upk(T - Ms);                                     // m > T: push
+      ds[h] = upk(__builtin_elementwise_max(T, w.HIGH) - Ms);  // m > T and m > high: strong
     }
-    // nibble of group k (pixel 2h + t <-> bit t of half h)
-    const uint32_t xp = (push[0] & 0x00020001u) | (push[1] & 0x00080004u);
-    const uint32_t xs = (strong[0] & 0x00020001u) | (strong[1] & 0x00080004u);
-    cw |= ((xp | (xp >> 16)) & 0xfu) << (4 * k);
-    sw |= ((xs | (xs >> 16)) & 0xfu) << (4 * k);
+    // the four sign bits as bytes 0 / -1 (v_perm sign replication), then one
+    // signed byte dot with weights -2^(4k + t): group k's nibble added in place
+    const int WK = k == 0 ? (int)0xf8fcfeffu : (int)0x80c0e0f0u;  // (-1, -2, -4, -8), (-16, .., -128)
+    const uint32_t bp = __builtin_amdgcn_perm(dp[1], dp[0], 0x0b0a0908u), bs = __builtin_amdgcn_perm(ds[1], ds[0], 0x0b0a0908u);
+    cw = (uint32_t)__builtin_amdgcn_sdot4((int)bp, WK, (int)cw, false);
+    sw = (uint32_t)__builtin_amdgcn_sdot4((int)bs, WK, (int)sw, false);
   }
   // the lane's 4K bits into 32-bit words of 8 / K lanes (outside the frame:
   // lanes past the last column group of an edge strip)
@@ -968,6 +997,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 
     constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << 15) + 0.5);
     w.KH = -2 * TG22;
     w.KV = -(2 * TG22 + (1 << 17));
+    w.TWO = 0x00020002u;
+    asm volatile("" : "+s"(w.TWO));
   }
   w.bgr = fd.bgr;
   w.loff = (uint32_t)lc * 3u;
