@@ -4326,13 +4326,14 @@ typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 struct MaskLds {
   lds_cu32* m;
   int Hp;  // bits::tiled_rows(H)
-  __device__ uint32_t word(int, int x, int y) const { return m[(x >> 5) * Hp + y]; }
+  // (24-bit multiplies: x >> 5 and Hp are far below 2^24; v_mul_lo_u32 is quarter rate)
+  __device__ uint32_t word(int, int x, int y) const { return m[__umul24((uint32_t)(x >> 5), (uint32_t)Hp) + y]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 struct MaskBits {
   const uint32_t* m;
   int Hp, W;
-  __device__ uint32_t word(int, int x, int y) const { return m[(x >> 5) * Hp + y]; }
+  __device__ uint32_t word(int, int x, int y) const { return m[__umul24((uint32_t)(x >> 5), (uint32_t)Hp) + y]; }
   __device__ bool test(uint32_t w, int x) const { return (w >> (x & 31)) & 1u; }
 };
 // B, G, R of pixel lin as the low 24 bits of one (unaligned) dword load; the
@@ -4688,7 +4689,7 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
       const bool in = st[k] == SCR_IN;  // interior pixel: no wrap, inside the buffer
       px[k] = in ? x : 0;
       py[k] = in ? y : 0;
-      lin[k] = in ? y * W + x : 0;
+      lin[k] = in ? (int)__umul24((uint32_t)y, (uint32_t)W) + x : 0;  // y, W < 2^13
     }
     // mask words and pixel loads issued unconditionally (address 0 when not
     // needed), so the U loads of a lane are in flight together
@@ -4704,7 +4705,12 @@ __device__ inline void wave_sums_screen_t(const PoseF& P, const LM& lm_at, int l
     for (int k = 0; k < U; k++) {
       const bool hit = st[k] == SCR_IN && mask.test(mw[k], px[k]);
       hm[k] = hit ? -1 : 0;
-      const uint32_t off = hit ? 3u * (uint32_t)lin[k] - 1u : 0u;  // 32-bit offset from the scalar base
+      // 3 lin - 1 as one v_lshl_add_u32 and a v_add (asm: otherwise it becomes a
+      // quarter-rate 64-bit v_mad_u64_u32 and a 64-bit address add per load,
+      // instead of the scalar-base + 32-bit-offset form)
+      uint32_t l3;
+      asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(l3) : "v"(lin[k]));
+      const uint32_t off = hit ? l3 - 1u : 0u;  // 32-bit offset from the scalar base
       typedef __attribute__((address_space(1), aligned(1))) const uint32_t gu32u;
       pv[k] = *(gu32u*)(gbytes(bgr) + off);
     }

@@ -154,11 +154,13 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   const float ez = xn + P.tn;  // 6u (|X|_1 + |t|_1), both parts pre-scaled (screen_landmark, posef_from)
   const float rho2 = fmaf(x, x, y * y);
   const float z2 = z * z;
-  const float rinv = scr_rsq(rho2 + z2);
   const float irho = scr_rsq(rho2);
   const float rho = rho2 * irho;
   const bool wide = rho > z;
-  const float q = (wide ? z : rho) * scr_rcp(wide ? rho : z);
+  // 1 / max(rho, z) >= 1 / |p| (|p| <= sqrt(2) max): the bound's 1 / |p| without
+  // a third transcendental (round 5; the eps term it scales grows by <= sqrt(2))
+  const float rinv = scr_rcp(wide ? rho : z);
+  const float q = (wide ? z : rho) * rinv;
   const float a = scr_atan01(q);
   const float th = wide ? 1.57079632679489662f - a : a;
   const float t2 = th * th;
