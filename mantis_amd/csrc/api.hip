@@ -149,8 +149,6 @@ struct Ctx {
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
   bool tiles_done = false;   // this batch's tiled detector plane was written by the walker
   bool walk_tiles = false;   // MANTIS_WALK_TILES=1: the walker writes it (else k_tile_bits)
-  bool trace_bands = true;   // k_trace_bands for the large batches (MANTIS_TRACE_BANDS=0: k_trace_borders on the tiled plane)
-  bool trace_bands_ok = false;
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
@@ -408,11 +406,6 @@ bool trace_on_lds(const Ctx* c, int n, int Wp, int Hp) {
   return c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames;
 }
 mantis_status run_hysteresis(Ctx* c, int n, int W, int H, bool edge_bytes);
-// border walks per (frame, band of checkpoint rows) with the band's rows in LDS
-bool trace_on_bands(const Ctx* c, int Wp, int Hp) {
-  const size_t lds = ((size_t)band_rows(c->seg_m) * dbits_wpw(Wp) + 1) * sizeof(uint32_t);
-  return c->trace_bands && c->trace_bands_ok && c->seg_m > 0 && lds <= c->trace_lds_max;
-}
 
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
 mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false, bool det_bytes = false) {
@@ -555,11 +548,6 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   if (trace_on_lds(c, n, Wp, Hp)) {
     k_trace_borders_lds<<<n, 1024, tb_lds, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_scratch,
                                                    c->pool_cap, Wp, Hp, kMaxBorders, c->d_rowb, c->rstride, rx, P);
-  } else if (trace_on_bands(c, Wp, Hp)) {
-    const size_t lds = ((size_t)band_rows(c->seg_m) * dbits_wpw(Wp) + 1) * sizeof(uint32_t);
-    k_trace_bands<<<dim3((Hp - 2) / c->seg_m + 1, n), MK_TBB_THREADS, lds, c->s>>>(
-        c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_scratch, c->pool_cap, Wp, Hp, kMaxBorders, c->d_rowb,
-        c->rstride, rx, P);
   } else {
     const int wpw = dbits_wpw(Wp);
     if (!c->tiles_done)  // the morphology walker wrote them already
@@ -1025,7 +1013,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_WALK_TILES")) c->walk_tiles = e[0] == '1';
-  if (const char* e = std::getenv("MANTIS_TRACE_BANDS")) c->trace_bands = e[0] != '0';
   // tests: start the run CCL's mark epoch near its wrap (4..255; the flag plane is cleared at the wrap)
   if (const char* e = std::getenv("MANTIS_HYST_EPOCH0")) c->hyst_epoch = std::max(3, std::min(255, std::atoi(e)));
   c->F = cfg.max_cams;
@@ -1040,8 +1027,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     c->trace_lds_max = 160 * 1024 - 512 * 8 - 64;
     c->trace_lds_ok = hipFuncSetAttribute((const void*)k_trace_borders_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)c->trace_lds_max) == hipSuccess;
-    c->trace_bands_ok = hipFuncSetAttribute((const void*)k_trace_bands, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)c->trace_lds_max) == hipSuccess;
     const char* so = getenv("MANTIS_SCREEN");
     c->screen_off = so && so[0] == '0';
     const char* e = getenv("MANTIS_TRACE_LDS_FRAMES");

@@ -3064,232 +3064,6 @@ __global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __re
   }
 }
 
-// Throughput path (round 5): one block per (frame, band). Band q stages the
-// padded plane's rows qM - 1 .. (q + 2)M + 1 (row-major words: one coalesced
-// copy, ~22 KB at M = 64) in LDS and walks the segments that start in it: the
-// checkpoints of sampled row (q + 1)M, whose walks stay between the sampled
-// rows either side (a walk that reaches one stops at its checkpoint visit
-// there), and the start segments of the borders starting in rows qM + 1 ..
-// (q + 1)M - 1 (a border starts in its top row, so its start segment runs down
-// to row (q + 1)M at most). Each frame's plane is read about twice in all,
-// instead of an L2 round trip per step on a plane that does not stay in L2
-// (k_trace_borders). A step outside the staged rows reads the global plane, so
-// the result never rests on that locality: the walks, points and segment
-// records are k_trace_borders_lds's.
-struct BitsBand {
-  const uint32_t* g;  // the frame's padded plane, row-major (dbits)
-  int wpw, lo, nrows;  // staged rows lo .. lo + nrows - 1 in tb_lds
-  __device__ uint32_t row3(int x, int y) const {
-    const int w = (x - 1) >> 5;
-    const unsigned r = (unsigned)(y - lo);
-    uint32_t a, b;
-    if (r < (unsigned)nrows) {
-      const int o = (int)r * wpw + w;
-      a = tb_lds[o];
-      b = tb_lds[o + 1];
-    } else {
-      const uint32_t* p = g + (size_t)y * wpw + w;
-      a = p[0];
-      b = p[1];
-    }
-    const uint64_t v = ((uint64_t)b << 32) | a;
-    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
-  }
-  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
-  // rows y - 1 .. y + 1 as walk_step's p9; one wave-uniform test for the
-  // staged rows (a per-lane branch per row costs the step ~40 instructions)
-  __device__ uint32_t p9(int x, int y) const {
-    const int w = (x - 1) >> 5, sh = (x - 1) & 31, r = y - 1 - lo;
-    if (__ballot((unsigned)r > (unsigned)(nrows - 3)) == 0) {
-      uint32_t p = 0;
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int o = (r + k) * wpw + w;
-        const uint64_t v = ((uint64_t)tb_lds[o + 1] << 32) | tb_lds[o];
-        p |= ((uint32_t)(v >> sh) & 7u) << (3 * k);
-      }
-      return p;
-    }
-    return row3(x, y - 1) | (row3(x, y) << 3) | (row3(x, y + 1) << 6);
-  }
-};
-// staged rows of a band at checkpoint spacing M (the host sizes the LDS with it)
-__device__ __host__ inline int band_rows(int M) { return 2 * M + 3; }
-#ifndef MK_TBB_THREADS
-#define MK_TBB_THREADS 64
-#endif
-#ifndef MK_TBB_LUT
-#define MK_TBB_LUT 1
-#endif
-// one step of the follower on a neighbourhood functor (walk_step's, which
-// reads the tiled plane itself)
-template <class NB, class EM>
-__device__ inline bool walk_step_nb(const NB& nb, const uint8_t* lut, EM& em, Walk& w, int M, const int32_t* r,
-                                    const uint16_t* X, const int32_t* rowbase, int& nx) {
-  const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
-  const uint32_t p9 = nb.p9(x, y);
-#if MK_TBB_LUT
-  const int s = lut[(p9 << 3) | w.s];
-#else  // the table's rule (build_next_lut), computed: no LDS table, no LDS round trip
-  const uint32_t m = nb8_from_rows(p9 & 7u, (p9 >> 3) & 7u, (p9 >> 6) & 7u);
-  const uint32_t rr = ((m | (m << 8)) >> (w.s + 1)) & 0xffu;
-  const int s = rr ? (w.s + 1 + __builtin_ctz(rr)) & 7 : 8;
-#endif
-  if (M > 0 && !w.first && y % M == 0) {
-    const bool west = arc_has(w.s, s, 4);
-    if (west || arc_has(w.s, s, 0)) {
-      nx = seg_id_at(x, y, west ? 0 : 1, M, r, X, rowbase);
-      return false;
-    }
-  }
-  w.first = 0;
-  if (s != w.prev_s) {
-    em(x - 1, y - 1);
-    w.n++;
-    w.prev_s = s;
-  }
-  const uint32_t np = w.pos + wdelta(s);
-  if (np == w.spos && w.pos == w.p1) {
-    nx = -1;
-    return false;
-  }
-  w.pos = np;
-  w.s = (s + 4) & 7;
-  w.steps++;
-  return true;
-}
-constexpr int kBandJobs = 512;  // start segments of one band held in the job list (more: filtered in place)
-__global__ __launch_bounds__(MK_TBB_THREADS) void k_trace_bands(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                                const Border* __restrict__ borders, FrameState* st,
-                                                                int32_t* __restrict__ scratch, int pool_cap, int Wp,
-                                                                int Hp, int border_cap, const int32_t* __restrict__ rowb,
-                                                                size_t rstride, const uint16_t* __restrict__ rx,
-                                                                size_t plane) {
-  constexpr int NT = MK_TBB_THREADS;
-#if MK_TBB_LUT
-  __shared__ uint8_t next_lut[512 * 8];
-#else
-  const uint8_t* next_lut = nullptr;
-#endif
-  __shared__ int32_t next_job, nsj;
-  __shared__ int32_t sj[kBandJobs];
-  const int f = blockIdx.y, q = blockIdx.x, lane = threadIdx.x & 63;
-  const int M = st[f].seg_m;  // 0: the frame's borders walked whole (band 0, global reads)
-  const int nsr = M > 0 ? (Hp - 2) / M : 0;
-  if (q > nsr) return;
-  const int wpw = dbits_wpw(Wp);
-  const int lo = M > 0 ? max(0, q * M - 1) : 0;
-  const int nrows = M > 0 ? min(Hp - 1, (q + 2) * M + 1) - lo + 1 : 0;
-#if MK_TBB_LUT
-  build_next_lut(next_lut, threadIdx.x, NT);
-#endif
-  if (threadIdx.x == 0) {
-    next_job = 0;
-    nsj = 0;
-  }
-  const uint32_t* B = dbits + (size_t)f * dstride;
-  for (int k = threadIdx.x; k < nrows * wpw; k += NT) tb_lds[k] = B[(size_t)lo * wpw + k];
-  int nb = st[f].n_borders;
-  if (nb > border_cap) nb = border_cap;
-  const Border* bs = borders + (size_t)f * border_cap;
-  int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
-  const int max_chunks = pool_cap / kChunk;
-  int32_t* chunks = sc;
-  int32_t* owner = sc + 2 * (size_t)pool_cap;
-  int32_t* ordv = owner + max_chunks;
-  int32_t* ccount = ordv + max_chunks;
-  const SegTab T = seg_tab(sc, pool_cap);
-  if (nb > T.cap) nb = T.cap;  // k_seg_plan flagged the frame
-  const int NC = st[f].seg_nc;
-  const int32_t* r = rowb + (size_t)f * rstride;
-  const uint16_t* X = rx + (size_t)f * plane;
-  const BitsBand nbh{B, wpw, lo, nrows};
-  __syncthreads();
-  // the job list: this band's checkpoints (sampled row q: ids [c0, c1)), then
-  // the start segments of the borders starting in this band
-  for (int b = threadIdx.x; b < nb; b += NT) {
-    const int sy = bs[b].start / Wp;
-    if ((M > 0 ? min(sy / M, nsr) : 0) == q && T.sdir[NC + b] == kSegStart) {
-      const int k = atomicAdd(&nsj, 1);
-      if (k < kBandJobs) sj[k] = NC + b;
-    }
-  }
-  __syncthreads();
-  const int c0 = q < nsr ? T.rowbase[q] : 0, c1 = q < nsr ? (q + 1 < nsr ? T.rowbase[q + 1] : NC) : 0;
-  const int nck = c1 - c0;
-  const bool listed = nsj <= kBandJobs;  // else every border is a job, filtered when taken
-  const int njobs = nck + (listed ? nsj : nb);
-  const auto job_id = [&](int jj) -> int {
-    if (jj < nck) return c0 + jj;
-    if (listed) return sj[jj - nck];
-    const int b = jj - nck, sy = bs[b].start / Wp;
-    return (M > 0 ? min(sy / M, nsr) : 0) == q && T.sdir[NC + b] == kSegStart ? NC + b : -1;
-  };
-  // k_trace_borders' loop: a lane whose segment ended takes the next job once
-  // a quarter of its wave is idle
-  ChunkEmit em{chunks, owner, ordv, ccount, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
-  Walk w;
-  int i = -1;
-  bool act = false;
-  bool exhausted = njobs == 0;  // wave-uniform
-  const uint64_t below = (1ull << lane) - 1;
-  const auto finish = [&](int nx) {
-    T.cnt[i] = w.n;
-    T.next[i] = nx;
-    em.flush();
-    if (em.ovf) atomicOr(&st[f].overflow, 2);
-    atomicMax(&st[f].trace_steps_max, w.steps);
-    atomicAdd(&st[f].trace_steps_sum, w.steps);
-  };
-  for (;;) {
-    const uint64_t idle = __ballot(!act);
-    const int nidle = __popcll(idle);
-    if (!exhausted && (nidle >= 16 || nidle == 64)) {
-      const int leader = __ffsll((unsigned long long)idle) - 1;
-      int next = 0;
-      if (lane == leader) next = atomicAdd(&next_job, nidle);
-      next = __shfl(next, leader);
-      if (next + nidle >= njobs) exhausted = true;
-      if (!act) {
-        const int jj = next + __popcll(idle & below);
-        const int j = jj < njobs ? job_id(jj) : -1;
-        if (j >= 0) {
-          const int sd = T.sdir[j];
-          if (sd != kSegUnused && sd != kSegAlias) {
-            i = j;
-            const Border b = bs[T.border[j]];
-            em.border = j; em.cur = -1; em.k = 0; em.nch = 0; em.ovf = false;
-            if (sd == kSegStart) {
-              act = walk_start(nbh, b.start % Wp, b.start / Wp, b.hole != 0, em, w);
-              w.first = 0;
-              if (!act) finish(-1);
-            } else if (sd == kSegSingle) {
-              const uint32_t p = (uint32_t)T.pos[j];
-              em((int)(p & 0xffffu) - 1, (int)(p >> 16) - 1);
-              w.n = 1;
-              w.steps = 0;
-              finish(-1);
-            } else {
-              seg_begin(nbh, b, Wp, (uint32_t)T.pos[j], sd, w);
-              act = true;
-            }
-          }
-        }
-      }
-      continue;
-    }
-    if (nidle == 64) {
-      if (exhausted) break;
-      continue;
-    }
-    int nx = -1;
-    if (act && !walk_step_nb(nbh, next_lut, em, w, M, r, X, T.rowbase, nx)) {
-      act = false;
-      finish(nx);
-    }
-  }
-}
-
 // 5 waves per SIMD (96 VGPRs, 32 B of spills) rather than the 106 VGPRs / 4
 // waves the 1024-thread bound allows: in throughput mode (256-thread blocks)
 // a fifth block per CU, 5.34 -> 4.75 ms per 4096 frames
