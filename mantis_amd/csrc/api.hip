@@ -563,7 +563,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
   k_frame_contours<<<n, n <= c->fc_small_frames ? 1024 : MK_FC_THREADS, 0, c->s>>>(c->d_dbits, c->dstride, c->d_borders, c->d_st, c->d_bcount, c->d_boff,
                                          c->d_pool, c->d_scratch, c->pool_cap, c->d_quads, c->d_dbg, c->d_frames, Wp,
                                          Hp, P, kMaxBorders, (double)c->cfg.polygon_epsilon,
-                                         c->cfg.search_radius_multiplier);
+                                         c->cfg.search_radius_multiplier, c->d_rowb, c->rstride, rx);
   mark(c, "contours_quads");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;

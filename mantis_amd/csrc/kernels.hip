@@ -2237,10 +2237,12 @@ __global__ __launch_bounds__(256) void k_run_border(const int32_t* __restrict__ 
         b.start = key; b.hole = 0; b.parent = key;
       } else {
         // hole: the run on its left is foreground; its component's root run
-        // starts at the key of the enclosing outer border
+        // starts at the key of the enclosing outer border. Kept as -(root + 1):
+        // k_frame_contours turns it into that key for the few borders that
+        // become quads (the root's row is a binary search of dependent loads,
+        // the longest chain of this kernel when it ran for every hole here)
         const int pr = uf_find_c(L, id - 1);
-        const int py = run_at_row(r, Hp, pr);
-        b.start = key - 1; b.hole = 1; b.parent = py * Wp + X[pr];
+        b.start = key - 1; b.hole = 1; b.parent = -(pr + 1);
       }
     }
     // one counter atomic per wave trip for all its roots
@@ -3077,7 +3079,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
                                                          int32_t* __restrict__ scratch, int pool_cap,
                                                          QuadRec* __restrict__ quads, FrameDebug* dbg,
                                                          const FrameDesc* __restrict__ frames, int Wp, int Hp,
-                                                         size_t plane, int border_cap, double eps, double search_mult) {
+                                                         size_t plane, int border_cap, double eps, double search_mult,
+                                                         const int32_t* __restrict__ rowb, size_t rstride,
+                                                         const uint16_t* __restrict__ rx) {
   __shared__ int32_t scan[1024];
   __shared__ RawQuad raw[kMaxQuads];
   __shared__ int32_t nraw, total, nkeep;
@@ -3104,7 +3108,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     const int q = atomicAdd(&nraw, 1);
     if (q < kMaxQuads) {
       for (int k = 0; k < 8; k++) raw[q].c[k] = q4[k];
-      raw[q].parent = bs[i].parent;
+      int par = bs[i].parent;
+      if (par < 0) {  // a hole's parent as its component's root run (k_run_border): that run's key
+        const int pr = -par - 1;
+        par = run_at_row(rowb + (size_t)f * rstride, Hp, pr) * Wp + rx[(size_t)f * plane + pr];
+      }
+      raw[q].parent = par;
       raw[q].hole = bs[i].hole;
       raw[q].key = bs[i].key;
     } else {

@@ -26,7 +26,7 @@ struct Border {  // one Suzuki–Abe border in the parallel formulation
   int32_t key;     // raster index (padded) where the scan would discover it
   int32_t start;   // padded index of the start pixel
   int32_t hole;    // 1 = hole border
-  int32_t parent;  // CCOMP parent: key of the enclosing component's outer border (own key for outers)
+  int32_t parent;  // CCOMP parent: key of the enclosing component's outer border (own key for outers); holes: -(root run + 1) until k_frame_contours resolves it
 };
 
 struct QuadRec {
