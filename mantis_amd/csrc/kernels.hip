@@ -3066,6 +3066,9 @@ __global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __re
   }
 }
 
+#ifndef MK_FC_CU
+#define MK_FC_CU 4  // compaction trips in flight per wave (k_frame_contours step 3)
+#endif
 // 5 waves per SIMD (96 VGPRs, 32 B of spills) rather than the 106 VGPRs / 4
 // waves the 1024-thread bound allows: in throughput mode (256-thread blocks)
 // a fifth block per CU, 5.34 -> 4.75 ms per 4096 frames
@@ -3176,7 +3179,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
   // then the border's offset, then the store) costs one round trip per kCU
   // trips instead of per trip
   if (nchunk > 0) {
-    constexpr int CPW = 64 / kChunk, kCU = 4;
+    constexpr int CPW = 64 / kChunk, kCU = MK_FC_CU;
     const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
     const int32_t* ccount = ordv + max_chunks;
     const int l = lane % kChunk;

@@ -225,22 +225,45 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       init_iters = 1;
     }
   }
+  // The point reads of the scans below go kApproxAhead at a time (indices
+  // wrapped, every load issued before the first is used): one memory round
+  // trip per group instead of per point on the device, where one lane walks a
+  // border and each read is an L2 trip. Same points, same order, same
+  // arithmetic as cv::approxPolyDP's scans.
+#ifndef MK_APPROX_AHEAD
+#define MK_APPROX_AHEAD 4
+#endif
+  constexpr int kApproxAhead = MK_APPROX_AHEAD;
   if (is_closed) {
     rs_s = 0;
     for (i = 0; i < init_iters; i++) {
       double dist, max_dist = 0;
       pos = (pos + rs_s) % count;
       MK_READ(spx, spy, pos);
-      for (j = 1; j < count; j++) {
-        double dx, dy;
-        MK_READ(ptx, pty, pos);
-        dx = ptx - spx;
-        dy = pty - spy;
-        dist = dx * dx + dy * dy;
-        if (dist > max_dist) {
-          max_dist = dist;
-          rs_s = j;
+      for (j = 1; j < count; j += kApproxAhead) {
+        int gx[kApproxAhead], gy[kApproxAhead];
+        int p = pos;
+        for (int k = 0; k < kApproxAhead; k++) {  // wrapped indices stay inside the border
+          gx[k] = src[2 * p];
+          gy[k] = src[2 * p + 1];
+          if (++p >= count) p = 0;
         }
+        const int nk = count - j < kApproxAhead ? count - j : kApproxAhead;
+        for (int k = 0; k < kApproxAhead; k++) {
+          if (k >= nk) break;
+          double dx, dy;
+          dx = gx[k] - spx;
+          dy = gy[k] - spy;
+          dist = dx * dx + dy * dy;
+          if (dist > max_dist) {
+            max_dist = dist;
+            rs_s = j + k;
+          }
+        }
+        ptx = gx[nk - 1];
+        pty = gy[nk - 1];
+        pos += nk;
+        if (pos >= count) pos -= count;
       }
       le_eps = max_dist <= eps;
     }
@@ -264,13 +287,29 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       double dx, dy, dist, max_dist = 0;
       dx = epx - spx;
       dy = epy - spy;
-      while (pos != sl_e) {
-        MK_READ(ptx, pty, pos);
-        dist = fabs((pty - spy) * dx - (ptx - spx) * dy);
-        if (dist > max_dist) {
-          max_dist = dist;
-          rs_s = (pos + count - 1) % count;
+      int left = sl_e - pos;  // reads until pos reaches sl_e
+      if (left < 0) left += count;
+      while (left > 0) {
+        int gx[kApproxAhead], gy[kApproxAhead];
+        int p = pos;
+        for (int k = 0; k < kApproxAhead; k++) {
+          gx[k] = src[2 * p];
+          gy[k] = src[2 * p + 1];
+          if (++p >= count) p = 0;
         }
+        const int nk = left < kApproxAhead ? left : kApproxAhead;
+        for (int k = 0; k < kApproxAhead; k++) {
+          if (k >= nk) break;
+          ptx = gx[k];
+          pty = gy[k];
+          if (++pos >= count) pos = 0;
+          dist = fabs((pty - spy) * dx - (ptx - spx) * dy);
+          if (dist > max_dist) {
+            max_dist = dist;
+            rs_s = (pos + count - 1) % count;
+          }
+        }
+        left -= nk;
       }
       le_eps = max_dist * max_dist <= eps * (dx * dx + dy * dy);
     } else {
