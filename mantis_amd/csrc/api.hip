@@ -614,6 +614,9 @@ mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::R
   return MANTIS_OK;
 }
 
+#ifndef MK_S1B_WPC
+#define MK_S1B_WPC 32  // k_rpp_s1b waves per CU at most (a grid-stride loop over the items; 8: rpp_2nd 2.1 vs 1.8 ms per 4096 frames)
+#endif
 void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, int32_t* jobs1, RppQueue* q,
                        RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads,
                        bool paired, bool small = false) {
@@ -628,7 +631,7 @@ void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, 
                         lanes, rounds);
   mark(c, "rpp_first");
   const int spread = small ? c->s1b_spread_small : 1;
-  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items * spread + 63) / 64, (size_t)c->n_cu * 8), 64, 0, c->s>>>(
+  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items * spread + 63) / 64, (size_t)c->n_cu * MK_S1B_WPC), 64, 0, c->s>>>(
       items, jobs0, jobs1, q, pr, spread);
   mark(c, "rpp_2nd");
   run_objpose_rounds<1>(c, blocks_for(expected_items * 2), items, rf, jobs1, q, st, 0, lanes, rounds);
