@@ -535,7 +535,7 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
     k_run_scan<<<n, 256, 0, c->s>>>(c->d_rowb, c->rstride, c->d_st, Hp);
     k_run_emit<<<grow, 256, 0, c->s>>>(c->d_dbits, c->dstride, c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
   }
-  k_run_band<<<dim3((Hp + RB_ROWS - 1) / RB_ROWS, n), 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
+  k_run_band<<<dim3((Hp + RB_ROWS - 1) / RB_ROWS, n), RB_THREADS, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
   const int seams = (Hp - 1) / RB_ROWS;
   if (seams > 0)
     k_run_seam<<<dim3((seams + 3) / 4, n), 256, 0, c->s>>>(c->d_rowb, c->rstride, rx, c->d_lab, P, Wp, Hp);
