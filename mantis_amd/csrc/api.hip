@@ -406,6 +406,9 @@ bool trace_on_lds(const Ctx* c, int n, int Wp, int Hp) {
   return c->trace_lds_ok && tb_lds <= c->trace_lds_max && n <= c->trace_lds_frames;
 }
 mantis_status run_hysteresis(Ctx* c, int n, int W, int H, bool edge_bytes);
+#ifndef MK_MW_ROLES
+#define MK_MW_ROLES 2  // k_morph_walk waves per segment: detector and mask chains apart (1: one wave does both)
+#endif
 
 // gray..Canny, hysteresis, detector binary (padded) and clean mask
 mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = false, bool det_bytes = false) {
@@ -452,7 +455,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     // small batches (latency): short segments, many waves per frame (the
     // walk down a whole frame is ~1 ms of dependent steps)
     const int seg = n <= c->fc_small_frames ? c->morph_walk_small : c->morph_walk;
-    const int nseg = (H + seg - 1) / seg, nwv = nseg * n;
+    const int nseg = (H + seg - 1) / seg, nwv = nseg * n * MK_MW_ROLES;
     // MANTIS_WALK_TILES=1: the walker also writes the tiled plane the L2 border
     // walker reads (measured slower: morph 2.4 -> 3.8 ms per 4096 frames for
     // border_trace 4.65 -> 4.3: its 8-byte scattered row stores cost more than
@@ -463,11 +466,11 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     c->tiles_done = tiles;
     if (nseg == 1) {
       k_morph_walk<true><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
-                                                                      c->dstride, seg, nseg, nwv, wr);
+                                                                      c->dstride, seg, nseg, nwv, wr, MK_MW_ROLES);
       c->runs_done = true;
     } else {
       k_morph_walk<false><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
-                                                                       c->dstride, seg, nseg, nwv, wr);
+                                                                       c->dstride, seg, nseg, nwv, wr, MK_MW_ROLES);
     }
     mark(c, "morph/k_morph_walk");
   } else {

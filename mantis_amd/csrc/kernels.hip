@@ -1862,9 +1862,17 @@ struct WalkRuns {
 template <bool RUNS>
 __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                     uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
-                                                    size_t dstride, int seg_rows, int nseg, int nwaves, WalkRuns wr) {
-  const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
-  if (gw >= nwaves) return;
+                                                    size_t dstride, int seg_rows, int nseg, int nwaves, WalkRuns wr,
+                                                    int roles) {
+  const int gw0 = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
+  if (gw0 >= nwaves) return;
+  // roles == 2 (round 5): two waves per segment, the detector chain (dilate 5,
+  // erode 3, runs) on one and the mask chain (NOT gradient, border, seven
+  // stages) on the other, each reading the edge rows itself: the per-row
+  // dependent chain of a wave is about half as long and twice the waves run
+  const int role = roles == 2 ? (gw0 & 1) : -1;  // 0 detector, 1 mask, -1 both
+  const bool det = role != 1, msk = role != 0;
+  const int gw = roles == 2 ? gw0 >> 1 : gw0;
   const int lane = threadIdx.x & 63;
   const int f = gw / nseg, sg = gw - f * nseg;
   const int ys = sg * seg_rows, ye = min(H, ys + seg_rows);
@@ -1880,10 +1888,10 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     if (TB && lane < wpw) TB[((size_t)(py >> 5) * wpw + lane) * 32 + (py & 31)] = (uint64_t)v | ((uint64_t)nx << 32);
   };
   // padded detector ring rows (zero) by the first / last segment
-  if (sg == 0 && lane < wpw) D[lane] = 0u;
-  if (ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
-  if (sg == 0) tile(0u, 0);
-  if (ye == H) tile(0u, H + 1);
+  if (det && sg == 0 && lane < wpw) D[lane] = 0u;
+  if (det && ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
+  if (det && sg == 0) tile(0u, 0);
+  if (det && ye == H) tile(0u, H + 1);
   int32_t* RB = RUNS ? wr.rowb + (size_t)f * wr.rstride : nullptr;
   uint16_t* RX = RUNS ? wr.rx + (size_t)f * wr.plane : nullptr;
   int32_t* RL = RUNS ? wr.lab + (size_t)f * wr.plane : nullptr;
@@ -1907,7 +1915,7 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     }
     run_id += 1 + __builtin_amdgcn_readlane(inc, 63);
   };
-  if (RUNS) emit_runs(0u, 0);
+  if (RUNS && det) emit_runs(0u, 0);
   MwStage<2, true> d1;   // detector dilate 5x5 of E
   MwStage<1, false> d2;  // detector erode 3x3
   MwStage<3, true> s1;
@@ -1929,16 +1937,20 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     q0 = ld(i + 2);
     q1 = ld(i + 3);
     // NOT(gradient) rows i - 1, i; M0 rows i - 2, i - 1
-    const uint32_t g0 = in(i - 1) ? mw_ng(eA, in(i - 2), eB, e0, in(i), vm) : 0u;
-    const uint32_t g1 = in(i) ? mw_ng(eB, in(i - 1), e0, e1, in(i + 1), vm) : 0u;
-    const uint32_t m0 = in(i - 2) ? mw_m0(eA, nA, nB, g0, vm) : 0u;
-    const uint32_t m1 = in(i - 1) ? mw_m0(eB, nB, g0, g1, vm) : 0u;
+    uint32_t m0 = 0u, m1 = 0u;
+    if (msk) {
+      const uint32_t g0 = in(i - 1) ? mw_ng(eA, in(i - 2), eB, e0, in(i), vm) : 0u;
+      const uint32_t g1 = in(i) ? mw_ng(eB, in(i - 1), e0, e1, in(i + 1), vm) : 0u;
+      m0 = in(i - 2) ? mw_m0(eA, nA, nB, g0, vm) : 0u;
+      m1 = in(i - 1) ? mw_m0(eB, nB, g0, g1, vm) : 0u;
+      nA = g0;
+      nB = g1;
+    }
     eA = e0;
     eB = e1;
-    nA = g0;
-    nB = g1;
-    // detector: dilate r2 of E (rows i, i + 1 in; i - 2, i - 1 out), erode r1 (i - 3, i - 2 out)
     uint32_t a0, a1, b0, b1;
+    if (det) {
+    // detector: dilate r2 of E (rows i, i + 1 in; i - 2, i - 1 out), erode r1 (i - 3, i - 2 out)
     d1.push2(e0, in(i), e1, in(i + 1), a0, a1);
     d2.push2((a0 & vm) | ~vm, in(i - 2), (a1 & vm) | ~vm, in(i - 1), b0, b1);
     b0 &= vm;
@@ -1958,6 +1970,8 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
         if (RUNS) emit_runs(v1, y + 2);
       }
     }
+    }
+    if (!msk) continue;
     // mask: {dilate, erode}(3), (4), (5), erode(3): M0 rows i - 2, i - 1 in; i - 29, i - 28 out
     s1.push2(m0, in(i - 2), m1, in(i - 1), a0, a1);
     s2.push2((a0 & vm) | ~vm, in(i - 5), (a1 & vm) | ~vm, in(i - 4), b0, b1);
@@ -1970,7 +1984,7 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
     if (y >= ys && y < ye && lane < WW) M[bits::tiled_word(y, lane, Hp)] = a0 & vm;
     if (y + 1 >= ys && y + 1 < ye && lane < WW) M[bits::tiled_word(y + 1, lane, Hp)] = a1 & vm;
   }
-  if (RUNS) {
+  if (RUNS && det) {
     emit_runs(0u, H + 1);
     if (lane == 0) {
       RB[H + 2] = run_id;
