@@ -248,7 +248,8 @@ mantis_status mantis_markov_get(void* ctx, double* planes, double* yaw, int32_t*
 mantis_status mantis_canny(void* ctx, const mantis_image* img, uint8_t* canny_out);
 /* cv::Canny's hysteresis alone (the stack walk of QuadDetection.h:212 / HypothesisEvaluation.h:327's
  * Canny): cls W*H bytes, 0 = no candidate, 1 = weak candidate (NMS passed, mag > low), 2 = strong
- * (mag > high); out W*H bytes 0/255 = the candidates 8-connected to a strong pixel */
+ * (mag > high); out W*H bytes 0/255 = the candidates 8-connected to a strong pixel. Any other
+ * class byte (e.g. a 0/255 plane) returns MANTIS_ERR_ARG */
 mantis_status mantis_hysteresis(void* ctx, const uint8_t* cls, int32_t width, int32_t height, uint8_t* edges_out);
 /* detector binary (dilate x2, erode x1, QuadDetection.h:213-214) and the
  * cleanImageByEdge mask (HypothesisEvaluation.h:319-386); either output may be NULL */

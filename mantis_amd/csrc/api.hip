@@ -116,7 +116,7 @@ struct Ctx {
   // batch calls wait for the stream on a blocking-sync event (the host thread
   // sleeps instead of spinning in hipStreamSynchronize: one spinning thread per
   // context was most of a step's host CPU time); calls of at most
-  // spin_frames frames spin (latency). MANTIS_SPIN_FRAMES overrides.
+  // spin_frames frames spin (latency).
   hipEvent_t ev_wait = nullptr;
   int spin_frames = 16;
   std::string err;
@@ -183,7 +183,6 @@ struct Ctx {
   // Fewer jobs per wave measured slower once correct (one per wave in one round:
   // rpp_first 3.28 -> 3.64 / 3.80 ms, profiles/r04_p50_objpose_lanes_fixed.txt)
   int op_lanes_small = 64, op_rounds_small = 6;
-  int s1b_spread_small = 1;  // k_rpp_s1b lanes per item for small batches (MANTIS_S1B_SPREAD_SMALL: 1, 2, 4 ... 64)
   int seg_m = 64;        // border-walk checkpoint rows (k_seg_plan; 0: borders walked whole)
   int canny_strip = 2;  // k_canny_strip: 2 = 8 columns per lane where W % 8 == 0, 1 = 4 columns; 0 = tiles (MANTIS_CANNY_STRIP)
   // the same for batches of at most fc_small_frames frames (the rig-latency
@@ -633,9 +632,8 @@ void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, 
   run_objpose_rounds<0>(c, blocks_for(paired ? expected_items / 2 : expected_items), items, rf, jobs0, q, st, pr,
                         lanes, rounds);
   mark(c, "rpp_first");
-  const int spread = small ? c->s1b_spread_small : 1;
-  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items * spread + 63) / 64, (size_t)c->n_cu * MK_S1B_WPC), 64, 0, c->s>>>(
-      items, jobs0, jobs1, q, pr, spread);
+  k_rpp_s1b<<<(unsigned)std::min<size_t>((expected_items + 63) / 64, (size_t)c->n_cu * MK_S1B_WPC), 64, 0, c->s>>>(
+      items, jobs0, jobs1, q, pr);
   mark(c, "rpp_2nd");
   run_objpose_rounds<1>(c, blocks_for(expected_items * 2), items, rf, jobs1, q, st, 0, lanes, rounds);
   mark(c, "rpp_cand");
@@ -710,18 +708,15 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // drawing thread), so the copy overlaps the RPP kernels still queued on s;
   // s waits for it only before the scoring kernels. d_gauss / h_gauss are free:
   // the previous batch's call synchronised s, which had waited on this copy.
-  // default: the side-stream copy (score stage 11.13 / 11.34 -> 10.95 / 10.97 ms per 4096
-  // frames in a 6-context A/B); MANTIS_GAUSS_ZEROCOPY=1: k_score_init reads the pinned buffer
-  static const bool zc = getenv("MANTIS_GAUSS_ZEROCOPY") != nullptr;
-  if (!zc) {
-    HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
-    HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
-    HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
-  }
+  // (the side-stream copy: score stage 11.13 / 11.34 -> 10.95 / 10.97 ms per 4096
+  // frames in a 6-context A/B against k_score_init reading the pinned buffer)
+  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
+  HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
+  HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
   mark(c, "gauss_h2d");
   Landmarks L = lmk_of(c);
   k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
-                                              c->d_dbg, c->d_sst, zc ? c->h_gauss : nullptr, c->d_gauss, per);
+                                              c->d_dbg, c->d_sst);
   mark(c, "score_pf_yaw/k_score_init");
   // particle filter: 16 waves per frame, each task one particle over a
   // 1/kPfSplit slice of the landmarks (the integer partial sums combine
@@ -1010,10 +1005,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_LANES_SMALL")) c->op_lanes_small = std::max(1, std::min(64, std::atoi(e)));
-  if (const char* e = std::getenv("MANTIS_S1B_SPREAD_SMALL")) {
-    const int v = std::atoi(e);
-    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) c->s1b_spread_small = v;
-  }
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
@@ -1078,7 +1069,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     c->morph_walk = std::max(0, atoi(e));
     c->morph_walk_small = std::max(1, c->morph_walk);
   }
-  if (const char* e = getenv("MANTIS_SPIN_FRAMES")) c->spin_frames = atoi(e);
   if (const char* e = getenv("MANTIS_MORPH_WALK_SMALL")) c->morph_walk_small = std::max(1, atoi(e));
   if (morph_lds(c->Wmax, c->morph_bh) > 160 * 1024 ||
       hipFuncSetAttribute((const void*)k_morph, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1154,7 +1144,11 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     return st;
   }
   (void)hipGetLastError();
-  if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess) {
+  // the run CCL's mark plane starts clean: a first epoch set near the wrap
+  // (MANTIS_HYST_EPOCH0) skips the clear at epoch 4, and k_hyst_fix reads the
+  // flags of roots k_hyst_mark never wrote
+  if (hipMemset(c->d_dbg, 0, sizeof(FrameDebug) * F) != hipSuccess ||
+      hipMemset(c->d_strong, 0, c->fstride * (size_t)F) != hipSuccess) {
     g_create_err = "hipMemset failed";
     mantis_destroy(c);
     return MANTIS_ERR_DEVICE;
@@ -1731,6 +1725,10 @@ mantis_status mantis_hysteresis(void* ctx, const uint8_t* cls, int32_t width, in
   if (!c || !cls || !edges_out) return MANTIS_ERR_ARG;
   const int W = width, H = height;
   if (W <= 2 || H <= 2 || W > c->Wmax || H > c->Hmax) { c->err = "image size outside [3, max]"; return MANTIS_ERR_ARG; }
+  // class bytes are 0 / 1 / 2 only: k_cls_to_bits reads any non-zero byte as a
+  // candidate, the oracle only 1 and 2, so other values are refused
+  for (size_t i = 0; i < (size_t)W * H; i++)
+    if (cls[i] > 2) { c->err = "class plane: bytes must be 0 (none), 1 (weak) or 2 (strong)"; return MANTIS_ERR_ARG; }
   HIP_OK(hipMemcpyAsync(c->d_edge, cls, (size_t)W * H, hipMemcpyHostToDevice, c->s));
   k_cls_to_bits<<<blocks_for((size_t)bits::words(W) * H), 256, 0, c->s>>>(c->d_edge, c->d_b1, c->d_b2, W, H);
   if (mantis_status st = run_hysteresis(c, 1, W, H, true); st != MANTIS_OK) return st;

@@ -736,6 +736,8 @@ __device__ __forceinline__ void strip_advance(StripWave<K>& w, int i) {
 // k+1, or the neighbouring lanes' last / first group by DPP.
 template <int K, int S, bool ROWS, bool EDGE>
 __device__ __forceinline__ void strip_step(StripWave<K>& w, StripRegs<K>& R, int i) {
+  // the nibble packing below (WK) has weights for groups 0 and 1 only: bits 0..7 of a lane's byte
+  static_assert(K == 1 || K == 2, "k_canny_strip packs at most two 4-column groups per lane");
   constexpr int S1 = (S + 1) % 3, S2 = (S + 2) % 3;  // slots of rows i-2 / i+1, i-1
   constexpr int SHIFT = 15;
   constexpr int TG22 = (int)(0.4142135623730950488016887242097 * (1 << SHIFT) + 0.5);
@@ -1929,7 +1931,10 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   const auto in = [H](int y) { return (unsigned)y < (unsigned)H; };
   uint32_t eA = 0, eB = 0;  // E rows i - 2, i - 1 (masked to the image, 0 outside it)
   uint32_t nA = 0, nB = 0;  // NG rows i - 3, i - 2
-  const int i0 = max(0, ys - MB_HALO), i1 = min(H, ye) + MB_HALO;
+  // input rows a segment needs: the detector's output row y reads E rows y - 3 .. y + 3 (dilate 2 +
+  // erode 1), the mask's y - 29 .. y + 29; a detector-only wave walks its own reach
+  const int halo = role == 0 ? 3 : MB_HALO;
+  const int i0 = max(0, ys - halo), i1 = min(H, ye) + halo;
   const auto ld = [&](int y) { return (in(y) && lane < WW) ? E[(size_t)y * WW + lane] & vm : 0u; };
   uint32_t q0 = ld(i0), q1 = ld(i0 + 1);  // E rows prefetched a step ahead
   for (int i = i0; i < i1; i += 2) {
@@ -3736,13 +3741,9 @@ __global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, 
 #define MK_S1B_WPE 2
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MK_S1B_WPE))) void k_rpp_s1b(RppItem* __restrict__ items, const int32_t* __restrict__ jobs0,
-                                                int32_t* __restrict__ jobs1, RppQueue* q, int paired, int spread) {
+                                                int32_t* __restrict__ jobs1, RppQueue* q, int paired) {
   const int n0 = q->n0 << (paired ? 1 : 0);  // paired: both orientations of every first-queue job
-  // spread > 1 (small batches): one item per `spread` lanes, so an item's
-  // root-finder path does not wait on other items' divergent ones
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g % spread) return;
-  for (int k = g / spread; k < n0; k += gridDim.x * blockDim.x / spread) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n0; k += gridDim.x * blockDim.x) {
     const int32_t i = paired ? jobs0[k >> 1] + (k & 1) : jobs0[k];
     if (!items[i].active) continue;
     double model[12];
@@ -4617,7 +4618,10 @@ __device__ inline void block_drain(UQueue q, const double* lmd, const Cam* cmp, 
 // init / final: 10 waves per frame. Particle filter block: 16 waves, tasks = (particle, 1/kPfSplit of the
 // landmarks): 100 tasks over 16 waves at split 2 -- 18.3 ms per 4096 frames
 // against 20.5 for 10 waves with one task per particle (50 tasks, 5 rounds)
-constexpr int kPfThreads = 1024;
+#ifndef MK_PF_THREADS
+#define MK_PF_THREADS 1024
+#endif
+constexpr int kPfThreads = MK_PF_THREADS;
 #ifndef MK_PF_SPLIT
 #define MK_PF_SPLIT 2
 #endif
@@ -4673,16 +4677,9 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_score_init(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
-    ScoreState* __restrict__ sst, const float* __restrict__ hgauss, float* __restrict__ dgauss, int per) {
+    ScoreState* __restrict__ sst) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // hgauss != null: this frame's slice of the host-drawn gaussian stream is
-  // read from pinned host memory straight into the device buffer the
-  // particle filter reads (no separate copy and no cross-stream wait)
-  if (hgauss && st[f].reaches_pf) {
-    const size_t o = (size_t)st[f].gauss_offset;
-    for (int i = tid; i < per; i += NT) dgauss[o + i] = hgauss[o + i];
-  }
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
   const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
@@ -5300,7 +5297,10 @@ __global__ __launch_bounds__(NT) void k_score_final(
   // on the original image. Set k derives from set k-1; all four are built
   // first (P[20k + i], the shifts are no longer needed) so their 80 scorings
   // share one pass over the waves (5 rounds at 16 waves instead of 4 x 2).
-  __shared__ PoseLds Y[20];
+  // the top 20 staged in the COLOR scratch (not in use yet): LDS per block
+  // 83.2 -> 78.5 KB, under half a CU's 160 KB
+  static_assert(sizeof(ColorPairs) >= 20 * sizeof(PoseLds), "top-20 staging");
+  PoseLds* Y = (PoseLds*)&cpairs;
   if (tid < 20) {
     const PoseLds& s = P[top[tid]];
     Y[tid] = s;

@@ -174,12 +174,18 @@ MK_HD int screen_project(const PoseF& P, float X, float Y, float Z, float xn, co
   const bool valid = (int)(z > ez) & (int)(rho2 > 1e-12f * z2) & (int)(eps < 0.25f);
 #if defined(__HIP_DEVICE_COMPILE__)
   // v_cvt_i32_f32 is defined for every input (NaN -> 0, out of range saturates);
-  // a value that is not `valid` decides nothing below
+  // a value that is not `valid` decides nothing below. Emitted as the
+  // instruction itself: a C++ float -> int conversion of an
+  // out-of-range value is poison in LLVM IR, which a compiler may fold into
+  // anything, `valid & ...` included
   const float ru = rintf(u), rv = rintf(v);
+  int iu, iv;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(iu) : "v"(ru));
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(iv) : "v"(rv));
 #else
   const float ru = rintf(valid ? u : 0.f), rv = rintf(valid ? v : 0.f);  // (int) of NaN / huge is UB on the host
-#endif
   const int iu = (int)ru, iv = (int)rv;
+#endif
   const bool round_ok = (int)(fabsf(u - ru) < 0.5f - eps) & (int)(fabsf(v - rv) < 0.5f - eps);
   const bool interior = (int)((unsigned)(iu - 1) < (unsigned)(W - 1)) & (int)((unsigned)(iv - 1) < (unsigned)(H - 1));
   const bool outside = (int)((unsigned)iu > (unsigned)W) | (int)((unsigned)iv > (unsigned)H);
