@@ -51,6 +51,10 @@ import subprocess
 import sys
 import time
 
+# the rig-latency path (the p50 leg) replays hipGraphs only with the HIP
+# runtime's graph packet capture off, set before HIP initialises
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -255,6 +255,20 @@ struct Ctx {
   int markov_n = 0;
   int32_t* d_agree = nullptr;  // sharded calls: the failure flag all-reduced by agree()
   bool agreed_fail = false;     // the last failure was agreed on by every rank (agree())
+  // hipGraphs of the rig-latency path (batches of at most fc_small_frames
+  // frames): the call's device work as two graphs -- image stages .. RPP ..
+  // gaussian offsets, then scoring + result copies -- captured once per call
+  // shape and replayed (MANTIS_GRAPHS=0, or the runtime's graph packet
+  // capture on: every kernel launched directly)
+  struct CallGraph {
+    int n = 0, W = 0, H = 0, live = 0, nw = 0, nr = 0, ng = 0;
+    bool vec = false;
+    const void* lm = nullptr;
+    const void* gauss = nullptr;
+    hipGraphExec_t pre = nullptr, post = nullptr;
+  };
+  std::vector<CallGraph> graphs;
+  bool use_graphs = false;
   // MANTIS_SCREEN=0 at mantis_create: the fast scorers' FP32 projection screen is
   // off (every landmark takes the exact FP64 fallback; a test / A-B switch)
   bool screen_off = false;
@@ -702,7 +716,7 @@ void gen_gauss(Ctx* c, int n) {  // n <= c->gauss_cap
   }
 }
 
-mantis_status run_score(Ctx* c, int n, int n_gauss) {
+mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   const int per = c->cfg.particles * c->cfg.iterations * 6;
   // on the side stream as soon as the host has drawn it (the caller joined the
   // drawing thread), so the copy overlaps the RPP kernels still queued on s;
@@ -710,9 +724,11 @@ mantis_status run_score(Ctx* c, int n, int n_gauss) {
   // the previous batch's call synchronised s, which had waited on this copy.
   // (the side-stream copy: score stage 11.13 / 11.34 -> 10.95 / 10.97 ms per 4096
   // frames in a 6-context A/B against k_score_init reading the pinned buffer)
-  HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
-  HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
-  HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
+  if (copy_gauss) {  // (graph calls copy on c->s before the scoring graph)
+    HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * n_gauss, hipMemcpyHostToDevice, c->s_copy));
+    HIP_OK(hipEventRecord(c->ev_gauss, c->s_copy));
+    HIP_OK(hipStreamWaitEvent(c->s, c->ev_gauss, 0));
+  }
   mark(c, "gauss_h2d");
   Landmarks L = lmk_of(c);
   k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
@@ -809,6 +825,59 @@ mantis_status ensure_gauss(Ctx* c, int n) {
   return MANTIS_OK;
 }
 
+// Stream capture of one part of a call into an executable graph. A failure
+// inside the body ends the capture (the stream leaves capture mode either way)
+// and discards what was captured.
+template <class F>
+mantis_status capture_graph(Ctx* c, hipGraphExec_t* out, F&& body) {
+  HIP_OK(hipStreamBeginCapture(c->s, hipStreamCaptureModeThreadLocal));
+  const mantis_status st = body();
+  hipGraph_t gr = nullptr;
+  const hipError_t e = hipStreamEndCapture(c->s, &gr);
+  if (st != MANTIS_OK || e != hipSuccess) {
+    if (gr) (void)hipGraphDestroy(gr);
+    if (st != MANTIS_OK) return st;
+    c->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+    return MANTIS_ERR_DEVICE;
+  }
+  const hipError_t ei = hipGraphInstantiate(out, gr, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(gr);
+  if (ei != hipSuccess) {
+    *out = nullptr;
+    c->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(ei);
+    return MANTIS_ERR_DEVICE;
+  }
+  return MANTIS_OK;
+}
+
+// The cached graphs of a call shape (created empty, captured by the call), or
+// null when the call takes the direct launches: sharded calls (collectives and
+// host agreement between the parts), profiling (per-stage events), batches
+// past the latency path, and frames whose hysteresis takes the run CCL (its
+// per-call mark epoch is a kernel argument). Everything else a launch bakes in
+// is part of the key: the shape, whether the frames allow dword loads, the
+// live-context count (the ObjPose grid), the map and the gaussian buffer.
+Ctx::CallGraph* call_graph(Ctx* c, int n, int W, int H, const Shard* sh) {
+  if (!c->use_graphs || sh || c->prof || n > c->fc_small_frames) return nullptr;
+  const size_t hr_lds = (size_t)((H + HR_ROWS - 1) / HR_ROWS) * HR_ROWS * bits::words(W) * sizeof(uint32_t);
+  if (!(c->hyst_rec && bits::words(W) <= 63 && H <= HR_ROWS * HR_MAXW && hr_lds <= c->hyst_rec_lds)) return nullptr;
+  const int live = std::max(1, g_live_ctx[c->cfg.device & 63].load());
+  for (auto& g : c->graphs)
+    if (g.n == n && g.W == W && g.H == H && g.vec == c->vec_ok && g.live == live && g.lm == c->d_lm &&
+        g.nw == c->nw && g.nr == c->nr && g.ng == c->ng && g.gauss == c->d_gauss)
+      return &g;
+  if (c->graphs.size() >= 8) {  // the oldest shape goes
+    if (c->graphs.front().pre) (void)hipGraphExecDestroy(c->graphs.front().pre);
+    if (c->graphs.front().post) (void)hipGraphExecDestroy(c->graphs.front().post);
+    c->graphs.erase(c->graphs.begin());
+  }
+  Ctx::CallGraph g;
+  g.n = n; g.W = W; g.H = H; g.vec = c->vec_ok; g.live = live;
+  g.lm = c->d_lm; g.nw = c->nw; g.nr = c->nr; g.ng = c->ng; g.gauss = c->d_gauss;
+  c->graphs.push_back(g);
+  return &c->graphs.back();
+}
+
 mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shard* sh = nullptr) {
   if (!c->d_lm) { c->err = "map not set (mantis_set_map)"; return MANTIS_ERR_STATE; }
   if (n <= 0 || n > c->F) { c->err = "frame count exceeds max_cams"; return MANTIS_ERR_ARG; }
@@ -829,17 +898,49 @@ mantis_status process_frames(Ctx* c, const mantis_image* cams, int n, const Shar
   gauss.t = std::thread([c, ng] { gen_gauss(c, ng); });
   int W, H;
   mantis_status st = stage_frames(c, cams, n, W, H);
-  if (st == MANTIS_OK) st = run_image_stages(c, n, W, H);
-  if (st == MANTIS_OK) st = run_contours(c, n, W, H);
-  if (st == MANTIS_OK) st = run_pose(c, n);
-  if (sh) st = agree(c, st);  // before the PF-flag all-gather
-  if (st != MANTIS_OK) return st;
-  if ((st = gauss_offsets(c, n, sh)) != MANTIS_OK) return st;
-  gauss.t.join();
-  if ((st = run_score(c, n, ng)) != MANTIS_OK) return st;
-  HIP_OK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(mantis_cam_result) * n, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(c->h_gtotal, c->d_gtotal, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
+  const auto results_d2h = [&]() -> mantis_status {
+    HIP_OK(hipMemcpyAsync(c->h_res, c->d_res, sizeof(mantis_cam_result) * n, hipMemcpyDeviceToHost, c->s));
+    HIP_OK(hipMemcpyAsync(c->h_st, c->d_st, sizeof(FrameState) * n, hipMemcpyDeviceToHost, c->s));
+    HIP_OK(hipMemcpyAsync(c->h_gtotal, c->d_gtotal, sizeof(int32_t), hipMemcpyDeviceToHost, c->s));
+    return MANTIS_OK;
+  };
+  Ctx::CallGraph* g = st == MANTIS_OK ? call_graph(c, n, W, H, sh) : nullptr;
+  if (g) {
+    // the rig-latency path as two graph launches: the frames' descriptors (and
+    // any host frames) were copied above, the gaussians are copied between the
+    // two launches once the host thread has drawn them
+    if (!g->pre)
+      st = capture_graph(c, &g->pre, [&]() -> mantis_status {
+        mantis_status s2 = run_image_stages(c, n, W, H);
+        if (s2 == MANTIS_OK) s2 = run_contours(c, n, W, H);
+        if (s2 == MANTIS_OK) s2 = run_pose(c, n);
+        if (s2 == MANTIS_OK) s2 = gauss_offsets(c, n, nullptr);
+        return s2;
+      });
+    if (st != MANTIS_OK) return st;
+    HIP_OK(hipGraphLaunch(g->pre, c->s));
+    gauss.t.join();
+    const int per = c->cfg.particles * c->cfg.iterations * 6;
+    HIP_OK(hipMemcpyAsync(c->d_gauss, c->h_gauss, sizeof(float) * per * ng, hipMemcpyHostToDevice, c->s));
+    if (!g->post)
+      st = capture_graph(c, &g->post, [&]() -> mantis_status {
+        mantis_status s2 = run_score(c, n, ng, false);
+        if (s2 == MANTIS_OK) s2 = results_d2h();
+        return s2;
+      });
+    if (st != MANTIS_OK) return st;
+    HIP_OK(hipGraphLaunch(g->post, c->s));
+  } else {
+    if (st == MANTIS_OK) st = run_image_stages(c, n, W, H);
+    if (st == MANTIS_OK) st = run_contours(c, n, W, H);
+    if (st == MANTIS_OK) st = run_pose(c, n);
+    if (sh) st = agree(c, st);  // before the PF-flag all-gather
+    if (st != MANTIS_OK) return st;
+    if ((st = gauss_offsets(c, n, sh)) != MANTIS_OK) return st;
+    gauss.t.join();
+    if ((st = run_score(c, n, ng)) != MANTIS_OK) return st;
+    if ((st = results_d2h()) != MANTIS_OK) return st;
+  }
   if (sh) HIP_OK(hipMemcpyAsync(c->h_sh_flags, c->d_sh_flags, sizeof(int32_t) * ng, hipMemcpyDeviceToHost, c->s));
   HIP_OK(wait_stream(c, n));
   finish_profile(c);
@@ -1010,6 +1111,17 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_WALK_TILES")) c->walk_tiles = e[0] == '1';
+  {
+    // graph replays need the HIP runtime's AQL packet capture of graphs off
+    // (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before HIP starts):
+    // with it on (ROCm 7.2's default) a replay of the rig-latency graphs after
+    // other contexts had come and gone faulted the GPU (illegal address) in the
+    // round-6 GPU tests, and the same replay with it off ran clean (DESIGN.md
+    // §4). Without that setting every kernel is launched directly.
+    const char* pc = std::getenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE");
+    c->use_graphs = pc && pc[0] == '0';
+    if (const char* e = std::getenv("MANTIS_GRAPHS")) c->use_graphs = c->use_graphs && e[0] != '0';
+  }
   // tests: start the run CCL's mark epoch near its wrap (4..255; the flag plane is cleared at the wrap)
   if (const char* e = std::getenv("MANTIS_HYST_EPOCH0")) c->hyst_epoch = std::max(3, std::min(255, std::atoi(e)));
   c->F = cfg.max_cams;
@@ -1166,6 +1278,10 @@ mantis_status mantis_destroy(void* ctx) {
   if (c->counted) g_live_ctx[c->cfg.device & 63].fetch_sub(1);
   if (c->s) (void)hipStreamSynchronize(c->s);
   if (c->comm) (void)ncclCommDestroy((ncclComm_t)c->comm);
+  for (auto& g : c->graphs) {
+    if (g.pre) (void)hipGraphExecDestroy(g.pre);
+    if (g.post) (void)hipGraphExecDestroy(g.post);
+  }
   if (c->d_rwjobs) (void)hipFree(c->d_rwjobs);
   if (c->d_markov) (void)hipFree(c->d_markov);
   if (c->d_mops) (void)hipFree(c->d_mops);

@@ -1,6 +1,10 @@
 import os
 import sys
 
+# the library replays hipGraphs on the rig-latency path only with the HIP
+# runtime's graph packet capture off (set before HIP initialises)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

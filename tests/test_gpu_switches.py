@@ -93,7 +93,8 @@ SMALL = [("MANTIS_PF_SPLIT", "0"),            # one particle-filter block per fr
          ("MANTIS_MORPH_WALK_SMALL", "16"),   # 16-row walker segments (45 per frame)
          ("MANTIS_MORPH_WALK_SMALL", "100000"),  # one segment per frame: the walker numbers the runs
          ("MANTIS_FC_SMALL_FRAMES", "0"),     # the throughput kernels on a one-rig batch
-         ("MANTIS_RPP_BLOCKS", "1")]          # a one-block ObjPose grid (the small path sizes its own grid: no effect)
+         ("MANTIS_RPP_BLOCKS", "1"),          # a one-block ObjPose grid (the small path sizes its own grid: no effect)
+         ("MANTIS_GRAPHS", "0")]              # every kernel launched directly instead of the two replayed hipGraphs
 # the throughput path (80 frames)
 LARGE = [("MANTIS_RPP_BLOCKS", "8"),          # a small persistent ObjPose grid: every lane serves many jobs
          ("MANTIS_RPP_BLOCKS", "32"),
@@ -137,3 +138,45 @@ def test_switched_paths_against_oracle(scene, landmark_map):
         orc = O.Oracle(*landmark_map, seed=1)
         for f in range(CAMS):
             _cmp_debug(got["records"][f], orc.process(host[f], K, D), f"{env} frame {f}")
+
+
+def test_graph_replay_across_call_shapes(scene, landmark_map):
+    """The rig-latency path replays captured hipGraphs (one pair per call shape):
+    repeated calls, a call of another shape in between (a second capture) and
+    the first shape again must give the same bytes as the first call, and the
+    same as a context without graphs, including the cv::RNG state carried
+    from call to call."""
+    import mantis_amd as M
+
+    imgs = scene[0]
+
+    def calls(env):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            m = M.Mantis(max_cams=8, max_width=W, max_height=H)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+        out = []
+        try:
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+            for batch, rigs in ((imgs[:4], 1), (imgs[:4], 1), (imgs[4:12], 2), (imgs[8:12], 1), (imgs[:4], 1)):
+                rig, cams = m.process(batch, rigs=rigs)
+                out.append(([bytes(r) for r in rig], [bytes(c) for c in cams],
+                            [bytes(m.frame_debug(f)) for f in range(len(batch))], m.rng_state))
+        finally:
+            m.close()
+        return out
+
+    g, d = calls({}), calls({"MANTIS_GRAPHS": "0"})
+    assert len(g) == len(d)
+    for k, (a, b) in enumerate(zip(g, d)):
+        assert a == b, f"call {k}: graph replay differs from direct launches"
+    # the same rig at another RNG state gives another particle filter, at the
+    # same state the same bytes: the replays read the state-dependent inputs
+    assert g[0][3] != g[1][3]
