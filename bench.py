@@ -490,7 +490,7 @@ def run_config3(a, rk, cpu):
         "score_pf_yaw": ("valu", frames_step * (FLOPS_PER_PROJ * (s_fast + 37 * slow_per_frame) +
                                                 FLOPS_PER_WINDOW * 37 * slow_per_frame)),
     }
-    stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_final"),
+    stage_kernels = {"score_pf_yaw": ("k_score_init", "k_score_pf", "k_score_shift_part", "k_score_final"),
                      "canny_nms": ("k_canny_strip<2>", "k_canny_strip<1>", "k_canny"),
                      "hysteresis": ("k_hyst_rec", "k_hyst_band", "k_hyst_seam", "k_hyst_mark", "k_hyst_fix"),
                      "morph": ("k_morph",)}

@@ -189,6 +189,11 @@ struct Ctx {
   // path): tiles, whose ~230 blocks per frame run at once, where the strip
   // walk of a frame is 720 dependent row steps (MANTIS_CANNY_STRIP sets both)
   int canny_small = 0;
+#ifndef MK_SHIFT_SPLIT
+#define MK_SHIFT_SPLIT 0
+#endif
+  bool shift_split = MK_SHIFT_SPLIT;  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
+  bool canny_cat = true;  // k_canny_strip<2> over the frames side by side where W % 32 == 0 (MANTIS_CANNY_CAT=0: per frame)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
   // dense scoring (mantis_score_argmin): hypotheses, errors, counts; (err, idx) pairs per rank
@@ -432,15 +437,18 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   const int cstrip = n <= c->fc_small_frames ? c->canny_small : c->canny_strip;
   if (cstrip >= 2 && c->vec_ok && W % 8 == 0 && W >= 16 && H >= 3) {
     // column strips walked by one wave each, 8 columns per lane (W % 8 == 0)
-    const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols, nw = ns * n;
+    // W % 32 == 0: the strips tile the frames laid side by side (no partial strip per frame)
+    const int ns = (W + StripGeom<2>::cols - 1) / StripGeom<2>::cols;
+    const bool cat = c->canny_cat && W % 32 == 0;
+    const int nw = cat ? (int)(((int64_t)n * W + StripGeom<2>::cols - 1) / StripGeom<2>::cols) : ns * n;
     k_canny_strip<2><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
-                                                                 c->d_b1, c->d_b2, B, ns, nw);
+                                                                 c->d_b1, c->d_b2, B, ns, nw, cat ? 1 : 0, n);
     mark(c, "canny_nms/k_canny_strip<2>");
   } else if (cstrip && c->vec_ok && W >= 8 && H >= 3) {
     // 4 columns per lane (W % 4 == 0, dword-aligned rows)
     const int ns = (W + StripGeom<1>::cols - 1) / StripGeom<1>::cols, nw = ns * n;
     k_canny_strip<1><<<(unsigned)((nw + 3) / 4), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
-                                                                 c->d_b1, c->d_b2, B, ns, nw);
+                                                                 c->d_b1, c->d_b2, B, ns, nw, 0, n);
     mark(c, "canny_nms/k_canny_strip<1>");
   } else {
     k_canny<<<(unsigned)(tgx * tgy * n), 256, 0, c->s>>>(c->d_frames, c->cfg.canny_low, 3 * c->cfg.canny_low,
@@ -760,13 +768,18 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
         c->cfg.iterations);
   mark(c, "score_pf_yaw/k_score_pf");
-  if (split) {  // small batches: the 81 shifts over several blocks per frame first
+  // the 81 shifts over several blocks per frame first (small batches; large
+  // ones with shift_split: the shift tasks in a lean kernel instead of beside
+  // k_score_final's sorting, COLOR and publishing code)
+  const bool shifts_apart = split || c->shift_split;
+  if (shifts_apart) {
     constexpr int spb = kScoreTail / 128;
     k_score_shift_part<kScoreTail><<<dim3((81 + spb - 1) / spb, n), kScoreTail, 0, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_sst, c->cfg.grid_spacing, 9, spb);
+    mark(c, "score_pf_yaw/k_score_shift_part");
   }
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
-                                               c->d_sst, c->cfg.grid_spacing, 9, split);
+                                               c->d_sst, c->cfg.grid_spacing, 9, shifts_apart);
   mark(c, "score_pf_yaw/k_score_final");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
@@ -1109,6 +1122,8 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(16, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
+  if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
+  if (const char* e = std::getenv("MANTIS_SHIFT_SPLIT")) c->shift_split = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_WALK_TILES")) c->walk_tiles = e[0] == '1';
   {

@@ -969,28 +969,52 @@ __device__ __forceinline__ void strip_walk(StripWave<K>& w, StripRegs<K>& R) {
     if (i + 2 < rows) strip_step<K, 2, true, EDGE>(w, R, i + 2);
   }
 }
-// one wave per (frame, strip); needs W % (4K) == 0, W >= 8K, H >= 3
+// one wave per (frame, strip); needs W % (4K) == 0, W >= 8K, H >= 3.
+// cat (W % 32 == 0, round 6): the strips tile the batch's frames laid side by
+// side -- strip s covers columns [s cols, (s + 1) cols) of that n W-column
+// band, so a strip may hold the end of one frame and the start of the next
+// (frame boundaries fall on 32-column words, so every output word belongs to
+// one frame; a lane takes its frame's rows, the border rules apply per lane
+// at each frame's own edges, and DPP neighbours across a boundary are never
+// read). ceil(n W / cols) waves instead of n ceil(W / cols): at 1280 columns
+// and 480-column strips 2.67 instead of 3 waves per frame, the partial third
+// strip's idle lanes gone.
 template <int K>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 : MK_STRIP2_WAVES))) void k_canny_strip(const FrameDesc* __restrict__ frames, int low, int high,
                                                      uint32_t* __restrict__ cbits, uint32_t* __restrict__ sbits,
-                                                     size_t bstride, int nstrip, int nwaves) {
+                                                     size_t bstride, int nstrip, int nwaves, int cat, int nframes) {
   // the wave index is wave-uniform: frame fields and row conditions stay scalar
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wv >= nwaves) return;
   StripWave<K> w;
   w.lane = threadIdx.x & 63;
-  const int f = wv / nstrip, sidx = wv - f * nstrip;
-  const FrameDesc fd = frames[f];
-  const int W = fd.w;
-  w.H = fd.h;
-  w.WW = bits::words(W);
   constexpr int G = 4 * K;  // columns per lane
-  const int base = sidx * StripGeom<K>::cols;
-  const int c0 = w.lane == 63 ? base - G : base + G * w.lane;     // this lane's first column
+  constexpr int LPW = StripGeom<K>::lanes_per_word;
+  const int W = frames[0].w;  // one size per batch
+  w.H = frames[0].h;
+  w.WW = bits::words(W);
+  int f, base, c0;
+  bool edge_strip;
+  if (cat) {
+    const int vbase = wv * StripGeom<K>::cols;                        // the strip's first column in the band
+    const int vc = w.lane == 63 ? vbase - G : vbase + G * w.lane;     // this lane's
+    const int fl = vc < 0 ? 0 : vc / W;
+    f = fl < nframes ? fl : nframes - 1;
+    c0 = vc - f * W;                                                  // frame-local (outside [0, W) past the band)
+    base = c0 - G * w.lane;                                           // for the store-lane test below (lanes < 60)
+    edge_strip = true;
+  } else {
+    f = wv / nstrip;
+    const int sidx = wv - f * nstrip;
+    base = sidx * StripGeom<K>::cols;
+    c0 = w.lane == 63 ? base - G : base + G * w.lane;
+    edge_strip = sidx == 0 || sidx == nstrip - 1;
+  }
   const int lc = c0 < 0 ? 0 : (c0 > W - G ? W - G : c0);           // loads stay inside the row
   w.left_edge = c0 == 0;                                           // columns -1.. come from the border rules
   w.right_edge = c0 == W - G;
   w.inside = c0 >= 0 && c0 <= W - G;
+  if (cat) edge_strip = __builtin_amdgcn_ballot_w64(w.left_edge || w.right_edge || !w.inside) != 0;
   const int lowc = low < -1 ? -1 : (low > 32767 ? 32767 : low);
   const int highc = high < -1 ? -1 : (high > 32767 ? 32767 : high);
   w.LOW = s16x2{(short)lowc, (short)lowc};
@@ -1002,18 +1026,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 1 ? 8 
     w.TWO = 0x00020002u;
     asm volatile("" : "+s"(w.TWO));
   }
-  w.bgr = fd.bgr;
-  w.loff = (uint32_t)lc * 3u;
   w.rstep = (uint32_t)W * 3u;
-  w.cb = cbits + (size_t)f * bstride + (size_t)(base >> 5);
-  w.sbp = sbits + (size_t)f * bstride + (size_t)(base >> 5);
-  constexpr int LPW = StripGeom<K>::lanes_per_word;
-  w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes &&
-                 base + G * (w.lane & ~(LPW - 1)) < W;
+  if (cat) {
+    // per lane: its frame's pixels and planes (at most two frames per wave)
+    w.bgr = frames[f].bgr;
+    w.loff = (uint32_t)lc * 3u;
+    const size_t wo = (size_t)f * bstride + (size_t)((c0 < 0 ? 0 : c0) >> 5) - (size_t)(w.lane / LPW);
+    w.cb = cbits + wo;
+    w.sbp = sbits + wo;
+    w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes && w.inside;
+  } else {
+    w.bgr = frames[f].bgr;
+    w.loff = (uint32_t)lc * 3u;
+    w.cb = cbits + (size_t)f * bstride + (size_t)(base >> 5);
+    w.sbp = sbits + (size_t)f * bstride + (size_t)(base >> 5);
+    w.store_lane = (w.lane & (LPW - 1)) == LPW - 1 && w.lane < StripGeom<K>::out_lanes &&
+                   base + G * (w.lane & ~(LPW - 1)) < W;
+  }
   StripRegs<K> R = {};
 #pragma unroll
   for (int p = 0; p < strip_pf<K>(); p++) strip_load_to(w, p < w.H ? p : w.H - 1, w.rows[p]);
-  if (sidx == 0 || sidx == nstrip - 1) strip_walk<K, true>(w, R);
+  if (edge_strip) strip_walk<K, true>(w, R);
   else strip_walk<K, false>(w, R);
 }
 

@@ -103,7 +103,10 @@ LARGE = [("MANTIS_RPP_BLOCKS", "8"),          # a small persistent ObjPose grid:
          ("MANTIS_OP_SPILL", "0"),            # a wave never hands its jobs on
          ("MANTIS_OP_SPILL", "64"),           # every wave with an idle lane hands its jobs on
          ("MANTIS_FC_SMALL_FRAMES", "100000"),  # the latency kernels on an 80-frame batch
-         ("MANTIS_PF_SPLIT", "0")]            # (no effect on a large batch)
+         ("MANTIS_PF_SPLIT", "0"),            # (no effect on a large batch)
+         ("MANTIS_CANNY_CAT", "0"),           # Canny strips per frame instead of over the frames side by side
+         ("MANTIS_SHIFT_SPLIT", "1"),         # the 81 shifts in k_score_shift_part blocks
+         ("MANTIS_SHIFT_SPLIT", "0")]
 
 
 def test_rig_latency_path_switches(scene, landmark_map):
@@ -180,3 +183,51 @@ def test_graph_replay_across_call_shapes(scene, landmark_map):
     # the same rig at another RNG state gives another particle filter, at the
     # same state the same bytes: the replays read the state-dependent inputs
     assert g[0][3] != g[1][3]
+
+
+@pytest.mark.parametrize("wh", [(1280, 720), (992, 600), (1000, 600)])
+def test_canny_strips_side_by_side(landmark_map, wh):
+    """k_canny_strip<2> over the batch's frames laid side by side (W % 32 == 0:
+    a strip may hold one frame's last columns and the next frame's first ones)
+    against the per-frame strips and the oracle: 6 frames in one batch with
+    the strip kernel forced on the small path (MANTIS_CANNY_STRIP=2). 992
+    columns put the frame boundaries at a different place in every strip;
+    1000 (W % 32 != 0) keeps the per-frame strips."""
+    import mantis_amd as M
+
+    Wc, Hc = wh
+    K, D = synth.intrinsics(Wc, Hc)
+    rng = np.random.default_rng(31)
+    host = []
+    for f in range(6):
+        R, pos = synth.random_pose(rng)
+        host.append(synth.render_host(synth.make_cam(R, pos, Wc, Hc), synth.frame_seed(7, f)))
+    host[3] = np.clip(host[3].astype(np.int16) + rng.integers(-40, 40, host[3].shape), 0, 255).astype(np.uint8)
+    imgs = [M.make_image(x, K, D) for x in host]
+
+    def run(env):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            m = M.Mantis(max_cams=6, max_width=Wc, max_height=Hc)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+        try:
+            m.set_map(*landmark_map)
+            m.rng_state = 1
+            _, cams = m.process(imgs, rigs=6)
+            return ([bytes(c) for c in cams], [bytes(m.frame_debug(f)) for f in range(6)],
+                    [list(m.frame_counters(f)[:3]) for f in range(6)], [m.frame_debug(f) for f in range(6)])
+        finally:
+            m.close()
+
+    per = run({"MANTIS_CANNY_STRIP": "2", "MANTIS_CANNY_CAT": "0"})
+    cat = run({"MANTIS_CANNY_STRIP": "2"})
+    assert cat[0] == per[0] and cat[1] == per[1] and cat[2] == per[2], f"{wh}: side-by-side strips differ"
+    orc = O.Oracle(*landmark_map, seed=1)
+    for f in range(6):
+        _cmp_debug(cat[3][f], orc.process(host[f], K, D), f"{wh} frame {f}")
