@@ -539,7 +539,9 @@ def run_config3(a, rk, cpu):
     # HBM traffic and VALU issue from PMC summaries of this same build
     # (tools/pmc_score.sh / tools/pmc_traffic.sh write lib_sha16): per launch =
     # per-frame counters x frames_step; null when no summary matches the build
-    pj = pmc_for(os.path.join("profiles", "r05_pmc.json"))
+    pmc_path = next((p for p in (os.path.join("profiles", "r06_pmc.json"), os.path.join("profiles", "r05_pmc.json"))
+                     if pmc_for(p) is not None), os.path.join("profiles", "r06_pmc.json"))
+    pj = pmc_for(pmc_path)
     pmc_k = {} if pj is None else pj["kernels"]
     pmc_fr = None if pj is None else pj["frames_per_launch"]
 
@@ -559,7 +561,7 @@ def run_config3(a, rk, cpu):
             r["valu_instructions_per_launch"] = int(vi)
             # wave64 VALU instruction = 2 cycles on a SIMD-32 (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
             r["valu_issue_frac"] = round(vi * 2 / (1024 * 2.4e9 * r["avg_launch_ms"] * 1e-3), 4)
-        r["pmc_source"] = ("profiles/r05_pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step); "
+        r["pmc_source"] = (pmc_path + " (FETCH_SIZE x 2 + WRITE_SIZE, SQ_INSTS_VALU; per frame x frames_step); "
                            "the x2 is calibrated on gfx950 for every load width the stages issue (4 / 12 / 16 B "
                            "coalesced, 4-B gathers) and WRITE_SIZE is 1x for full-line stores: profiles/r05_pmc_calib.txt")
 

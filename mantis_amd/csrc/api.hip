@@ -147,8 +147,6 @@ struct Ctx {
   int morph_bh = 48;       // k_morph output rows per band (MB_BH, or MB_BH_NARROW at wide max_width)
   int morph_walk = 1 << 20;  // k_morph_walk rows per segment (0: the LDS band kernel k_morph); MANTIS_MORPH_WALK
   bool runs_done = false;    // this batch's detector runs were numbered by the walker (one segment per frame)
-  bool tiles_done = false;   // this batch's tiled detector plane was written by the walker
-  bool walk_tiles = false;   // MANTIS_WALK_TILES=1: the walker writes it (else k_tile_bits)
   int morph_walk_small = 48; // walker segment rows for batches of at most fc_small_frames frames; MANTIS_MORPH_WALK_SMALL
   size_t pf_mask_lds = 0;  // bytes of dynamic LDS for k_score_pf's staged mask (0: global mask)
   int hyst_epoch = 3;      // hysteresis mark value of the current call (4..255; 3: the plane is not cleared yet)
@@ -469,7 +467,6 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
   HIP_OK(hipMemsetAsync(c->d_st, 0, sizeof(FrameState) * n, c->s));
 #endif
   c->runs_done = false;
-  c->tiles_done = false;
   if (c->morph_walk > 0 && bits::words(W) <= 62 && dbits_wpw(W + 2) <= 63) {
     // register walker: one wave per (frame, row segment); with one segment per
     // frame it also numbers the detector runs (k_run_count / scan / emit)
@@ -477,14 +474,7 @@ mantis_status run_image_stages(Ctx* c, int n, int W, int H, bool edge_bytes = fa
     // walk down a whole frame is ~1 ms of dependent steps)
     const int seg = n <= c->fc_small_frames ? c->morph_walk_small : c->morph_walk;
     const int nseg = (H + seg - 1) / seg, nwv = nseg * n * MK_MW_ROLES;
-    // MANTIS_WALK_TILES=1: the walker also writes the tiled plane the L2 border
-    // walker reads (measured slower: morph 2.4 -> 3.8 ms per 4096 frames for
-    // border_trace 4.65 -> 4.3: its 8-byte scattered row stores cost more than
-    // k_tile_bits' staged pass)
-    const bool tiles = c->walk_tiles && !trace_on_lds(c, n, W + 2, H + 2);
-    const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st,
-                      tiles ? (uint64_t*)c->d_tbits : nullptr, c->tstride};
-    c->tiles_done = tiles;
+    const WalkRuns wr{c->d_rowb, c->rstride, c->d_lroot, c->d_lab, c->plane, c->d_st};
     if (nseg == 1) {
       k_morph_walk<true><<<(unsigned)((nwv + 3) / 4), 256, 0, c->s>>>(c->d_eb, c->d_dbits, c->d_mbits, W, H, B,
                                                                       c->dstride, seg, nseg, nwv, wr, MK_MW_ROLES);
@@ -574,9 +564,8 @@ mantis_status run_contours(Ctx* c, int n, int W, int H) {
                                                    c->pool_cap, Wp, Hp, kMaxBorders, c->d_rowb, c->rstride, rx, P);
   } else {
     const int wpw = dbits_wpw(Wp);
-    if (!c->tiles_done)  // the morphology walker wrote them already
-      k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, 32 * wpw * sizeof(uint32_t), c->s>>>(c->d_dbits, c->dstride,
-                                                                                    c->d_tbits, c->tstride, wpw, Hp);
+    k_tile_bits<<<dim3((Hp + 31) / 32, n), 256, kTbRows * wpw * sizeof(uint32_t), c->s>>>(
+        c->d_dbits, c->dstride, c->d_tbits, c->tstride, wpw, Wp, Hp);
     k_trace_borders<<<n, 64 * MK_TB_WAVES, 0, c->s>>>(c->d_tbits, c->tstride, c->d_borders, c->d_st, c->d_scratch, c->pool_cap, Wp,
                                         kMaxBorders, c->d_rowb, c->rstride, rx, P);
   }
@@ -1125,7 +1114,6 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_SHIFT_SPLIT")) c->shift_split = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
-  if (const char* e = std::getenv("MANTIS_WALK_TILES")) c->walk_tiles = e[0] == '1';
   {
     // graph replays need the HIP runtime's AQL packet capture of graphs off
     // (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in the environment before HIP starts):
@@ -1220,7 +1208,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   chk(dalloc(c, &c->d_b1, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_b2, (size_t)F * c->bstride));
   chk(dalloc(c, &c->d_dbits, (size_t)F * c->dstride));
-  c->tstride = tbits_words(dbits_wpw(c->Wmax + 2), c->Hmax + 2);
+  c->tstride = tbits_words(c->Wmax + 2, c->Hmax + 2);
   chk(dalloc(c, &c->d_tbits, (size_t)F * c->tstride));
   c->rstride = (size_t)c->Hmax + 3 + (c->Hmax + HB_ROWS - 1) / HB_ROWS;  // + the hysteresis band run counts
   chk(dalloc(c, &c->d_rowb, (size_t)F * c->rstride));

@@ -1887,13 +1887,10 @@ struct WalkRuns {
   int32_t* lab;
   size_t plane;
   FrameState* st;
-  // the same padded rows as the border walks' tiled plane (k_tile_bits' layout:
-  // the 64-bit window of words w, w + 1 of row py at ((py / 32) wpw + w) 32 +
-  // py % 32), written here instead of by a pass of its own; null: not needed
-  // (the LDS border walker of small batches reads the row-major plane)
-  uint64_t* tb;
-  size_t tstride;  // uint32 words per frame
 };
+#ifndef MK_MW_PF
+#define MK_MW_PF 1  // k_morph_walk: steps of E-row prefetch
+#endif
 template <bool RUNS>
 __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__ eb, uint32_t* __restrict__ dbits,
                                                     uint32_t* __restrict__ mbits, int W, int H, size_t bstride,
@@ -1916,17 +1913,9 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   const uint32_t* E = eb + (size_t)f * bstride;
   uint32_t* D = dbits + (size_t)f * dstride;
   uint32_t* M = mbits + (size_t)f * bstride;
-  uint64_t* TB = wr.tb ? (uint64_t*)((uint32_t*)wr.tb + (size_t)f * wr.tstride) : nullptr;
-  // a padded row's word and the next lane's into the tiled plane
-  const auto tile = [&](uint32_t v, int py) {
-    const uint32_t nx = dpp_from_right(v);  // lanes past the row hold 0
-    if (TB && lane < wpw) TB[((size_t)(py >> 5) * wpw + lane) * 32 + (py & 31)] = (uint64_t)v | ((uint64_t)nx << 32);
-  };
   // padded detector ring rows (zero) by the first / last segment
   if (det && sg == 0 && lane < wpw) D[lane] = 0u;
   if (det && ye == H && lane < wpw) D[(size_t)(H + 1) * wpw + lane] = 0u;
-  if (det && sg == 0) tile(0u, 0);
-  if (det && ye == H) tile(0u, H + 1);
   int32_t* RB = RUNS ? wr.rowb + (size_t)f * wr.rstride : nullptr;
   uint16_t* RX = RUNS ? wr.rx + (size_t)f * wr.plane : nullptr;
   int32_t* RL = RUNS ? wr.lab + (size_t)f * wr.plane : nullptr;
@@ -1969,11 +1958,16 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
   const int halo = role == 0 ? 3 : MB_HALO;
   const int i0 = max(0, ys - halo), i1 = min(H, ye) + halo;
   const auto ld = [&](int y) { return (in(y) && lane < WW) ? E[(size_t)y * WW + lane] & vm : 0u; };
-  uint32_t q0 = ld(i0), q1 = ld(i0 + 1);  // E rows prefetched a step ahead
+  // E rows prefetched MK_MW_PF steps (2 MK_MW_PF rows) ahead
+  uint32_t q[2 * MK_MW_PF];
+#pragma unroll
+  for (int k = 0; k < 2 * MK_MW_PF; k++) q[k] = ld(i0 + k);
   for (int i = i0; i < i1; i += 2) {
-    const uint32_t e0 = q0, e1 = q1;  // E rows i, i + 1
-    q0 = ld(i + 2);
-    q1 = ld(i + 3);
+    const uint32_t e0 = q[0], e1 = q[1];  // E rows i, i + 1
+#pragma unroll
+    for (int k = 0; k + 2 < 2 * MK_MW_PF; k++) q[k] = q[k + 2];
+    q[2 * MK_MW_PF - 2] = ld(i + 2 * MK_MW_PF);
+    q[2 * MK_MW_PF - 1] = ld(i + 2 * MK_MW_PF + 1);
     // NOT(gradient) rows i - 1, i; M0 rows i - 2, i - 1
     uint32_t m0 = 0u, m1 = 0u;
     if (msk) {
@@ -1999,12 +1993,10 @@ __global__ __launch_bounds__(256) void k_morph_walk(const uint32_t* __restrict__
       const uint32_t v0 = lane < wpw ? (b0 << 1) | (p0 >> 31) : 0u, v1 = lane < wpw ? (b1 << 1) | (p1 >> 31) : 0u;
       if (y >= ys && y < ye) {
         if (lane < wpw) D[(size_t)(y + 1) * wpw + lane] = v0;
-        tile(v0, y + 1);
         if (RUNS) emit_runs(v0, y + 1);
       }
       if (y + 1 >= ys && y + 1 < ye) {
         if (lane < wpw) D[(size_t)(y + 2) * wpw + lane] = v1;
-        tile(v1, y + 2);
         if (RUNS) emit_runs(v1, y + 2);
       }
     }
@@ -2534,36 +2526,54 @@ struct RawQuad {
   int32_t parent, hole, key;
 };
 
-// The detector bit plane again for the walks: the 64-bit window (word w,
-// word w + 1) of every row and word, in tiles of 32 rows (256 bytes per word
-// column and tile), so a step reads one 8-byte word per row and a walk moving
-// vertically stays in the lines it already holds instead of touching a new
-// row-major line (with thousands of frames walking at once, an HBM round
-// trip) per step.
-__device__ __host__ inline size_t tbits_words(int wpw, int Hp) { return (size_t)2 * wpw * ((Hp + 31) & ~31); }
+// The detector bit plane again for the walks (round 6 layout): for each
+// 32-row tile ty and 16-pixel group g, kTbRows = 34 32-bit words -- rows
+// 32 ty - 1 .. 32 ty + 32 of the 32-pixel window 16 g - 8 .. 16 g + 23. A walk
+// step at (x, y) needs pixels x - 1 .. x + 1 of rows y - 1 .. y + 1: group
+// x >> 4, bit (x & 15) + 7 of three consecutive words (entries y & 31 ..
+// + 2 of the tile), so ONE 12-byte load per step instead of three 8-byte
+// ones of round 5's 64-bit row windows (the walks were bound by the vector
+// memory pipeline: TA 64 %, TD 77 % busy, profiles/r05_pmc.json); a walk
+// moving vertically stays in the lines it holds. Same size as before (~250 KB
+// per 720p frame).
+constexpr int kTbRows = 34;
+__device__ __host__ inline int tb_groups(int Wp) { return ((Wp - 2) >> 4) + 1; }
+__device__ __host__ inline size_t tbits_words(int Wp, int Hp) {
+  return (size_t)tb_groups(Wp) * kTbRows * (size_t)((Hp + 31) >> 5);
+}
+// word offset of the three rows y - 1 .. y + 1 around pixel x (1 <= x <= Wp - 2, 1 <= y <= Hp - 2)
+__device__ inline uint32_t tb_off(int x, int y, int G) {
+  return (uint32_t)(((y >> 5) * G + (x >> 4)) * kTbRows + (y & 31));
+}
 __global__ __launch_bounds__(256) void k_tile_bits(const uint32_t* __restrict__ dbits, size_t dstride,
-                                                   uint32_t* __restrict__ tbits, size_t tstride, int wpw, int Hp) {
-  extern __shared__ uint32_t tl_band[];  // 32 rows x wpw words
-  const int f = blockIdx.y, by = blockIdx.x, t = threadIdx.x;
-  const uint32_t* src = dbits + (size_t)f * dstride + (size_t)by * 32 * wpw;
-  const int nrow = min(32, Hp - by * 32);
-  for (int i = t; i < 32 * wpw; i += 256) tl_band[i] = i < nrow * wpw ? src[i] : 0u;
+                                                   uint32_t* __restrict__ tbits, size_t tstride, int wpw, int Wp,
+                                                   int Hp) {
+  extern __shared__ uint32_t tl_band[];  // kTbRows rows x wpw words
+  const int f = blockIdx.y, ty = blockIdx.x, t = threadIdx.x;
+  const uint32_t* src = dbits + (size_t)f * dstride;
+  const int r0 = 32 * ty - 1;
+  for (int i = t; i < kTbRows * wpw; i += 256) {
+    const int e = i / wpw, r = r0 + e;
+    tl_band[i] = r >= 0 && r < Hp ? src[(size_t)r * wpw + (i - e * wpw)] : 0u;
+  }
   __syncthreads();
-  uint64_t* dst = (uint64_t*)(tbits + (size_t)f * tstride) + (size_t)by * wpw * 32;
-  for (int o = t; o < 32 * wpw; o += 256) {
-    const int r = o & 31, w = o >> 5;
-    const uint32_t lo = tl_band[r * wpw + w], hi = w + 1 < wpw ? tl_band[r * wpw + w + 1] : 0u;
-    dst[o] = (uint64_t)lo | ((uint64_t)hi << 32);
+  const int G = tb_groups(Wp);
+  uint32_t* dst = tbits + (size_t)f * tstride + (size_t)ty * G * kTbRows;
+  for (int o = t; o < G * kTbRows; o += 256) {
+    const int g = o / kTbRows, e = o - g * kTbRows;
+    const int p = 16 * g - 8, w = p >> 5, sh = p & 31;  // sh is 8 or 24
+    const uint32_t lo = w >= 0 ? tl_band[e * wpw + w] : 0u, hi = w + 1 < wpw ? tl_band[e * wpw + w + 1] : 0u;
+    dst[o] = (lo >> sh) | (hi << (32 - sh));
   }
 }
 struct BitsTiled {
-  const uint64_t* __restrict__ b;
-  int wpw;
-  __device__ uint32_t row3(int x, int y) const {
-    const uint64_t v = b[((size_t)(y >> 5) * wpw + ((x - 1) >> 5)) * 32 + (y & 31)];
-    return (uint32_t)(v >> ((x - 1) & 31)) & 7u;
+  const uint32_t* __restrict__ b;
+  int G;
+  __device__ uint32_t operator()(int x, int y) const {
+    const uint32_t* p = b + tb_off(x, y, G);
+    const int sh = (x & 15) + 7;
+    return nb8_from_rows((p[0] >> sh) & 7u, (p[1] >> sh) & 7u, (p[2] >> sh) & 7u);
   }
-  __device__ uint32_t operator()(int x, int y) const { return nb8_from_rows(row3(x, y - 1), row3(x, y), row3(x, y + 1)); }
 };
 
 // trace_border_lut as a resumable walk (one step per call), so a lane whose
@@ -2686,20 +2696,15 @@ __device__ inline void seg_begin(const NB& nb, const Border& b, int Wp, uint32_t
 // words per row); false once the segment ended: nx = the next segment's
 // checkpoint id, -1 when the border closed
 template <class EM>
-__device__ inline bool walk_step(const uint64_t* __restrict__ tb, int wpw32, const uint8_t* lut, EM& em, Walk& w,
+__device__ inline bool walk_step(const uint32_t* __restrict__ tb, int G, const uint8_t* lut, EM& em, Walk& w,
                                  int M, const int32_t* r, const uint16_t* X, const int32_t* rowbase, int& nx) {
   const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
-  const int xm = x - 1, col = xm & ~31, sh = xm & 31;
-  const char* base = (const char*)tb;
-  const int rr = y & 31, t0 = (y >> 5) * wpw32 + col, om = t0 + rr;
-  const uint32_t off[3] = {(uint32_t)(rr == 0 ? t0 - wpw32 + 31 : om - 1), (uint32_t)om,
-                           (uint32_t)(rr == 31 ? t0 + wpw32 : om + 1)};
-  uint32_t p9 = 0;
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const uint64_t v = *(const uint64_t*)(base + (off[k] << 3));
-    p9 |= ((uint32_t)(v >> sh) & 7u) << (3 * k);
-  }
+  // rows y - 1 .. y + 1 as three consecutive words: one 12-byte load (scalar
+  // base + 32-bit byte offset)
+  typedef unsigned int u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+  const u32x3a v = *(const __attribute__((address_space(1))) u32x3a*)((const char*)tb + (tb_off(x, y, G) << 2));
+  const int sh = (x & 15) + 7;
+  const uint32_t p9 = ((v.x >> sh) & 7u) | (((v.y >> sh) & 7u) << 3) | (((v.z >> sh) & 7u) << 6);
   const int s = lut[(p9 << 3) | w.s];
   if (M > 0 && !w.first && y % M == 0) {
     const bool west = arc_has(w.s, s, 4);
@@ -2943,7 +2948,7 @@ __global__ __launch_bounds__(64 * MK_TB_WAVES) void k_trace_borders(const uint32
   const int NC = st[f].seg_nc, M = st[f].seg_m, NS = NC + nb;
   const int32_t* r = rowb + (size_t)f * rstride;
   const uint16_t* X = rx + (size_t)f * plane;
-  const BitsTiled nbh{(const uint64_t*)B, wpw};
+  const BitsTiled nbh{B, tb_groups(Wp)};
   int32_t* smax = &st[f].trace_steps_max;
   ChunkEmit em{chunks, owner, ordv, ccount, &st[f].n_chunks, max_chunks, 0, -1, 0, 0, false};
   Walk w;
@@ -3000,7 +3005,7 @@ __global__ __launch_bounds__(64 * MK_TB_WAVES) void k_trace_borders(const uint32
       continue;
     }
     int nx = -1;
-    if (act && !walk_step(nbh.b, 32 * wpw, next_lut, em, w, M, r, X, T.rowbase, nx)) {
+    if (act && !walk_step(nbh.b, nbh.G, next_lut, em, w, M, r, X, T.rowbase, nx)) {
       act = false;
       finish(nx);
     }
@@ -4232,7 +4237,11 @@ __device__ inline int color_row_run(const uint8_t* bgr, long lin0) {
   const uint32_t m = (uint32_t)(b & 3);
   typedef __attribute__((address_space(1), aligned(4))) const cu32x4 gu4a;
   const uint8_t* a = bgr + (b - m);
-  return color_row_words(*(gu4a*)a, *(gu4a*)(a + 16), *(gu32*)(a + 32), m);
+  // the ninth dword only when the row starts at byte 3 of its first dword
+  // (bytes m + 28, m + 29 are the last ones used: inside the first eight for m <= 2)
+  uint32_t d8 = 0u;
+  if (m == 3u) d8 = *(gu32*)(a + 32);
+  return color_row_words(*(gu4a*)a, *(gu4a*)(a + 16), d8, m);
 }
 __device__ inline void wave_score_color(const Xf& c2w, const double* green, int ngr, const Cam& cm,
                                         const uint8_t* bgr, int W, int H, ColorLds* cl, double* err_out,

@@ -126,15 +126,13 @@ def test_morphology_kernels_bit_exact(walk, trace_lds):
     binary and cleanImageByEdge mask, and the contours that follow against
     findContours: widths ending mid-word, segments shorter than the 29-row
     reach, frames shorter than it, blob noise and i.i.d. noise. With
-    MANTIS_TRACE_LDS_FRAMES=0 the borders are walked on the tiled plane in L2,
-    which the walker writes as it goes (MANTIS_WALK_TILES=1) and k_tile_bits
-    after k_morph."""
+    MANTIS_TRACE_LDS_FRAMES=0 the borders are walked on the tiled plane in L2
+    (k_tile_bits' 16-pixel-group windows of three rows)."""
     import mantis_amd as M
 
     env = {"MANTIS_MORPH_WALK": walk}
-    if trace_lds is not None:  # the L2 walker on the tiled plane, written by the morphology walker
+    if trace_lds is not None:  # the L2 walker on the tiled plane
         env["MANTIS_TRACE_LDS_FRAMES"] = trace_lds
-        env["MANTIS_WALK_TILES"] = "1"
     saved = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

@@ -9,7 +9,7 @@ path (ADVICE / VERDICT r05 weak item 6).
 
 Switches tested elsewhere: MANTIS_OP_LANES_SMALL / _ROUNDS_SMALL
 (test_small_batch_objpose_queue_settings), MANTIS_CANNY_STRIP, MANTIS_MORPH_WALK,
-MANTIS_TRACE_LDS_FRAMES, MANTIS_WALK_TILES, MANTIS_SEG_M, MANTIS_SCREEN
+MANTIS_TRACE_LDS_FRAMES, MANTIS_SEG_M, MANTIS_SCREEN
 (test_gpu_parity.py), MANTIS_PF_MASK_GLOBAL (test_gpu_pipeline.py),
 MANTIS_HYST_REC, MANTIS_HYST_EPOCH0 (test_hysteresis.py).
 """
