@@ -190,7 +190,8 @@ struct Ctx {
 #ifndef MK_SHIFT_SPLIT
 #define MK_SHIFT_SPLIT 0
 #endif
-  bool shift_split = MK_SHIFT_SPLIT;  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
+  bool shift_split = MK_SHIFT_SPLIT;
+  bool pf_shifts = true;  // large batches: the 81 shifts at the end of k_score_pf (MANTIS_PF_SHIFTS)  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
   bool canny_cat = true;  // k_canny_strip<2> over the frames side by side where W % 32 == 0 (MANTIS_CANNY_CAT=0: per frame)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
@@ -742,6 +743,9 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   // iteration's launch, so a config without iterations runs the one-block kernel
   const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles &&
                      c->cfg.iterations > 0;
+  // large batches: the 81 shifts scored at the end of k_score_pf, the frame's
+  // mask still in LDS (pf_shifts; MANTIS_PF_SHIFTS=0: in k_score_final)
+  const bool pf_shifts = !split && c->pf_shifts;
   if (split) {
     const int nblk = (c->cfg.particles + ppb - 1) / ppb;
     for (int it = 0; it < c->cfg.iterations; it++)
@@ -751,16 +755,16 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   } else if (ml)
     k_score_pf<kPfThreads, kPfSplit, true><<<n, kPfThreads, ml, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-        c->cfg.iterations);
+        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9);
   else
     k_score_pf<kPfThreads, kPfSplit, false><<<n, kPfThreads, 0, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-        c->cfg.iterations);
+        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9);
   mark(c, "score_pf_yaw/k_score_pf");
   // the 81 shifts over several blocks per frame first (small batches; large
   // ones with shift_split: the shift tasks in a lean kernel instead of beside
   // k_score_final's sorting, COLOR and publishing code)
-  const bool shifts_apart = split || c->shift_split;
+  const bool shifts_apart = !pf_shifts && (split || c->shift_split);
   if (shifts_apart) {
     constexpr int spb = kScoreTail / 128;
     k_score_shift_part<kScoreTail><<<dim3((81 + spb - 1) / spb, n), kScoreTail, 0, c->s>>>(
@@ -768,7 +772,7 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
     mark(c, "score_pf_yaw/k_score_shift_part");
   }
   k_score_final<kScoreTail><<<n, kScoreTail, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_res, c->d_dbg,
-                                               c->d_sst, c->cfg.grid_spacing, 9, shifts_apart);
+                                               c->d_sst, c->cfg.grid_spacing, 9, shifts_apart || pf_shifts);
   mark(c, "score_pf_yaw/k_score_final");
   HIP_OK(hipGetLastError());
   return MANTIS_OK;
@@ -1113,6 +1117,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_SHIFT_SPLIT")) c->shift_split = e[0] != '0';
+  if (const char* e = std::getenv("MANTIS_PF_SHIFTS")) c->pf_shifts = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   {
     // graph replays need the HIP runtime's AQL packet capture of graphs off

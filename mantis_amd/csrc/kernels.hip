@@ -4848,6 +4848,23 @@ __global__ __launch_bounds__(NT) void k_score_init(
   }
 }
 
+// computeAllShiftedHypothesesFAST (HypothesisEvaluation.h): the 9 x 9 grid of
+// translations of the optimum by whole grid cells
+__device__ inline void shift_values(int grid_size, double grid_spacing, double* shv) {
+  double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
+  int k = 0;
+  for (; x < ((double)grid_size / 2.0) * grid_spacing && k < 9; x += grid_spacing) shv[k++] = x;
+}
+__device__ inline void shift_pose(const Xf& w2c, const double* shv, int j, PoseLds& o) {
+  Xf nw = w2c;
+  nw.t[0] += shv[j / 9];
+  nw.t[1] += shv[j % 9];
+  nw.t[2] += 0.0;
+  Hyp h;
+  hyp_set_w2c(h, nw);
+  o.c2w = h.c2w; o.w2c = h.w2c; o.q = h.q;
+}
+
 // particle pose of the six gaussians g6 around the current pose
 __device__ inline void pf_particle(const Xf& cur_w2c, const float* g6, Xf& w2c, Xf& c2w) {
   double yaw = (double)g6[0] * 0.03, pitch = (double)g6[1] * 0.03, roll = (double)g6[2] * 0.03;
@@ -4867,7 +4884,8 @@ template <int NT, int SPLIT, bool LM>
 __global__ __launch_bounds__(NT) void k_score_pf(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
-    FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations) {
+    FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations, int shifts, double grid_spacing,
+    int grid_size) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (!st[f].reaches_pf) return;
@@ -5013,6 +5031,63 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     D.pf_err = cur_err;
     res[f].pf_error = cur_err;
   }
+  if (!shifts) return;
+  // shifts (round 6): the 81 shifted hypotheses of k_score_final scored here,
+  // while the frame's mask is still in LDS (lookups by ds_read instead of L2
+  // gathers); their integer sums and counts go to ScoreState, where
+  // k_score_final (pre) takes them, as after k_score_shift_part. Same poses
+  // (shift_pose of the same optimum), same sums.
+  constexpr int NS = 81;
+  static_assert(NS <= 96, "shift poses in the particle arrays");
+  __shared__ double shv[9];
+  if (tid == 0) {
+    uqn = 0;
+    shift_values(grid_size, grid_spacing, shv);
+  }
+  __syncthreads();
+  if (tid < NS) {
+    PoseLds o;
+    shift_pose(cur_w2c, shv, tid, o);
+    Pc[tid] = o.c2w;
+    Pf[tid] = posef_from(o.c2w);
+  }
+  for (int i = tid; i < NS * SPLIT; i += NT) {
+    Ps[i] = 0;
+    Pn[i] = 0;
+  }
+  __syncthreads();
+  for (int task = __builtin_amdgcn_readfirstlane(wave); task < NS * SPLIT; task += kW) {
+    const int j = task / SPLIT;
+    long long sum;
+    int cnt;
+    if (LM) wl.sums(Pf[j], fd.scam, W, H, fd.bgr, mlds, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+    else wl.sums(Pf[j], fd.scam, W, H, fd.bgr, mglb, q, j, &Pc[j], lmk.xyz, &frames[f].cam, sum, cnt);
+    if (lane == 0) {
+      Ps[task] = (unsigned long long)sum;
+      Pn[task] = cnt;
+    }
+  }
+  __syncthreads();
+  {
+    const auto pose_of = [&](int t) -> const Xf& { return Pc[t]; };
+    const auto add = [&](int t, int e) {
+      atomicAdd(&Ps[t * SPLIT], (unsigned long long)e);
+      atomicAdd(&Pn[t * SPLIT], 1);
+    };
+    if (LM) block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mlds, pose_of, add);
+    else block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mglb, pose_of, add);
+  }
+  __syncthreads();
+  if (tid < NS) {
+    long long sum = 0;
+    int cnt = 0;
+    for (int h = 0; h < SPLIT; h++) {
+      sum += (long long)Ps[tid * SPLIT + h];
+      cnt += Pn[tid * SPLIT + h];
+    }
+    sst[f].psum[tid] = sum;
+    sst[f].pcnt[tid] = cnt;
+  }
 }
 
 // One iteration of the particle filter spread over `nblk` blocks per frame
@@ -5132,21 +5207,6 @@ __global__ __launch_bounds__(NT) void k_score_pf_part(
 
 // computeAllShiftedHypothesesFAST's shift values (accumulated in double as the
 // reference loop does) and shifted pose j = (j / 9, j % 9) of the optimum
-__device__ inline void shift_values(int grid_size, double grid_spacing, double* shv) {
-  double x = -((double)grid_size / 2.0) * grid_spacing + ((double)grid_spacing / 2.0);
-  int k = 0;
-  for (; x < ((double)grid_size / 2.0) * grid_spacing && k < 9; x += grid_spacing) shv[k++] = x;
-}
-__device__ inline void shift_pose(const Xf& w2c, const double* shv, int j, PoseLds& o) {
-  Xf nw = w2c;
-  nw.t[0] += shv[j / 9];
-  nw.t[1] += shv[j % 9];
-  nw.t[2] += 0.0;
-  Hyp h;
-  hyp_set_w2c(h, nw);
-  o.c2w = h.c2w; o.w2c = h.w2c; o.q = h.q;
-}
-
 // The 81 shifted hypotheses' screened sums spread over `nblk` blocks per frame
 // (small batches): block b takes shifts [b * spb, (b+1) * spb), one task per
 // (shift, landmark half), drains its own unsure landmarks, and writes each

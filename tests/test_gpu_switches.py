@@ -105,6 +105,7 @@ LARGE = [("MANTIS_RPP_BLOCKS", "8"),          # a small persistent ObjPose grid:
          ("MANTIS_FC_SMALL_FRAMES", "100000"),  # the latency kernels on an 80-frame batch
          ("MANTIS_PF_SPLIT", "0"),            # (no effect on a large batch)
          ("MANTIS_CANNY_CAT", "0"),           # Canny strips per frame instead of over the frames side by side
+         ("MANTIS_PF_SHIFTS", "0"),           # the 81 shifts in k_score_final instead of at the end of k_score_pf
          ("MANTIS_SHIFT_SPLIT", "1"),         # the 81 shifts in k_score_shift_part blocks
          ("MANTIS_SHIFT_SPLIT", "0")]
 
