@@ -191,7 +191,9 @@ struct Ctx {
 #define MK_SHIFT_SPLIT 0
 #endif
   bool shift_split = MK_SHIFT_SPLIT;
-  bool pf_shifts = true;  // large batches: the 81 shifts at the end of k_score_pf (MANTIS_PF_SHIFTS)  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
+  bool pf_shifts = true;  // large batches: the 81 shifts at the end of k_score_pf (MANTIS_PF_SHIFTS)
+  int pf_init = 1;  // large batches: k_score_init's work at the start of k_score_pf (MANTIS_PF_INIT; 2: its
+                   // per-hypothesis arrays in global scratch, as for more hypotheses than its LDS buffer takes)  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
   bool canny_cat = true;  // k_canny_strip<2> over the frames side by side where W % 32 == 0 (MANTIS_CANNY_CAT=0: per frame)
   bool counted = false;  // included in g_live_ctx
   bool vec_ok = false;
@@ -729,9 +731,17 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   }
   mark(c, "gauss_h2d");
   Landmarks L = lmk_of(c);
-  k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps, c->d_res,
-                                              c->d_dbg, c->d_sst);
-  mark(c, "score_pf_yaw/k_score_init");
+  const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles &&
+                     c->cfg.iterations > 0;
+  // large batches: k_score_init's work at the start of k_score_pf (pf_init), the
+  // 81 shifts at its end (pf_shifts), both with the frame's mask in LDS
+  const bool pf_shifts = !split && c->pf_shifts;
+  const int pf_init = split ? 0 : c->pf_init;
+  if (!pf_init) {
+    k_score_init<kScoreInit><<<n, kScoreInit, 0, c->s>>>(c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_hyps,
+                                                        c->d_res, c->d_dbg, c->d_sst);
+    mark(c, "score_pf_yaw/k_score_init");
+  }
   // particle filter: 16 waves per frame, each task one particle over a
   // 1/kPfSplit slice of the landmarks (the integer partial sums combine
   // exactly); the frame's mask plane goes to LDS when it fits (pf_mask_lds > 0:
@@ -741,11 +751,6 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   // small batches split the filter's iterations over blocks (MANTIS_PF_SPLIT); the
   // end-of-filter writes (pf_error, the filter's pose) belong to the last
   // iteration's launch, so a config without iterations runs the one-block kernel
-  const bool split = c->pf_split && n <= c->fc_small_frames && c->cfg.particles <= kPfMaxParticles &&
-                     c->cfg.iterations > 0;
-  // large batches: the 81 shifts scored at the end of k_score_pf, the frame's
-  // mask still in LDS (pf_shifts; MANTIS_PF_SHIFTS=0: in k_score_final)
-  const bool pf_shifts = !split && c->pf_shifts;
   if (split) {
     const int nblk = (c->cfg.particles + ppb - 1) / ppb;
     for (int it = 0; it < c->cfg.iterations; it++)
@@ -755,11 +760,13 @@ mantis_status run_score(Ctx* c, int n, int n_gauss, bool copy_gauss = true) {
   } else if (ml)
     k_score_pf<kPfThreads, kPfSplit, true><<<n, kPfThreads, ml, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9);
+        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9, pf_init, c->d_hyps,
+        (unsigned char*)c->d_gen);
   else
     k_score_pf<kPfThreads, kPfSplit, false><<<n, kPfThreads, 0, c->s>>>(
         c->d_frames, c->d_mbits, c->bstride, L, c->d_st, c->d_gauss, c->d_res, c->d_dbg, c->d_sst, c->cfg.particles,
-        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9);
+        c->cfg.iterations, pf_shifts ? 1 : 0, c->cfg.grid_spacing, 9, pf_init, c->d_hyps,
+        (unsigned char*)c->d_gen);
   mark(c, "score_pf_yaw/k_score_pf");
   // the 81 shifts over several blocks per frame first (small batches; large
   // ones with shift_split: the shift tasks in a lean kernel instead of beside
@@ -1118,6 +1125,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_SHIFT_SPLIT")) c->shift_split = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_PF_SHIFTS")) c->pf_shifts = e[0] != '0';
+  if (const char* e = std::getenv("MANTIS_PF_INIT")) c->pf_init = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   {
     // graph replays need the HIP runtime's AQL packet capture of graphs off

@@ -4715,75 +4715,55 @@ __device__ inline Xf rfl(const Xf& T) {
   return u;
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_score_init(
-    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
-    FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
-    ScoreState* __restrict__ sst) {
-  const int f = blockIdx.x;
+// A frame that returns before scoring (no quadrilaterals / no hypotheses,
+// src/mantis3.cpp:82-97): its result record
+__device__ inline void score_early_result(const FrameState& s, mantis_cam_result& R, FrameDebug& D) {
+  R.status = 0;
+  R.reason = s.n_quads == 0 ? MANTIS_NO_QUADS : MANTIS_NO_HYPS;
+  R.publish = 0;
+  R.n_quads = s.n_quads;
+  R.n_hyps = s.n_hyps;
+  R.n_scored = 0;
+  D.reason = R.reason;
+  D.publish = 0;
+}
+
+// evaluateHypotheses(C hyps) + getBestNHypotheses(1) of one frame, by the
+// whole block (k_score_init, or k_score_pf taking the init itself): screened
+// tasks (hypothesis, landmark half; a wave's half in wl), the unsure
+// landmarks exactly, errors and debug records, the best one by a unique-
+// minimum reduction or, on ties, the libstdc++-order sort. ei / hs / hn hold
+// C entries (LDS, or global scratch for more hypotheses than the LDS takes);
+// the first npfi hypotheses' screen poses are staged in pfi. Leaves the best
+// in cur (and sst), the scored count in nsc. Ends on a barrier.
+template <int NT, class MK>
+__device__ inline void block_score_init(const FrameDesc& fd, const Cam* cmp, const MK& mask, const Landmarks& lmk,
+                                        const WaveLms<kScrUnroll>& wl, HypRec* Hh, int C, FrameDebug& D, ErrIdx* ei,
+                                        unsigned long long* hs, int32_t* hn, PoseF* pfi, int npfi, UQueue q,
+                                        int32_t* uqn, PoseLds& cur, int32_t& nsc, int32_t& uniq_bi, ScoreState& S) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
-  const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(H), W};
-  mantis_cam_result& R = res[f];
-  FrameDebug& D = dbg[f];
-  const int nl = lmk.nw + lmk.nr + lmk.ng;
-  __shared__ float4 lmf[768];
-  __shared__ ErrIdx ei[kMaxHyps];
-  __shared__ unsigned long long hs[kMaxHyps];  // per hypothesis: integer error sum, count
-  __shared__ int32_t hn[kMaxHyps];
-  __shared__ uint32_t uqe[kInitQueue];
-  __shared__ int32_t uqn;
-  __shared__ PoseLds cur;
-  __shared__ int32_t nsc;
-  if (!st[f].reaches_pf) {
-    if (tid == 0) {
-      R.status = 0;
-      R.reason = st[f].n_quads == 0 ? MANTIS_NO_QUADS : MANTIS_NO_HYPS;
-      R.publish = 0;
-      R.n_quads = st[f].n_quads;
-      R.n_hyps = st[f].n_hyps;
-      R.n_scored = 0;
-      D.reason = R.reason;
-      D.publish = 0;
-    }
-    return;
-  }
-  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
-  if (tid == 0) uqn = 0;
-  __syncthreads();
-  HypRec* Hh = hyps + (size_t)f * kMaxHyps;
-  const int C = st[f].n_hyps;
-  // evaluateHypotheses(hyps, cleaned): screened pass, then the unsure landmarks exactly
-  const UQueue q{uqe, &uqn, kInitQueue};
-  // tasks = (hypothesis, half of the landmarks), a wave's half in registers
-  // (as in the particle filter and the shifts); the halves' sums add exactly
-  // the first kInitPoses hypotheses' screen poses staged in LDS once (a task
-  // then reads its pose from LDS instead of global memory)
-  constexpr int kInitPoses = 128;
-  __shared__ PoseF pfi[kInitPoses];
+  if (tid == 0) *uqn = 0;
   for (int h = tid; h < C; h += NT) {
     hs[h] = 0;
     hn[h] = 0;
-    if (h < kInitPoses) pfi[h] = posef_from(Hh[h].c2w);
+    if (h < npfi) pfi[h] = posef_from(Hh[h].c2w);
   }
   __syncthreads();
-  static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
-  WaveLms<kScrUnroll> wl;
-  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
+  // tasks = (hypothesis, half of the landmarks); the halves' sums add exactly
   for (int t = __builtin_amdgcn_readfirstlane(wave); t < 2 * C; t += (NT / 64)) {
     const int h = t >> 1;
     long long s;
     int n;
-    const PoseF P = h < kInitPoses ? pfi[h] : posef_from(Hh[h].c2w);
-    wl.sums(P, fd.scam, W, H, fd.bgr, mask, q, h, &Hh[h].c2w, lmk.xyz, &frames[f].cam, s, n);
+    const PoseF P = h < npfi ? pfi[h] : posef_from(Hh[h].c2w);
+    wl.sums(P, fd.scam, W, H, fd.bgr, mask, q, h, &Hh[h].c2w, lmk.xyz, cmp, s, n);
     if (lane == 0) {
       atomicAdd(&hs[h], (unsigned long long)s);
       atomicAdd(&hn[h], n);
     }
   }
   __syncthreads();
-  block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return Hh[t].c2w; },
+  block_drain(q, lmk.xyz, cmp, W, H, fd.bgr, mask, [&](int t) -> const Xf& { return Hh[t].c2w; },
               [&](int t, int e) {
                 atomicAdd(&hs[t], (unsigned long long)e);
                 atomicAdd(&hn[t], 1);
@@ -4805,7 +4785,6 @@ __global__ __launch_bounds__(NT) void k_score_init(
   // getBestNHypotheses(1): std::sort, keep back(). When the minimum error is
   // unique, back() is that element whatever the sort's tie order, so wave 0
   // finds it with a reduction and the serial sort runs only on ties.
-  __shared__ int32_t uniq_bi;
   if (wave == 0) {
     double be = DBL_MAX;
     int bj = 0x7fffffff, cnt = 0;
@@ -4839,13 +4818,47 @@ __global__ __launch_bounds__(NT) void k_score_init(
     D.best1_err = cur.err;
     D.pf_iter_err[0] = cur.err;
     nsc = C + 1;
+    S.cur = cur;
+    S.nsc = nsc;
+    S.ctr = 0;
   }
   __syncthreads();
-  if (tid == 0) {
-    sst[f].cur = cur;
-    sst[f].nsc = nsc;
-    sst[f].ctr = 0;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_score_init(
+    const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
+    FrameState* st, HypRec* __restrict__ hyps, mantis_cam_result* __restrict__ res, FrameDebug* dbg,
+    ScoreState* __restrict__ sst) {
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const FrameDesc fd = frames[f];
+  const MaskBits mask{mbits + (size_t)f * bstride, bits::tiled_rows(fd.h), fd.w};
+  FrameDebug& D = dbg[f];
+  const int nl = lmk.nw + lmk.nr + lmk.ng;
+  __shared__ float4 lmf[768];
+  __shared__ ErrIdx ei[kMaxHyps];
+  __shared__ unsigned long long hs[kMaxHyps];  // per hypothesis: integer error sum, count
+  __shared__ int32_t hn[kMaxHyps];
+  __shared__ uint32_t uqe[kInitQueue];
+  __shared__ int32_t uqn;
+  __shared__ PoseLds cur;
+  __shared__ int32_t nsc, uniq_bi;
+  // the first kInitPoses hypotheses' screen poses staged in LDS once (a task
+  // then reads its pose from LDS instead of global memory)
+  constexpr int kInitPoses = 128;
+  __shared__ PoseF pfi[kInitPoses];
+  if (!st[f].reaches_pf) {
+    if (tid == 0) score_early_result(st[f], res[f], D);
+    return;
   }
+  for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
+  __syncthreads();
+  static_assert((NT / 64) % 2 == 0 && 64 * kScrUnroll * 2 >= 768, "one register trip per half");
+  WaveLms<kScrUnroll> wl;
+  wl.load(lmf, nl * (wave & 1) / 2, nl * ((wave & 1) + 1) / 2);
+  block_score_init<NT>(fd, &frames[f].cam, mask, lmk, wl, hyps + (size_t)f * kMaxHyps, st[f].n_hyps, D, ei, hs, hn,
+                       pfi, kInitPoses, UQueue{uqe, &uqn, kInitQueue}, &uqn, cur, nsc, uniq_bi, sst[f]);
 }
 
 // computeAllShiftedHypothesesFAST (HypothesisEvaluation.h): the 9 x 9 grid of
@@ -4885,10 +4898,13 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     const FrameDesc* __restrict__ frames, const uint32_t* __restrict__ mbits, size_t bstride, Landmarks lmk,
     const FrameState* __restrict__ st, const float* __restrict__ gauss, mantis_cam_result* __restrict__ res,
     FrameDebug* dbg, ScoreState* __restrict__ sst, int particles, int iterations, int shifts, double grid_spacing,
-    int grid_size) {
+    int grid_size, int init, HypRec* __restrict__ hyps, unsigned char* __restrict__ init_scratch) {
   const int f = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if (!st[f].reaches_pf) return;
+  if (!st[f].reaches_pf) {
+    if (init && tid == 0) score_early_result(st[f], res[f], dbg[f]);
+    return;
+  }
   const FrameDesc fd = frames[f];
   const int W = fd.w, H = fd.h;
   const uint32_t* fm = mbits + (size_t)f * bstride;
@@ -4903,18 +4919,24 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   FrameDebug& D = dbg[f];
   const int nl = lmk.nw + lmk.nr + lmk.ng;
   __shared__ float4 lmf[768];
-  __shared__ Xf Pc[96], Pw[96];
-  __shared__ PoseF Pf[96];
-  __shared__ double Pe[96];
-  __shared__ unsigned long long Ps[96 * SPLIT];
-  __shared__ int32_t Pn[96 * SPLIT];
+  // the particles' poses and sums (Pc, Pw, Pf, Pe, Ps, Pn) in one buffer, which
+  // the init phase (init: k_score_init's work done here, the mask already in
+  // LDS) uses first for its per-hypothesis errors, sums and counts
+  constexpr int kPfBuf = 96 * (2 * (int)sizeof(Xf) + (int)sizeof(PoseF) + 8 + SPLIT * 12);
+  __shared__ __align__(16) unsigned char pbuf[kPfBuf];
+  Xf* Pc = (Xf*)pbuf;
+  Xf* Pw = Pc + 96;
+  PoseF* Pf = (PoseF*)(Pw + 96);
+  double* Pe = (double*)(Pf + 96);
+  unsigned long long* Ps = (unsigned long long*)(Pe + 96);
+  int32_t* Pn = (int32_t*)(Ps + 96 * SPLIT);
   __shared__ uint32_t uqe[kPfQueue];
   __shared__ int32_t uqn;
   constexpr int kW = NT / 64;
   __shared__ Xf cur_c2w, cur_w2c;
   __shared__ double cur_err;
   for (int i = tid; i < nl; i += blockDim.x) lmf[i] = lmk.xyzf[i];
-  if (tid == 0) {
+  if (tid == 0 && !init) {
     cur_c2w = sst[f].cur.c2w;
     cur_w2c = sst[f].cur.w2c;
     cur_err = sst[f].cur.err;
@@ -4945,6 +4967,35 @@ __global__ __launch_bounds__(NT) void k_score_pf(
   {
     const int h = wave % SPLIT;
     wl.load(lmf, nl * h / SPLIT, nl * (h + 1) / SPLIT);
+  }
+  if (init) {
+    // evaluateHypotheses + getBestNHypotheses(1) (k_score_init's block
+    // function) with the mask lookups from LDS; the init's landmark halves are
+    // the particle tasks' slices (SPLIT == 2)
+    static_assert(SPLIT == 2, "the init tasks use landmark halves");
+    __shared__ PoseLds icur;
+    __shared__ int32_t insc, iuniq;
+    const int C = st[f].n_hyps;
+    HypRec* Hh = hyps + (size_t)f * kMaxHyps;
+    constexpr int kPer = (int)(sizeof(ErrIdx) + sizeof(unsigned long long) + sizeof(int32_t));
+    const auto run = [&](unsigned char* buf) {
+      ErrIdx* ei = (ErrIdx*)buf;
+      unsigned long long* hs = (unsigned long long*)(ei + C);
+      int32_t* hn = (int32_t*)(hs + C);
+      const UQueue qi{uqe, &uqn, kPfQueue};
+      if (LM) block_score_init<NT>(fd, &frames[f].cam, mlds, lmk, wl, Hh, C, D, ei, hs, hn, nullptr, 0, qi, &uqn,
+                                   icur, insc, iuniq, sst[f]);
+      else block_score_init<NT>(fd, &frames[f].cam, mglb, lmk, wl, Hh, C, D, ei, hs, hn, nullptr, 0, qi, &uqn, icur,
+                                insc, iuniq, sst[f]);
+    };
+    if (C * kPer <= kPfBuf && init != 2) run(pbuf);  // init == 2 (tests): the global-scratch path
+    else run(init_scratch + (size_t)f * kMaxHyps * kPer);  // more hypotheses than the LDS buffer takes: global scratch
+    if (tid == 0) {
+      cur_c2w = icur.c2w;
+      cur_w2c = icur.w2c;
+      cur_err = icur.err;
+    }
+    __syncthreads();
   }
   for (int it = 0; it < iterations; it++) {
     if (tid < particles) {
