@@ -4997,17 +4997,33 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     }
     __syncthreads();
   }
+  // the frame's gaussians in LDS (round 6): the landmark table's bytes, free
+  // once every wave holds its slice (wl) -- the particle phase then reads them
+  // by ds_read instead of a global round trip per iteration
+  const int ngs = particles * iterations * 6;
+  const bool gl = ngs <= (int)(sizeof(lmf) / sizeof(float));
+  float* glds = (float*)lmf;
+  __syncthreads();
+  if (gl)
+    for (int i = tid; i < ngs; i += NT) glds[i] = gs[i];
+  const float* gsrc = gl ? (const float*)glds : gs;
+  const auto particle = [&](int it, int j, const Xf& w2c_cur) {
+    Xf w2c, c2w;
+    pf_particle(w2c_cur, gsrc + (size_t)(it * particles + j) * 6, w2c, c2w);
+    Pw[j] = w2c;
+    Pc[j] = c2w;
+    Pf[j] = posef_from(c2w);
+  };
+  __syncthreads();
+  if (iterations > 0)
+    for (int j = tid; j < particles; j += NT) particle(0, j, cur_w2c);
+  if (tid == 0) uqn = 0;
+  __syncthreads();
+  MK_PTICK(1);
+  // each iteration: tasks, the unsure landmarks, then wave 0 alone: the
+  // particles' errors, the first strict minimum, the current pose, and the
+  // next iteration's particles (three barriers an iteration; round 5 had five)
   for (int it = 0; it < iterations; it++) {
-    if (tid < particles) {
-      Xf w2c, c2w;
-      pf_particle(cur_w2c, gs + (size_t)(it * particles + tid) * 6, w2c, c2w);
-      Pw[tid] = w2c;
-      Pc[tid] = c2w;
-      Pf[tid] = posef_from(c2w);
-    }
-    if (tid == 0) uqn = 0;
-    __syncthreads();
-    MK_PTICK(1);
     // SPLIT waves per particle (landmark slices; integer sums, so the
     // partials combine exactly in any order); a wave's tasks pipelined
     for (int task = __builtin_amdgcn_readfirstlane(wave); task < particles * SPLIT; task += kW) {
@@ -5032,35 +5048,40 @@ __global__ __launch_bounds__(NT) void k_score_pf(
     else block_drain(q, lmk.xyz, &frames[f].cam, W, H, fd.bgr, mglb, pose_of, add);
     __syncthreads();
     MK_PTICK(3);
-    if (tid < particles) {
-      long long sum = 0;
-      int cnt = 0;
-      for (int h = 0; h < SPLIT; h++) {
-        sum += (long long)Ps[tid * SPLIT + h];
-        cnt += Pn[tid * SPLIT + h];
-      }
-      Pe[tid] = cnt <= 0 ? DBL_MAX : (double)sum / ((double)cnt * 1.1);
-    }
-    __syncthreads();
-    MK_PTICK(4);
     if (wave == 0) {
       double be = DBL_MAX;
       int bj = 0x7fffffff;
-      for (int j = lane; j < particles; j += 64)
-        if (Pe[j] < be || bj == 0x7fffffff) { be = Pe[j]; bj = j; }
+      for (int j = lane; j < particles; j += 64) {
+        long long sum = 0;
+        int cnt = 0;
+        for (int h = 0; h < SPLIT; h++) {
+          sum += (long long)Ps[j * SPLIT + h];
+          cnt += Pn[j * SPLIT + h];
+        }
+        const double e = cnt <= 0 ? DBL_MAX : (double)sum / ((double)cnt * 1.1);
+        if (e < be || bj == 0x7fffffff) { be = e; bj = j; }
+      }
       for (int o = 32; o > 0; o >>= 1) {
         const double oe = __shfl_xor(be, o);
         const int oj = __shfl_xor(bj, o);
         if (oe < be || (oe == be && oj < bj)) { be = oe; bj = oj; }
       }
+      MK_PTICK(4);
+      // the winner (wave-uniform) read by every lane before any lane
+      // overwrites the particle arrays with the next iteration's
+      const bool upd = bj < particles && be < cur_err;
+      const Xf nw = upd ? Pw[bj] : cur_w2c;
       if (lane == 0) {
-        if (bj < particles && be < cur_err) {
+        if (upd) {
           cur_err = be;
           cur_c2w = Pc[bj];
-          cur_w2c = Pw[bj];
+          cur_w2c = nw;
         }
-        if (it + 1 < (int)(sizeof(D.pf_iter_err) / sizeof(double))) D.pf_iter_err[it + 1] = cur_err;  // the record holds 10 iterations
+        if (it + 1 < (int)(sizeof(D.pf_iter_err) / sizeof(double))) D.pf_iter_err[it + 1] = upd ? be : cur_err;  // the record holds 10 iterations
+        uqn = 0;
       }
+      if (it + 1 < iterations)
+        for (int j = lane; j < particles; j += 64) particle(it + 1, j, nw);
     }
     __syncthreads();
     MK_PTICK(5);
