@@ -191,6 +191,10 @@ struct Ctx {
 #define MK_SHIFT_SPLIT 0
 #endif
   bool shift_split = MK_SHIFT_SPLIT;
+#ifndef MK_GN_FUSED_ALL
+#define MK_GN_FUSED_ALL 1  // round 6: 29.2 / 29.3k -> 29.7 / 30.0k rig poses/s (6 contexts, A/B/A/B)
+#endif
+  bool gn_fused_all = MK_GN_FUSED_ALL;  // the rig GN as one k_rig_gn_fused launch for every batch size (MANTIS_GN_FUSED)
   bool pf_shifts = true;  // large batches: the 81 shifts at the end of k_score_pf (MANTIS_PF_SHIFTS)
   int pf_init = 1;  // large batches: k_score_init's work at the start of k_score_pf (MANTIS_PF_INIT; 2: its
                    // per-hypothesis arrays in global scratch, as for more hypotheses than its LDS buffer takes)  // large batches: the 81 shifts in k_score_shift_part blocks (MANTIS_SHIFT_SPLIT)
@@ -686,7 +690,7 @@ struct Shard {
 mantis_status gauss_offsets(Ctx* c, int n, const Shard* sh) {
   const int per = c->cfg.particles * c->cfg.iterations * 6;
   if (!sh) {
-    k_gauss_offsets<<<1, 1024, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
+    k_gauss_offsets<<<1, kGaussOffThreads, 0, c->s>>>(c->d_st, n, per, c->d_gtotal);
     HIP_OK(hipGetLastError());
     return MANTIS_OK;
   }
@@ -1125,6 +1129,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_SHIFT_SPLIT")) c->shift_split = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_PF_SHIFTS")) c->pf_shifts = e[0] != '0';
+  if (const char* e = std::getenv("MANTIS_GN_FUSED")) c->gn_fused_all = e[0] != '0';
   if (const char* e = std::getenv("MANTIS_PF_INIT")) c->pf_init = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_HYST_REC")) c->hyst_rec = e[0] != '0';
   {

@@ -309,7 +309,7 @@ mantis_status run_rig_gn(Ctx* c, const double* Tbc, int n_rigs, int cams_local, 
   // call; large ones keep the three kernels (1024 rigs: 0.62 vs 0.89 ms fused).
   // Both forms are bit-identical (the camera-sharded path always takes the
   // three kernels: test_config4_8cam_1080p_rig_and_sharded_one_rank)
-  if (!use_comm && n <= c->fc_small_frames) {
+  if (!use_comm && (n <= c->fc_small_frames || c->gn_fused_all)) {
     k_rig_gn_fused<<<n_rigs, 256, 0, c->s>>>(c->d_frames, c->d_st, c->d_quads, c->d_gncam, c->d_rigio, cams_local,
                                               c->d_gnobs, obs_cap, half, spacing, c->cfg.gn_iterations);
   } else {

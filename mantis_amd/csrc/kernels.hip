@@ -4059,10 +4059,15 @@ __global__ __launch_bounds__(256) void k_frame_hyps(const RppOut* __restrict__ r
 // prefix over frames: draws of the shared cv::RNG stream happen only for
 // frames that reach the particle filter, in frame order
 // (one 1024-thread block: per-thread serial chunk, wave scans, block scan)
-__global__ __launch_bounds__(1024) void k_gauss_offsets(FrameState* st, int nf, int per_frame, int32_t* total) {
-  __shared__ int wsum[16];
+// 256 threads (round 6; 1024 before): under the other contexts' load a
+// 16-wave block waits for a whole CU to drain (9 ms of stream time per batch in
+// the 6-context bench's gauss_h2d span), four waves fit beside them
+constexpr int kGaussOffThreads = 256;
+__global__ __launch_bounds__(kGaussOffThreads) void k_gauss_offsets(FrameState* st, int nf, int per_frame, int32_t* total) {
+  constexpr int NT = kGaussOffThreads;
+  __shared__ int wsum[NT / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int chunk = (nf + 1023) / 1024;
+  const int chunk = (nf + NT - 1) / NT;
   const int f0 = min(nf, t * chunk), f1 = min(nf, f0 + chunk);
   int mine = 0;
   for (int f = f0; f < f1; f++) mine += st[f].reaches_pf ? per_frame : 0;
@@ -4080,7 +4085,7 @@ __global__ __launch_bounds__(1024) void k_gauss_offsets(FrameState* st, int nf, 
     st[f].gauss_offset = acc;
     if (st[f].reaches_pf) acc += per_frame;
   }
-  if (t == 1023) *total = base + incl;
+  if (t == NT - 1) *total = base + incl;
 }
 
 // Camera-sharded rigs: this rank's (global frame index, reaches-PF flag) pairs,

@@ -106,6 +106,7 @@ LARGE = [("MANTIS_RPP_BLOCKS", "8"),          # a small persistent ObjPose grid:
          ("MANTIS_PF_SPLIT", "0"),            # (no effect on a large batch)
          ("MANTIS_CANNY_CAT", "0"),           # Canny strips per frame instead of over the frames side by side
          ("MANTIS_PF_SHIFTS", "0"),           # the 81 shifts in k_score_final instead of at the end of k_score_pf
+         ("MANTIS_GN_FUSED", "0"),            # the rig GN as obs / acc / step kernels instead of one fused launch
          ("MANTIS_PF_INIT", "0"),             # k_score_init launched instead of its work at the start of k_score_pf
          ("MANTIS_PF_INIT", "2"),             # that work with its per-hypothesis arrays in global scratch
          ("MANTIS_SHIFT_SPLIT", "1"),         # the 81 shifts in k_score_shift_part blocks

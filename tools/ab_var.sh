@@ -10,7 +10,7 @@ for spec in "$@"; do
   [ "$lib" = "-" ] && lib=mantis_amd/libmantis_amd.so
   envcmd=(env MANTIS_AMD_LIB="$R/$lib")
   if [ -n "$envs" ]; then IFS=, read -ra kv <<< "$envs"; envcmd+=("${kv[@]}"); fi
-  timeout -k 10 180 "${envcmd[@]}" python -u bench.py --steps 5 --warmup 2 --latency-iters 1 --no-cpu --ingest-steps 0 \
+  timeout -k 10 180 "${envcmd[@]}" python -u bench.py --steps ${BSTEPS:-5} --warmup 2 --latency-iters 1 --no-cpu --ingest-steps 0 $BARGS \
     > gpurun_out/ab/$name.json 2> gpurun_out/ab/$name.err || { echo "$name failed"; tail -3 gpurun_out/ab/$name.err; exit 1; }
   python3 -c "
 import json,sys
