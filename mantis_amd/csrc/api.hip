@@ -174,7 +174,7 @@ struct Ctx {
   // lanes (kOpFields doubles + a job id each), their counters, rounds per queue
   double* d_opool[2] = {nullptr, nullptr};
   int32_t* d_ojob[2] = {nullptr, nullptr};
-  int32_t* d_octl = nullptr;  // [2][2]: entries, next
+  int32_t* d_octl = nullptr;  // [queue][round]: entries, next (zeroed once per RPP launch sequence)
   int32_t op_cap = 0;
   int op_rounds = 6, op_spill = 32;
   // small batches (latency): ObjPose jobs per wave and rounds (MANTIS_OP_LANES_SMALL, MANTIS_OP_ROUNDS_SMALL).
@@ -612,6 +612,7 @@ unsigned objpose_blocks(const Ctx* c, size_t expected_jobs) {
 // One ObjPose queue as op_rounds launches over one grid (k_objpose_q, tail
 // compaction): round 0 serves the job list, every later round the states the
 // previous one spilled, the last runs every job to the end.
+constexpr int kOpMaxRounds = 16;  // ObjPose tail-compaction rounds per queue at most
 template <int MODE>
 mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::Refine* rf, const int32_t* jobs,
                                  RppQueue* q, FrameState* st, int paired, int lanes = 64, int rounds = 0) {
@@ -620,15 +621,17 @@ mantis_status run_objpose_rounds(Ctx* c, unsigned blocks, RppItem* items, rpp::R
   for (int r = 0; r < rounds; r++) {
     const int in = (r + 1) & 1, out = r & 1;
     OpRound rd;
-    rd.in = OpPool{c->d_opool[in], c->d_ojob[in], c->d_octl + 2 * in};
-    rd.out = OpPool{c->d_opool[out], c->d_ojob[out], c->d_octl + 2 * out};
+    // counters per (queue, round), all zeroed before the first queue (no
+    // memset launch between rounds); the data pools alternate
+    int32_t* ctl = c->d_octl + 2 * (MODE * kOpMaxRounds);
+    rd.in = OpPool{c->d_opool[in], c->d_ojob[in], ctl + 2 * (r > 0 ? r - 1 : 0)};
+    rd.out = OpPool{c->d_opool[out], c->d_ojob[out], ctl + 2 * r};
     rd.cap = c->op_cap;
     rd.first = r == 0;
     rd.last = r == rounds - 1;
     rd.spill_below = c->op_spill;
     rd.lanes = lanes;
     rd.pad = 0;
-    if (!rd.last) HIP_OK(hipMemsetAsync(rd.out.ctl, 0, 2 * sizeof(int32_t), c->s));
     k_objpose_q<MODE><<<blocks, 256, 0, c->s>>>(items, rf, jobs, q, st, paired, rd);
   }
   return MANTIS_OK;
@@ -641,6 +644,8 @@ void launch_rpp_queues(Ctx* c, RppItem* items, rpp::Refine* rf, int32_t* jobs0, 
                        RppOut* out, FrameState* st, size_t ni, size_t expected_items, const QuadRec* quads,
                        bool paired, bool small = false) {
   const int pr = paired ? 1 : 0;
+  // every (queue, round) counter pair of this launch sequence, once
+  (void)hipMemsetAsync(c->d_octl, 0, sizeof(int32_t) * 2 * 2 * kOpMaxRounds, c->s);
   // small batches: at most op_lanes_small jobs per wave, the grid sized for that
   const int lanes = small ? c->op_lanes_small : 64, rounds = small ? c->op_rounds_small : 0;
   auto blocks_for = [&](size_t jobs) {
@@ -1120,10 +1125,10 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg.device) != hipSuccess || c->n_cu < 1)
     c->n_cu = 256;
   if (const char* e = std::getenv("MANTIS_RPP_BLOCKS")) c->rpp_blocks = std::atoi(e);
-  if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(16, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_OP_ROUNDS")) c->op_rounds = std::max(1, std::min(kOpMaxRounds, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_SPILL")) c->op_spill = std::max(0, std::min(64, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_OP_LANES_SMALL")) c->op_lanes_small = std::max(1, std::min(64, std::atoi(e)));
-  if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(16, std::atoi(e)));
+  if (const char* e = std::getenv("MANTIS_OP_ROUNDS_SMALL")) c->op_rounds_small = std::max(1, std::min(kOpMaxRounds, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_SEG_M")) c->seg_m = std::max(0, std::min(4096, std::atoi(e)));
   if (const char* e = std::getenv("MANTIS_CANNY_STRIP")) c->canny_strip = c->canny_small = std::atoi(e);
   if (const char* e = std::getenv("MANTIS_CANNY_CAT")) c->canny_cat = e[0] != '0';
@@ -1254,7 +1259,7 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
       chk(dalloc(c, &c->d_opool[k], (size_t)kOpFields * c->op_cap));
       chk(dalloc(c, &c->d_ojob[k], (size_t)c->op_cap));
     }
-    chk(dalloc(c, &c->d_octl, 4));
+    chk(dalloc(c, &c->d_octl, 2 * 2 * kOpMaxRounds));
   }
   chk(dalloc(c, &c->d_gen, (size_t)F * kMaxHyps));
   chk(dalloc(c, &c->d_hyps, (size_t)F * kMaxHyps));
