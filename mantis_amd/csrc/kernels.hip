@@ -3696,8 +3696,11 @@ __device__ inline void op_load(const OpPool& p, int32_t cap, int k, rpp::OpState
 }
 static_assert(12 + 12 + 6 * rpp::NP + 9 + 9 + 3 + 3 + 4 + 3 <= kOpFields, "OpState fields");
 
+#ifndef MK_OP_WPE
+#define MK_OP_WPE 1  // k_objpose_q waves per SIMD the compiler targets (1: up to 512 registers)
+#endif
 template <int MODE>
-__global__ __launch_bounds__(256) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MK_OP_WPE))) void k_objpose_q(RppItem* __restrict__ items, rpp::Refine* __restrict__ rf,
                                                    const int32_t* __restrict__ jobs, RppQueue* q, FrameState* st,
                                                    int paired, OpRound rd) {
   const int lane = threadIdx.x & 63;
