@@ -2582,10 +2582,19 @@ struct BitsTiled {
 // is kept short: the position packed as x | y << 16 (one add moves it; the
 // emitted point is (x - 1, y - 1), as trace_border_lut's px, py), 32-bit byte
 // offsets into the tiled plane (scalar base + vector offset addressing).
+#ifndef MK_WALK_WINDOW
+#define MK_WALK_WINDOW 1  // walk_step keeps a 4-word window of the tiled plane (0: a load per step)
+#endif
+#ifndef MK_WALK_ALU
+#define MK_WALK_ALU 0  // walk_step's next direction computed in registers instead of the LDS table
+#endif
 struct Walk {
   uint32_t pos, spos, p1;  // current, start, and the start's last neighbour
   int s, prev_s, n, steps;
   int first;               // the next step is the segment's first (never a checkpoint stop)
+  // walk_step's window: 4 consecutive words of one (tile, group) column of the
+  // tiled plane, ck = (tile * G + group) << 5 | first word (~0u: none)
+  uint32_t ck, c0, c1, c2, c3;
 };
 __device__ inline uint32_t wpos(int x, int y) { return (uint32_t)x | ((uint32_t)y << 16); }
 __device__ inline uint32_t wdelta(int s) { return (uint32_t)(fdx(s) + (fdy(s) << 16)); }
@@ -2609,6 +2618,7 @@ __device__ inline bool walk_start(const NB& nb, int sx, int sy, bool hole, EM& e
   w.p1 = wpos(sx + fdx(s), sy + fdy(s));
   w.prev_s = s ^ 4;
   w.s = s;
+  w.ck = ~0u;
   return true;
 }
 // ------------------------------------------------ segmented border walks
@@ -2691,6 +2701,7 @@ __device__ inline void seg_begin(const NB& nb, const Border& b, int Wp, uint32_t
   w.n = 0;
   w.steps = 0;
   w.first = 1;
+  w.ck = ~0u;
 }
 // one step of the follower on the tiled plane (BitsTiled layout, wpw32 = 32 *
 // words per row); false once the segment ended: nx = the next segment's
@@ -2699,13 +2710,50 @@ template <class EM>
 __device__ inline bool walk_step(const uint32_t* __restrict__ tb, int G, const uint8_t* lut, EM& em, Walk& w,
                                  int M, const int32_t* r, const uint16_t* X, const int32_t* rowbase, int& nx) {
   const int x = (int)(w.pos & 0xffffu), y = (int)(w.pos >> 16);
+#if MK_WALK_WINDOW
+  // rows y - 1 .. y + 1 are the words (y & 31) .. + 2 of the (tile, group)
+  // column tg. A lane keeps 4 consecutive words of one column: a step that
+  // stays inside them (moves along the 16-pixel group, or one row on in the
+  // direction the window was placed) needs no load. The long segments that
+  // end a frame's walks run with one or two busy lanes per wave, so a step
+  // the window covers costs the lane's LDS lookup instead of an L2 round trip.
+  const uint32_t tg = (uint32_t)((y >> 5) * G + (x >> 4));
+  const int yr = y & 31;
+  int d = yr - (int)(w.ck & 31u);
+  if ((w.ck >> 5) != tg || (unsigned)d > 1u) {
+    // place the window so the next row in the walk's direction is inside it
+    // (words s0 .. s0 + 3 <= 33: inside the column's 34)
+    const int s0 = fdy(w.s ^ 4) < 0 ? max(yr - 1, 0) : min(yr, 30);
+    typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a v = *(const __attribute__((address_space(1))) u32x4a*)((const char*)tb + ((tg * kTbRows + s0) << 2));
+    w.c0 = v.x; w.c1 = v.y; w.c2 = v.z; w.c3 = v.w;
+    w.ck = (tg << 5) | (uint32_t)s0;
+    d = yr - s0;
+  }
+  const uint32_t va = d ? w.c1 : w.c0, vb = d ? w.c2 : w.c1, vc = d ? w.c3 : w.c2;
+  const int sh = (x & 15) + 7;
+#if MK_WALK_ALU
+  // the next direction as build_next_lut computes it, in registers: the 8
+  // neighbours (nb8_from_rows) swept counter-clockwise from w.s + 1
+  const uint32_t up3 = (va >> sh) & 7u, mid3 = (vb >> sh) & 7u, dn3 = (vc >> sh) & 7u;
+  const uint32_t m8 = ((mid3 >> 2) & 1u) | ((up3 & 4u) >> 1) | ((up3 & 2u) << 1) | ((up3 & 1u) << 3) |
+                      ((mid3 & 1u) << 4) | (dn3 << 5);
+  const uint32_t rr = ((m8 | (m8 << 8)) >> (w.s + 1)) & 0xffu;
+  const int s = rr ? (w.s + 1 + (int)__builtin_ctz(rr)) & 7 : 8;
+#else
+  const uint32_t p9 = ((va >> sh) & 7u) | (((vb >> sh) & 7u) << 3) | (((vc >> sh) & 7u) << 6);
+#endif
+#else
   // rows y - 1 .. y + 1 as three consecutive words: one 12-byte load (scalar
   // base + 32-bit byte offset)
   typedef unsigned int u32x3a __attribute__((ext_vector_type(3), aligned(4)));
   const u32x3a v = *(const __attribute__((address_space(1))) u32x3a*)((const char*)tb + (tb_off(x, y, G) << 2));
   const int sh = (x & 15) + 7;
   const uint32_t p9 = ((v.x >> sh) & 7u) | (((v.y >> sh) & 7u) << 3) | (((v.z >> sh) & 7u) << 6);
+#endif
+#if !(MK_WALK_WINDOW && MK_WALK_ALU)
   const int s = lut[(p9 << 3) | w.s];
+#endif
   if (M > 0 && !w.first && y % M == 0) {
     const bool west = arc_has(w.s, s, 4);
     if (west || arc_has(w.s, s, 0)) {

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.txt 2>&1; rc=$?
 tail -3 $O/gpu_tests.txt; [ $rc = 0 ] || exit 1
 for k in 1 2; do
-  MANTIS_AMD_LIB=$R/abvar/base.so timeout -k 10 120 python -u tools/p50_graph_ab.py 96 | sed 's/^/base /' || exit 1
+  MANTIS_AMD_LIB=$R/abvar/old.so timeout -k 10 120 python -u tools/p50_graph_ab.py 96 | sed 's/^/base /' || exit 1
   timeout -k 10 120 python -u tools/p50_graph_ab.py 96 | sed 's/^/fx   /' || exit 1
 done | tee $O/p50_ab.txt
-BSTEPS=8 bash tools/ab_var.sh base=abvar/base.so fx=- base2=abvar/base.so fx2=- | tee $O/ab.txt
+BSTEPS=8 bash tools/ab_var.sh base=abvar/old.so fx=- base2=abvar/old.so fx2=- | tee $O/ab.txt
