@@ -2585,9 +2585,6 @@ struct BitsTiled {
 #ifndef MK_WALK_WINDOW
 #define MK_WALK_WINDOW 1  // walk_step keeps a 4-word window of the tiled plane (0: a load per step)
 #endif
-#ifndef MK_WALK_ALU
-#define MK_WALK_ALU 0  // walk_step's next direction computed in registers instead of the LDS table
-#endif
 struct Walk {
   uint32_t pos, spos, p1;  // current, start, and the start's last neighbour
   int s, prev_s, n, steps;
@@ -2732,17 +2729,7 @@ __device__ inline bool walk_step(const uint32_t* __restrict__ tb, int G, const u
   }
   const uint32_t va = d ? w.c1 : w.c0, vb = d ? w.c2 : w.c1, vc = d ? w.c3 : w.c2;
   const int sh = (x & 15) + 7;
-#if MK_WALK_ALU
-  // the next direction as build_next_lut computes it, in registers: the 8
-  // neighbours (nb8_from_rows) swept counter-clockwise from w.s + 1
-  const uint32_t up3 = (va >> sh) & 7u, mid3 = (vb >> sh) & 7u, dn3 = (vc >> sh) & 7u;
-  const uint32_t m8 = ((mid3 >> 2) & 1u) | ((up3 & 4u) >> 1) | ((up3 & 2u) << 1) | ((up3 & 1u) << 3) |
-                      ((mid3 & 1u) << 4) | (dn3 << 5);
-  const uint32_t rr = ((m8 | (m8 << 8)) >> (w.s + 1)) & 0xffu;
-  const int s = rr ? (w.s + 1 + (int)__builtin_ctz(rr)) & 7 : 8;
-#else
   const uint32_t p9 = ((va >> sh) & 7u) | (((vb >> sh) & 7u) << 3) | (((vc >> sh) & 7u) << 6);
-#endif
 #else
   // rows y - 1 .. y + 1 as three consecutive words: one 12-byte load (scalar
   // base + 32-bit byte offset)
@@ -2751,9 +2738,7 @@ __device__ inline bool walk_step(const uint32_t* __restrict__ tb, int G, const u
   const int sh = (x & 15) + 7;
   const uint32_t p9 = ((v.x >> sh) & 7u) | (((v.y >> sh) & 7u) << 3) | (((v.z >> sh) & 7u) << 6);
 #endif
-#if !(MK_WALK_WINDOW && MK_WALK_ALU)
   const int s = lut[(p9 << 3) | w.s];
-#endif
   if (M > 0 && !w.first && y % M == 0) {
     const bool west = arc_has(w.s, s, 4);
     if (west || arc_has(w.s, s, 0)) {
