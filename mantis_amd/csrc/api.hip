@@ -1823,15 +1823,21 @@ mantis_status mantis_get_contours(void* ctx, int32_t frame, int32_t* counts, int
   size_t total = 0;
   for (int b = 0; b < nb; b++) total += (size_t)cnt[b];
   if (total > (size_t)max_points) { c->err = "mantis_get_contours: max_points too small"; return MANTIS_ERR_CAPACITY; }
-  std::vector<int32_t> pool(2 * (size_t)c->pool_cap);
+  std::vector<int32_t> pool((size_t)c->pool_cap);
   HIP_OK(hipMemcpy(pool.data(), c->d_pool + 2 * (size_t)frame * c->pool_cap, sizeof(int32_t) * pool.size(),
                    hipMemcpyDeviceToHost));
+  // the device pool holds the points packed, x | y << 16 (k_frame_contours)
+  const uint32_t* packed = (const uint32_t*)pool.data();
   size_t k = 0;
   for (int b = 0; b < nb; b++) {
     counts[b] = cnt[b];
     holes[b] = bs[b].hole;
     if ((size_t)off[b] + cnt[b] > (size_t)c->pool_cap) { c->err = "mantis_get_contours: pool overflow"; return MANTIS_ERR_CAPACITY; }
-    std::memcpy(points + 2 * k, pool.data() + 2 * (size_t)off[b], sizeof(int32_t) * 2 * cnt[b]);
+    for (int i = 0; i < cnt[b]; i++) {
+      const uint32_t v = packed[(size_t)off[b] + i];
+      points[2 * (k + i)] = (int32_t)(v & 0xffffu);
+      points[2 * (k + i) + 1] = (int32_t)(v >> 16);
+    }
     k += cnt[b];
   }
   return MANTIS_OK;

@@ -2425,8 +2425,8 @@ __device__ inline void wave_argmax(double& d, int& idx) {
 // approx_poly (mk_contour.h, closed, quad early exit) executed by one wave:
 // the farthest-point scans are lane-parallel reductions; lane 0 owns the DP
 // stack and the output (single-lane memory order), control is wave-uniform.
-__device__ int approx_poly_wave(const int32_t* __restrict__ src, int count, double eps, int32_t* dst, int32_t* stk,
-                                int max_dp) {
+__device__ int approx_poly_wave(const uint32_t* __restrict__ src, int count, double eps, int32_t* dst, int32_t* stk,
+                                int max_dp) {  // src: packed points (PtPacked)
   const int lane = threadIdx.x & 63;
   if (count == 0) return 0;
   eps *= eps;
@@ -2435,14 +2435,15 @@ __device__ int approx_poly_wave(const int32_t* __restrict__ src, int count, doub
   int spx = 0, spy = 0;
   for (int it = 0; it < 3; it++) {
     pos = (pos + rs_s) % count;
-    spx = src[2 * pos];
-    spy = src[2 * pos + 1];
+    spx = PtPacked::x(src[pos]);
+    spy = PtPacked::y(src[pos]);
     double best = 0;
     int bj = 0x7fffffff;
     for (int j = 1 + lane; j < count; j += 64) {
       int q = pos + j;
       if (q >= count) q -= count;
-      const double dx = src[2 * q] - spx, dy = src[2 * q + 1] - spy;
+      const uint32_t v = src[q];
+      const double dx = PtPacked::x(v) - spx, dy = PtPacked::y(v) - spy;
       const double d = dx * dx + dy * dy;
       if (d > best) { best = d; bj = j; }
     }
@@ -2466,11 +2467,11 @@ __device__ int approx_poly_wave(const int32_t* __restrict__ src, int count, doub
     int a0 = 0, a1 = 0;
     if (lane == 0) { a0 = stk[2 * top]; a1 = stk[2 * top + 1]; }
     const int sl_s = __shfl(a0, 0), sl_e = __shfl(a1, 0);
-    const int epx = src[2 * sl_e], epy = src[2 * sl_e + 1];
+    const int epx = PtPacked::x(src[sl_e]), epy = PtPacked::y(src[sl_e]);
     int p0 = sl_s + 1;
     if (p0 >= count) p0 = 0;
-    spx = src[2 * sl_s];
-    spy = src[2 * sl_s + 1];
+    spx = PtPacked::x(src[sl_s]);
+    spy = PtPacked::y(src[sl_s]);
     if (p0 != sl_e) {
       const double dx = epx - spx, dy = epy - spy;
       int L = sl_e - p0;
@@ -2480,7 +2481,8 @@ __device__ int approx_poly_wave(const int32_t* __restrict__ src, int count, doub
       for (int t = lane; t < L; t += 64) {
         int q = p0 + t;
         if (q >= count) q -= count;
-        const double dist = fabs((src[2 * q + 1] - spy) * dx - (src[2 * q] - spx) * dy);
+        const uint32_t v = src[q];
+        const double dist = fabs((PtPacked::y(v) - spy) * dx - (PtPacked::x(v) - spx) * dy);
         if (dist > best) { best = dist; bt = t; }
       }
       wave_argmax(best, bt);
@@ -3197,7 +3199,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
   const Border* bs = borders + (size_t)f * border_cap;
   int32_t* cnt = counts + (size_t)f * border_cap;
   int32_t* off = offs + (size_t)f * border_cap;
-  int32_t* pl = pool + 2 * (size_t)f * pool_cap;
+  uint32_t* pl = (uint32_t*)(pool + 2 * (size_t)f * pool_cap);  // the border points, packed (PtPacked)
   int32_t* sc = scratch + 4 * (size_t)f * pool_cap;
   int nb = st[f].n_borders;
   if (nb > border_cap) nb = border_cap;
@@ -3292,8 +3294,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
 #pragma unroll
       for (int u = 0; u < kCU; u++) o[u] = off[b[u]];
 #pragma unroll
-      for (int u = 0; u < kCU; u++)
-        if (l < cc[u]) *(pt2*)(pl + 2 * ((size_t)o[u] + k[u])) = v[u];
+      for (int u = 0; u < kCU; u++)  // packed x | y << 16 (PtPacked)
+        if (l < cc[u]) pl[(size_t)o[u] + k[u]] = (uint32_t)v[u].x | ((uint32_t)v[u].y << 16);
     }
   }
   __syncthreads();
@@ -3349,7 +3351,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
         const int i = longs[k], o = off[i], c = cnt[i];
         int32_t* dst = sc + 4 * (size_t)o;
         int32_t* stk = dst + 2 * (size_t)c;
-        const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
+        const int m = approx_poly_wave(pl + o, c, eps, dst, stk, 10);
         if (m == 4 && lane == 0) emit_raw(i, dst);
       }
       for (;;) {
@@ -3361,7 +3363,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
           const int i = scan[k + lane], o = off[i], c = cnt[i];
           int32_t* dst = sc + 4 * (size_t)o;
           int32_t* stk = dst + 2 * (size_t)c;
-          const int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
+          const int m = approx_poly(PtPacked{pl + o}, c, eps, true, dst, stk, 10);
           if (m == 4) emit_raw(i, dst);
         }
       }
@@ -3382,7 +3384,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
       }
       int32_t* dst = sc + 4 * (size_t)o;
       int32_t* stk = dst + 2 * (size_t)c;
-      int m = approx_poly(pl + 2 * (size_t)o, c, eps, true, dst, stk, 10);
+      int m = approx_poly(PtPacked{pl + o}, c, eps, true, dst, stk, 10);
       if (m == 4) emit_raw(i, dst);
     }
     __syncthreads();
@@ -3394,7 +3396,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
         const int i = longs[k], o = off[i], c = cnt[i];
         int32_t* dst = sc + 4 * (size_t)o;
         int32_t* stk = dst + 2 * (size_t)c;
-        const int m = approx_poly_wave(pl + 2 * (size_t)o, c, eps, dst, stk, 10);
+        const int m = approx_poly_wave(pl + o, c, eps, dst, stk, 10);
         if (m == 4 && (tid & 63) == 0) emit_raw(i, dst);
       }
     }

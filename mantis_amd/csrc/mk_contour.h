@@ -184,14 +184,46 @@ MK_HD int approx_cleanup(int32_t* dst, int new_count, double eps, bool closed0) 
   return new_count;
 }
 
+// Point sources of approx_poly: x, y int pairs, or (on the device's contour
+// pool) one 32-bit word per point, x | y << 16 (image coordinates < 65536): a
+// point is one load and one register, so a lane's read-ahead holds twice the
+// points in the same registers. `Raw` is what a read-ahead slot keeps.
+struct PtPairs {
+  const int32_t* p;
+  static constexpr int kAhead = 4;
+  struct Raw { int x, y; };
+  MK_HD Raw ld(int i) const { return Raw{p[2 * i], p[2 * i + 1]}; }
+  MK_HD static int x(const Raw& r) { return r.x; }
+  MK_HD static int y(const Raw& r) { return r.y; }
+};
+#ifndef MK_APPROX_AHEAD_PACKED
+#define MK_APPROX_AHEAD_PACKED 8
+#endif
+struct PtPacked {
+  const uint32_t* p;
+  static constexpr int kAhead = MK_APPROX_AHEAD_PACKED;
+  typedef uint32_t Raw;
+  MK_HD Raw ld(int i) const { return p[i]; }
+  MK_HD static int x(Raw r) { return (int)(r & 0xffffu); }
+  MK_HD static int y(Raw r) { return (int)(r >> 16); }
+};
+
 // cv::approxPolyDP (approxPolyDP_<int>, closed or open) on n points `src`
-// (x,y int pairs). dst needs n pairs, stack n slices (2 ints each).
-// Returns the output count.
+// (x,y int pairs, or a point source above). dst needs n pairs, stack n slices
+// (2 ints each). Returns the output count.
 // max_dp > 0: stop once the Douglas-Peucker stage has emitted max_dp points
 // and return max_dp + 1 (the quad detector passes 10: the clean-up removes at
 // most every other point, so 10 or more DP points can never end as 4).
+template <class PS>
+MK_HD int approx_poly(const PS& src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack,
+                      int max_dp = 0);
 MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack,
                       int max_dp = 0) {
+  return approx_poly(PtPairs{src}, count0, eps, closed0, dst, stack, max_dp);
+}
+template <class PS>
+MK_HD int approx_poly(const PS& src, int count0, double eps, bool closed0, int32_t* dst, int32_t* stack,
+                      int max_dp) {
   int count = count0;
   if (count == 0) return 0;
   int top = 0;
@@ -203,8 +235,9 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
   bool le_eps = false;
 #define MK_READ(X, Y, P)            \
   do {                              \
-    X = src[2 * (P)];               \
-    Y = src[2 * (P) + 1];           \
+    const auto r_ = src.ld(P);      \
+    X = PS::x(r_);                  \
+    Y = PS::y(r_);                  \
     if (++(P) >= count) (P) = 0;    \
   } while (0)
 #define MK_PUSH(S, E) \
@@ -214,8 +247,8 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
   eps *= eps;
   if (!is_closed) {
     rs_s = count;
-    epx = src[0]; epy = src[1];
-    spx = src[2 * (count - 1)]; spy = src[2 * (count - 1) + 1];
+    epx = PS::x(src.ld(0)); epy = PS::y(src.ld(0));
+    spx = PS::x(src.ld(count - 1)); spy = PS::y(src.ld(count - 1));
     if (spx != epx || spy != epy) {
       sl_s = 0;
       sl_e = count - 1;
@@ -230,10 +263,7 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
   // trip per group instead of per point on the device, where one lane walks a
   // border and each read is an L2 trip. Same points, same order, same
   // arithmetic as cv::approxPolyDP's scans.
-#ifndef MK_APPROX_AHEAD
-#define MK_APPROX_AHEAD 4
-#endif
-  constexpr int kApproxAhead = MK_APPROX_AHEAD;
+  constexpr int kApproxAhead = PS::kAhead;
   if (is_closed) {
     rs_s = 0;
     for (i = 0; i < init_iters; i++) {
@@ -241,27 +271,26 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       pos = (pos + rs_s) % count;
       MK_READ(spx, spy, pos);
       for (j = 1; j < count; j += kApproxAhead) {
-        int gx[kApproxAhead], gy[kApproxAhead];
+        typename PS::Raw g[kApproxAhead];
         int p = pos;
         for (int k = 0; k < kApproxAhead; k++) {  // wrapped indices stay inside the border
-          gx[k] = src[2 * p];
-          gy[k] = src[2 * p + 1];
+          g[k] = src.ld(p);
           if (++p >= count) p = 0;
         }
         const int nk = count - j < kApproxAhead ? count - j : kApproxAhead;
         for (int k = 0; k < kApproxAhead; k++) {
           if (k >= nk) break;
           double dx, dy;
-          dx = gx[k] - spx;
-          dy = gy[k] - spy;
+          dx = PS::x(g[k]) - spx;
+          dy = PS::y(g[k]) - spy;
           dist = dx * dx + dy * dy;
           if (dist > max_dist) {
             max_dist = dist;
             rs_s = j + k;
           }
         }
-        ptx = gx[nk - 1];
-        pty = gy[nk - 1];
+        ptx = PS::x(g[nk - 1]);
+        pty = PS::y(g[nk - 1]);
         pos += nk;
         if (pos >= count) pos -= count;
       }
@@ -280,7 +309,10 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
     top--;
     sl_s = stack[2 * top];
     sl_e = stack[2 * top + 1];
-    epx = src[2 * sl_e]; epy = src[2 * sl_e + 1];
+    {
+      const auto e_ = src.ld(sl_e);
+      epx = PS::x(e_); epy = PS::y(e_);
+    }
     pos = sl_s;
     MK_READ(spx, spy, pos);
     if (pos != sl_e) {
@@ -290,18 +322,17 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       int left = sl_e - pos;  // reads until pos reaches sl_e
       if (left < 0) left += count;
       while (left > 0) {
-        int gx[kApproxAhead], gy[kApproxAhead];
+        typename PS::Raw g[kApproxAhead];
         int p = pos;
         for (int k = 0; k < kApproxAhead; k++) {
-          gx[k] = src[2 * p];
-          gy[k] = src[2 * p + 1];
+          g[k] = src.ld(p);
           if (++p >= count) p = 0;
         }
         const int nk = left < kApproxAhead ? left : kApproxAhead;
         for (int k = 0; k < kApproxAhead; k++) {
           if (k >= nk) break;
-          ptx = gx[k];
-          pty = gy[k];
+          ptx = PS::x(g[k]);
+          pty = PS::y(g[k]);
           if (++pos >= count) pos = 0;
           dist = fabs((pty - spy) * dx - (ptx - spx) * dy);
           if (dist > max_dist) {
@@ -314,7 +345,8 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       le_eps = max_dist * max_dist <= eps * (dx * dx + dy * dy);
     } else {
       le_eps = true;
-      spx = src[2 * sl_s]; spy = src[2 * sl_s + 1];
+      const auto s_ = src.ld(sl_s);
+      spx = PS::x(s_); spy = PS::y(s_);
     }
     if (le_eps) {
       dst[2 * new_count] = spx; dst[2 * new_count + 1] = spy; new_count++;
@@ -326,7 +358,10 @@ MK_HD int approx_poly(const int32_t* src, int count0, double eps, bool closed0, 
       MK_PUSH(sl_s, sl_e);
     }
   }
-  if (!is_closed) { dst[2 * new_count] = src[2 * (count - 1)]; dst[2 * new_count + 1] = src[2 * (count - 1) + 1]; new_count++; }
+  if (!is_closed) {
+    const auto l_ = src.ld(count - 1);
+    dst[2 * new_count] = PS::x(l_); dst[2 * new_count + 1] = PS::y(l_); new_count++;
+  }
 #undef MK_READ
 #undef MK_PUSH
   return approx_cleanup(dst, new_count, eps, closed0);
