@@ -2345,7 +2345,7 @@ constexpr int kChunk = 16;
 // owner's point list (owner = border; during segmented walks the segment,
 // k_seg_chain then adds the segment's offset in its border and maps the owner).
 struct ChunkEmit {
-  int32_t* chunks;  // [chunk][64][2]
+  int32_t* chunks;  // [chunk][kChunk] packed points (x | y << 16)
   int32_t* owner;   // border (or segment) of each chunk
   int32_t* ordv;    // first point position of the chunk within its owner
   int32_t* ccount;  // points in the chunk
@@ -2358,20 +2358,21 @@ struct ChunkEmit {
   // stored at once: a chunk's 128-B line gets two full-width writes instead
   // of sixteen 8-byte ones spread over the walk (a selected slot per point:
   // the index is per lane)
-#if MK_CHUNK_BUF == 2  // packed (x + 1) | (y + 1) << 16: one register per point
+#if MK_CHUNK_BUF == 2  // packed x | y << 16 (points are image coordinates >= 0): one register per point
   uint32_t bp[8];
-  __device__ int bxv(int j) const { return (int)(bp[j] & 0xffffu) - 1; }
-  __device__ int byv(int j) const { return (int)(bp[j] >> 16) - 1; }
+  __device__ uint32_t pk(int j) const { return bp[j]; }
 #else
   int bx[8], by[8];
-  __device__ int bxv(int j) const { return bx[j]; }
-  __device__ int byv(int j) const { return by[j]; }
+  __device__ uint32_t pk(int j) const { return (uint32_t)bx[j] | ((uint32_t)by[j] << 16); }
 #endif
+  // chunk points packed x | y << 16 (PtPacked, what the contour pool holds):
+  // a half chunk is two 16-byte stores
   __device__ void store8(int k0) {
-    typedef int i32x4 __attribute__((ext_vector_type(4)));
-    i32x4* d = (i32x4*)(chunks + 2 * ((size_t)cur * kChunk + k0));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* d = (u32x4*)((uint32_t*)chunks + ((size_t)cur * kChunk + k0));
 #pragma unroll
-    for (int j = 0; j < 4; j++) d[j] = i32x4{bxv(2 * j), byv(2 * j), bxv(2 * j + 1), byv(2 * j + 1)};
+    for (int j = 0; j < 2; j++)
+      d[j] = u32x4{pk(4 * j), pk(4 * j + 1), pk(4 * j + 2), pk(4 * j + 3)};
   }
 #endif
   __device__ void operator()(int px, int py) {
@@ -2390,7 +2391,7 @@ struct ChunkEmit {
 #pragma unroll
     for (int j = 0; j < 8; j++) {
 #if MK_CHUNK_BUF == 2
-      bp[j] = j == i ? (uint32_t)(px + 1) | ((uint32_t)(py + 1) << 16) : bp[j];
+      bp[j] = j == i ? (uint32_t)px | ((uint32_t)py << 16) : bp[j];
 #else
       bx[j] = j == i ? px : bx[j];
       by[j] = j == i ? py : by[j];
@@ -2399,7 +2400,7 @@ struct ChunkEmit {
     k++;
     if ((k & 7) == 0) store8(k - 8);
 #else
-    *(int2*)(chunks + 2 * ((size_t)cur * kChunk + k)) = make_int2(px, py);  // one 8-byte store
+    ((uint32_t*)chunks)[(size_t)cur * kChunk + k] = (uint32_t)px | ((uint32_t)py << 16);  // one 4-byte store
     k++;
 #endif
   }
@@ -3279,23 +3280,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
     const int32_t* ccount = ordv + max_chunks;
     const int l = lane % kChunk;
-    typedef __attribute__((aligned(8))) int2 pt2;
+    const uint32_t* ch = (const uint32_t*)chunks;  // packed points (ChunkEmit)
     for (int c0 = wave * CPW * kCU; c0 < nchunk; c0 += nwaves * CPW * kCU) {
       int cc[kCU], b[kCU], k[kCU], o[kCU];
-      pt2 v[kCU];
+      uint32_t v[kCU];
 #pragma unroll
       for (int u = 0; u < kCU; u++) {
         const int c = min(c0 + u * CPW + lane / kChunk, nchunk - 1);
         cc[u] = c0 + u * CPW + lane / kChunk < nchunk ? ccount[c] : 0;
         b[u] = owner[c];
         k[u] = ordv[c] + l;
-        v[u] = *(const pt2*)(chunks + 2 * ((size_t)c * kChunk + l));
+        v[u] = ch[(size_t)c * kChunk + l];
       }
 #pragma unroll
       for (int u = 0; u < kCU; u++) o[u] = off[b[u]];
 #pragma unroll
       for (int u = 0; u < kCU; u++)  // packed x | y << 16 (PtPacked)
-        if (l < cc[u]) pl[(size_t)o[u] + k[u]] = (uint32_t)v[u].x | ((uint32_t)v[u].y << 16);
+        if (l < cc[u]) pl[(size_t)o[u] + k[u]] = v[u];
     }
   }
   __syncthreads();
