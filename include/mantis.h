@@ -52,7 +52,7 @@ typedef struct mantis_config {
   int32_t struct_size;          /* sizeof(mantis_config) */
   int32_t device;               /* HIP device ordinal */
   int32_t max_cams;             /* camera-frames per mantis_process_batch call */
-  int32_t max_width, max_height;
+  int32_t max_width, max_height; /* width <= 8190, height <= 65533, width x height < 2^25 (else MANTIS_ERR_ARG) */
   uint64_t rng_seed;            /* cv::RNG seed, 1 in the reference (Mantis3Params.h:87) */
   int32_t canny_low;            /* ~canny_hysteresis, 50 (Mantis3Params.h:162); high = 3x */
   int32_t polygon_epsilon;      /* ~polygon_epsilon, 10 (:164) */

@@ -1096,6 +1096,10 @@ mantis_status mantis_create(const mantis_config* cfg_in, void** out_ctx) {
     g_create_err = "max_width: at most 8190 (the hysteresis bands hold a row's worst-case runs in LDS)";
     return MANTIS_ERR_ARG;
   }
+  if (cfg.max_height > 65533) {
+    g_create_err = "max_height: at most 65533 (border walks and contour points pack y + 1 in 16 bits)";
+    return MANTIS_ERR_ARG;
+  }
   if ((int64_t)((cfg.max_height + HB_ROWS - 1) / HB_ROWS) * HB_ROWS * ((cfg.max_width + 1) / 2) >= (1 << 24)) {
     g_create_err = "max_width x max_height: at most 2^25 pixels (hysteresis run ids and their band row share a word)";
     return MANTIS_ERR_ARG;

@@ -129,3 +129,17 @@ def test_create_rejects_oversized_frames():
     st = M.lib().mantis_create(C.byref(cfg), C.byref(h))
     assert st == 1 and not h.value  # MANTIS_ERR_ARG
     assert b"2^25" in M.lib().mantis_last_error(None)
+
+
+def test_create_rejects_tall_frames():
+    """Border walks (Walk.pos) and the contour pool (PtPacked) pack a padded
+    row index in 16 bits: heights past 65533 are refused at creation (before
+    any device call)."""
+    import mantis_amd as M
+
+    cfg = M.default_config()
+    cfg.max_width, cfg.max_height = 16, 70000  # 1.1 M pixels: inside the 2^25 bound
+    h = C.c_void_p()
+    st = M.lib().mantis_create(C.byref(cfg), C.byref(h))
+    assert st == 1 and not h.value  # MANTIS_ERR_ARG
+    assert b"65533" in M.lib().mantis_last_error(None)
