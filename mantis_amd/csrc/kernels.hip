@@ -3163,8 +3163,11 @@ __global__ __launch_bounds__(1024) void k_trace_borders_lds(const uint32_t* __re
   }
 }
 
+#ifndef MK_FC_CPL
+#define MK_FC_CPL 2  // compaction points per lane (k_frame_contours step 3)
+#endif
 #ifndef MK_FC_CU
-#define MK_FC_CU 4  // compaction trips in flight per wave (k_frame_contours step 3)
+#define MK_FC_CU 8  // compaction trips in flight per wave (k_frame_contours step 3)
 #endif
 // 5 waves per SIMD (96 VGPRs, 32 B of spills) rather than the 106 VGPRs / 4
 // waves the 1024-thread bound allows: in throughput mode (256-thread blocks)
@@ -3270,33 +3273,44 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     return;
   }
   MK_TICK(0);  // scan
-  // 3. compact: 64 / kChunk chunks per wave, one lane per point, kCU wave
-  // trips at once: every load of the kCU trips is issued (at a clamped, valid
-  // chunk) before any is used, so a trip's chain (chunk count / owner / order,
-  // then the border's offset, then the store) costs one round trip per kCU
-  // trips instead of per trip
+  // 3. compact: kCPL points per lane (one 4- or 8-byte load of the packed
+  // chunk), 64 kCPL / kChunk chunks per wave, kCU wave trips at once: every
+  // load of the kCU trips is issued (at a clamped, valid chunk) before any is
+  // used, so a trip's chain (chunk count / owner / order, then the border's
+  // offset, then the stores) costs one round trip per kCU trips instead of per
+  // trip
   if (nchunk > 0) {
-    constexpr int CPW = 64 / kChunk, kCU = MK_FC_CU;
+    constexpr int kCPL = MK_FC_CPL, LPC = kChunk / kCPL, CPW = 64 / LPC, kCU = MK_FC_CU;
+    static_assert(kCPL == 1 || kCPL == 2, "points per lane");
     const int wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
     const int32_t* ccount = ordv + max_chunks;
-    const int l = lane % kChunk;
+    const int l = (lane % LPC) * kCPL;  // the lane's first point in its chunk
     const uint32_t* ch = (const uint32_t*)chunks;  // packed points (ChunkEmit)
+    typedef __attribute__((aligned(8))) uint2 u2a;
     for (int c0 = wave * CPW * kCU; c0 < nchunk; c0 += nwaves * CPW * kCU) {
       int cc[kCU], b[kCU], k[kCU], o[kCU];
-      uint32_t v[kCU];
+      uint32_t v[kCU][kCPL];
 #pragma unroll
       for (int u = 0; u < kCU; u++) {
-        const int c = min(c0 + u * CPW + lane / kChunk, nchunk - 1);
-        cc[u] = c0 + u * CPW + lane / kChunk < nchunk ? ccount[c] : 0;
+        const int c = min(c0 + u * CPW + lane / LPC, nchunk - 1);
+        cc[u] = c0 + u * CPW + lane / LPC < nchunk ? ccount[c] : 0;
         b[u] = owner[c];
         k[u] = ordv[c] + l;
-        v[u] = ch[(size_t)c * kChunk + l];
+        if (kCPL == 2) {
+          const uint2 w = *(const u2a*)(ch + (size_t)c * kChunk + l);
+          v[u][0] = w.x;
+          v[u][kCPL - 1] = w.y;
+        } else {
+          v[u][0] = ch[(size_t)c * kChunk + l];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kCU; u++) o[u] = off[b[u]];
 #pragma unroll
       for (int u = 0; u < kCU; u++)  // packed x | y << 16 (PtPacked)
-        if (l < cc[u]) pl[(size_t)o[u] + k[u]] = v[u];
+#pragma unroll
+        for (int e = 0; e < kCPL; e++)
+          if (l + e < cc[u]) pl[(size_t)o[u] + k[u] + e] = v[u][e];
     }
   }
   __syncthreads();
