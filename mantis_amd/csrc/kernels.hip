@@ -3369,6 +3369,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
         const int m = approx_poly_wave(pl + o, c, eps, dst, stk, 10);
         if (m == 4 && lane == 0) emit_raw(i, dst);
       }
+#ifdef MK_FC_TICK_SPLIT  // diagnostics (tools/fc_ticks.py): tick 2 = the long borders' end, tick 3 = the short ones'
+      MK_TICK(2);
+#endif
       for (;;) {
         int k = 0;
         if (lane == 0) k = atomicAdd(&next_short, 64);
@@ -3383,7 +3386,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
         }
       }
       __syncthreads();
+#ifdef MK_FC_TICK_SPLIT
+      MK_TICK(3);
+#else
       MK_TICK(2);  // approx (sorted)
+#endif
     } else {
       __syncthreads();
       if (tid == 0) nlong = 0;
@@ -3417,7 +3424,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
     }
   }
   __syncthreads();
+#ifndef MK_FC_TICK_SPLIT
   MK_TICK(3);  // long-border approx (waves)
+#endif
   const int nq = nraw < kMaxQuads ? nraw : kMaxQuads;
   // position in the CCOMP output order (keys are distinct)
   for (int i = tid; i < nq; i += blockDim.x) {
