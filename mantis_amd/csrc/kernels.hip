@@ -2426,8 +2426,18 @@ __device__ inline void wave_argmax(double& d, int& idx) {
 // approx_poly (mk_contour.h, closed, quad early exit) executed by one wave:
 // the farthest-point scans are lane-parallel reductions; lane 0 owns the DP
 // stack and the output (single-lane memory order), control is wave-uniform.
-__device__ int approx_poly_wave(const uint32_t* __restrict__ src, int count, double eps, int32_t* dst, int32_t* stk,
-                                int max_dp) {  // src: packed points (PtPacked)
+// STK: the DP stack's storage -- global scratch (int32_t*, as many slices as
+// points) or a wave's LDS slice of `cap` slices (lds_i32*): a push past cap
+// returns -1 and the caller runs the border again on the global stack (the DP
+// is deterministic, dst is rewritten)
+typedef __attribute__((address_space(3))) int32_t lds_i32;
+#ifndef MK_WAVE_STK
+#define MK_WAVE_STK 14  // 16 waves x 14 slices x 8 B: k_frame_contours stays under 32 KB of LDS (5 blocks per CU)
+#endif
+constexpr int kWaveStk = MK_WAVE_STK;  // DP stack slices per wave in LDS
+template <class STK>
+__device__ int approx_poly_wave(const uint32_t* __restrict__ src, int count, double eps, int32_t* dst, STK stk,
+                                int max_dp, int cap = 0x7fffffff) {  // src: packed points (PtPacked)
   const int lane = threadIdx.x & 63;
   if (count == 0) return 0;
   eps *= eps;
@@ -2497,6 +2507,7 @@ __device__ int approx_poly_wave(const uint32_t* __restrict__ src, int count, dou
       nc++;
       if (max_dp > 0 && nc >= max_dp) return max_dp + 1;
     } else {
+      if (top + 2 > cap) return -1;  // wave-uniform
       if (lane == 0) {
         stk[2 * top] = rs_s; stk[2 * top + 1] = sl_e;      // PUSH(rs_s, rs_e = sl_e)
         stk[2 * top + 2] = sl_s; stk[2 * top + 3] = rs_s;  // PUSH(sl_s, sl_e = rs_s)
@@ -3325,6 +3336,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
   // counters. The result does not depend on the order: emit_raw's slots are
   // re-ordered by CCOMP key below.
   __shared__ int32_t hist[33], nshort, next_long, next_short;
+  __shared__ int32_t wstk[16][2 * kWaveStk];  // each wave's DP stack for the long borders
   if (tid < 33) hist[tid] = 0;
   if (tid == 0) { next_long = 0; next_short = 0; }
   __syncthreads();
@@ -3366,7 +3378,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(MK_FC_WPE)
         const int i = longs[k], o = off[i], c = cnt[i];
         int32_t* dst = sc + 4 * (size_t)o;
         int32_t* stk = dst + 2 * (size_t)c;
-        const int m = approx_poly_wave(pl + o, c, eps, dst, stk, 10);
+        // the DP stack in the wave's LDS slice (one L2 round trip less per DP
+        // step); a deeper stack runs the border again on the global one
+        int m = approx_poly_wave(pl + o, c, eps, dst, (lds_i32*)wstk[tid >> 6], 10, kWaveStk);
+        if (m < 0) m = approx_poly_wave(pl + o, c, eps, dst, stk, 10);
         if (m == 4 && lane == 0) emit_raw(i, dst);
       }
 #ifdef MK_FC_TICK_SPLIT  // diagnostics (tools/fc_ticks.py): tick 2 = the long borders' end, tick 3 = the short ones'
