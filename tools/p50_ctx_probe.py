@@ -22,7 +22,8 @@ def main(max_cams, extra, calls):
     import mantis_amd as M
     from mantis_amd import synth
 
-    W, H, CAMS, ND = 1280, 720, 4, 16
+    W, H, CAMS = 1280, 720, 4
+    ND = int(os.environ.get("P50_RIGS", "16"))
     K, D = synth.intrinsics(W, H)
     rng = np.random.default_rng(1000)
     ext = synth.rig_extrinsics(CAMS)
